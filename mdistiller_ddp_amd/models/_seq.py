@@ -1,0 +1,54 @@
+"""Run ``nn.Sequential`` conv chains through the fused conv+BN+act op.
+
+The reference builds VGG / MobileNet blocks as ``nn.Sequential`` lists of
+``Conv2d, BatchNorm2d, ReLU`` (so their ``state_dict`` keys are positional,
+e.g. ``block0.1.running_mean``).  Keeping those containers preserves checkpoint
+compatibility; this helper walks them and groups each ``Conv2d[, BN][, act]``
+run into a single fused launch.
+"""
+from __future__ import annotations
+
+import torch.nn as nn
+
+from ..ops.nn import conv_bn_act, bn_act
+
+
+def _act_of(m):
+    if isinstance(m, nn.ReLU6):
+        return "relu6"
+    if isinstance(m, nn.ReLU):
+        return "relu"
+    return None
+
+
+def run_seq(seq, x, residual=None, want_preact=False):
+    """Returns ``(out, preact_of_last_group_or_None)``.
+
+    ``residual`` is added after the last group's BN, before its activation.
+    """
+    mods = list(seq)
+    i, pre = 0, None
+    n = len(mods)
+    while i < n:
+        m = mods[i]
+        if isinstance(m, nn.Conv2d):
+            bn, act, j = None, "none", i + 1
+            if j < n and isinstance(mods[j], nn.BatchNorm2d):
+                bn, j = mods[j], j + 1
+            if j < n and _act_of(mods[j]) is not None:
+                act, j = _act_of(mods[j]), j + 1
+            last = j >= n
+            x, pre = conv_bn_act(x, m, bn, act, residual if last else None, want_preact and last)
+            i = j
+        elif isinstance(m, nn.BatchNorm2d):
+            act, j = "none", i + 1
+            if j < n and _act_of(mods[j]) is not None:
+                act, j = _act_of(mods[j]), j + 1
+            last = j >= n
+            x, pre = bn_act(x, m, act, residual if last else None, want_preact and last)
+            i = j
+        else:
+            x = m(x)
+            pre = x
+            i += 1
+    return x, pre

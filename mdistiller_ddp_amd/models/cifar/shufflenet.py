@@ -1,0 +1,252 @@
+"""CIFAR ShuffleNet V1 (g=3) and V2 (1x).
+
+Layouts follow `mdistiller/models/cifar/ShuffleNetv1.py:7-169` and
+`ShuffleNetv2.py:7-233`.  ShuffleV2's head uses a global average pool instead
+of ``avg_pool2d(out, 4)``: identical on 32x32 inputs (4x4 map) and correct on
+64x64 Tiny-ImageNet inputs, where the reference produces 4096 features for a
+1024-wide classifier.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ...ops.nn import conv_bn_act, channel_shuffle
+from .._base import ModelBase, PreactStage
+from .resnet import Stage
+
+
+class ShuffleBlock(nn.Module):
+    def __init__(self, groups=2):
+        super().__init__()
+        self.groups = groups
+
+    def forward(self, x):
+        return channel_shuffle(x, self.groups)
+
+
+# ----------------------------------------------------------------------------- V1
+class BottleneckV1(nn.Module):
+    def __init__(self, in_planes, out_planes, stride, groups, is_last=False):
+        super().__init__()
+        self.is_last = is_last
+        self._need_preact = True
+        self.stride = stride
+        mid = int(out_planes / 4)
+        g = 1 if in_planes == 24 else groups
+        self.conv1 = nn.Conv2d(in_planes, mid, 1, groups=g, bias=False)
+        self.bn1 = nn.BatchNorm2d(mid)
+        self.shuffle1 = ShuffleBlock(groups=g)
+        self.conv2 = nn.Conv2d(mid, mid, 3, stride, 1, groups=mid, bias=False)
+        self.bn2 = nn.BatchNorm2d(mid)
+        self.conv3 = nn.Conv2d(mid, out_planes, 1, groups=groups, bias=False)
+        self.bn3 = nn.BatchNorm2d(out_planes)
+        self.shortcut = nn.Sequential()
+        if stride == 2:
+            self.shortcut = nn.Sequential(nn.AvgPool2d(3, stride=2, padding=1))
+
+    def forward(self, x):
+        out, _ = conv_bn_act(x, self.conv1, self.bn1, "relu")
+        out = self.shuffle1(out)
+        out, _ = conv_bn_act(out, self.conv2, self.bn2, "relu")
+        if self.stride == 2:
+            out, _ = conv_bn_act(out, self.conv3, self.bn3, "none")
+            preact = torch.cat([out, self.shortcut(x)], 1)
+            return F.relu(preact), preact
+        return conv_bn_act(out, self.conv3, self.bn3, "relu", residual=x, want_preact=True)
+
+
+class ShuffleNet(nn.Module, ModelBase):
+    def __init__(self, cfg, num_classes=10):
+        super().__init__()
+        out_planes, num_blocks, groups = cfg["out_planes"], cfg["num_blocks"], cfg["groups"]
+        self.conv1 = nn.Conv2d(3, 24, kernel_size=1, bias=False)
+        self.bn1 = nn.BatchNorm2d(24)
+        self.in_planes = 24
+        self.layer1 = self._make_layer(out_planes[0], num_blocks[0], groups)
+        self.layer2 = self._make_layer(out_planes[1], num_blocks[1], groups)
+        self.layer3 = self._make_layer(out_planes[2], num_blocks[2], groups)
+        self.linear = nn.Linear(out_planes[2], num_classes)
+        self.stage_channels = [24] + list(out_planes)
+
+    def _make_layer(self, out_planes, num_blocks, groups):
+        layers = []
+        for i in range(num_blocks):
+            stride = 2 if i == 0 else 1
+            cat_planes = self.in_planes if i == 0 else 0
+            layers.append(BottleneckV1(self.in_planes, out_planes - cat_planes, stride, groups,
+                                       is_last=(i == num_blocks - 1)))
+            self.in_planes = out_planes
+        return Stage(*layers)
+
+    def get_bn_before_relu(self):
+        raise NotImplementedError('ShuffleNet is not supported as an "Overhaul" (OFD) teacher')
+
+    def forward_stem(self, x):
+        return self.bn1(self.conv1(x))
+
+    def get_layers(self):
+        return nn.Sequential(PreactStage(self.layer1), PreactStage(self.layer2), PreactStage(self.layer3))
+
+    def forward_pool(self, x):
+        out = F.adaptive_avg_pool2d(F.relu(x), 1)
+        return out.reshape(out.size(0), -1)
+
+    def get_head(self):
+        return self.linear
+
+    def forward(self, x):
+        out, f0_pre = conv_bn_act(x, self.conv1, self.bn1, "relu", want_preact=True)
+        f0 = out
+        out, f1_pre = self.layer1(out)
+        f1 = out
+        out, f2_pre = self.layer2(out)
+        f2 = out
+        out, f3_pre = self.layer3(out)
+        f3 = out
+        avg = F.adaptive_avg_pool2d(out, 1).reshape(out.size(0), -1)
+        return self.linear(avg), {"feats": [f0, f1, f2, f3],
+                                  "preact_feats": [f0_pre, f1_pre, f2_pre, f3_pre],
+                                  "pooled_feat": avg}
+
+
+def ShuffleV1(**kw):
+    return ShuffleNet({"out_planes": [240, 480, 960], "num_blocks": [4, 8, 4], "groups": 3}, **kw)
+
+
+# ----------------------------------------------------------------------------- V2
+class SplitBlock(nn.Module):
+    def __init__(self, ratio):
+        super().__init__()
+        self.ratio = ratio
+
+    def forward(self, x):
+        c = int(x.size(1) * self.ratio)
+        return x[:, :c, :, :], x[:, c:, :, :]
+
+
+class BasicBlockV2(nn.Module):
+    def __init__(self, in_channels, split_ratio=0.5, is_last=False):
+        super().__init__()
+        self.is_last = is_last
+        self.split = SplitBlock(split_ratio)
+        c = int(in_channels * split_ratio)
+        self.conv1 = nn.Conv2d(c, c, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(c)
+        self.conv2 = nn.Conv2d(c, c, 3, 1, 1, groups=c, bias=False)
+        self.bn2 = nn.BatchNorm2d(c)
+        self.conv3 = nn.Conv2d(c, c, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(c)
+        self.shuffle = ShuffleBlock()
+
+    def forward(self, x):
+        x1, x2 = self.split(x)
+        out, _ = conv_bn_act(x2, self.conv1, self.bn1, "relu")
+        out, _ = conv_bn_act(out, self.conv2, self.bn2, "none")
+        out, pre = conv_bn_act(out, self.conv3, self.bn3, "relu", want_preact=True)
+        # preact is returned in the same (shuffled) channel order as ``out`` so that
+        # feats == relu(preact_feats) holds for the staged API
+        preact = self.shuffle(torch.cat([x1, pre], 1))
+        out = self.shuffle(torch.cat([x1, out], 1))
+        return out, preact
+
+
+class DownBlock(nn.Module):
+    def __init__(self, in_channels, out_channels):
+        super().__init__()
+        mid = out_channels // 2
+        self.conv1 = nn.Conv2d(in_channels, in_channels, 3, 2, 1, groups=in_channels, bias=False)
+        self.bn1 = nn.BatchNorm2d(in_channels)
+        self.conv2 = nn.Conv2d(in_channels, mid, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(mid)
+        self.conv3 = nn.Conv2d(in_channels, mid, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(mid)
+        self.conv4 = nn.Conv2d(mid, mid, 3, 2, 1, groups=mid, bias=False)
+        self.bn4 = nn.BatchNorm2d(mid)
+        self.conv5 = nn.Conv2d(mid, mid, 1, bias=False)
+        self.bn5 = nn.BatchNorm2d(mid)
+        self.shuffle = ShuffleBlock()
+
+    def forward(self, x):
+        o1, _ = conv_bn_act(x, self.conv1, self.bn1, "none")
+        o1, _ = conv_bn_act(o1, self.conv2, self.bn2, "relu")
+        o2, _ = conv_bn_act(x, self.conv3, self.bn3, "relu")
+        o2, _ = conv_bn_act(o2, self.conv4, self.bn4, "none")
+        o2, _ = conv_bn_act(o2, self.conv5, self.bn5, "relu")
+        out = self.shuffle(torch.cat([o1, o2], 1))
+        return out, out
+
+
+configs_v2 = {
+    0.2: {"out_channels": (40, 80, 160, 512), "num_blocks": (3, 3, 3)},
+    0.3: {"out_channels": (40, 80, 160, 512), "num_blocks": (3, 7, 3)},
+    0.5: {"out_channels": (48, 96, 192, 1024), "num_blocks": (3, 7, 3)},
+    1: {"out_channels": (116, 232, 464, 1024), "num_blocks": (3, 7, 3)},
+    1.5: {"out_channels": (176, 352, 704, 1024), "num_blocks": (3, 7, 3)},
+    2: {"out_channels": (224, 488, 976, 2048), "num_blocks": (3, 7, 3)},
+}
+
+
+class ShuffleNetV2(nn.Module, ModelBase):
+    def __init__(self, net_size, num_classes=10):
+        super().__init__()
+        out_channels = configs_v2[net_size]["out_channels"]
+        num_blocks = configs_v2[net_size]["num_blocks"]
+        self.conv1 = nn.Conv2d(3, 24, kernel_size=1, bias=False)
+        self.bn1 = nn.BatchNorm2d(24)
+        self.in_channels = 24
+        self.layer1 = self._make_layer(out_channels[0], num_blocks[0])
+        self.layer2 = self._make_layer(out_channels[1], num_blocks[1])
+        self.layer3 = self._make_layer(out_channels[2], num_blocks[2])
+        self.conv2 = nn.Conv2d(out_channels[2], out_channels[3], 1, 1, 0, bias=False)
+        self.bn2 = nn.BatchNorm2d(out_channels[3])
+        self.linear = nn.Linear(out_channels[3], num_classes)
+        self.stage_channels = out_channels
+
+    def _make_layer(self, out_channels, num_blocks):
+        layers = [DownBlock(self.in_channels, out_channels)]
+        for i in range(num_blocks):
+            layers.append(BasicBlockV2(out_channels, is_last=(i == num_blocks - 1)))
+            self.in_channels = out_channels
+        return Stage(*layers)
+
+    def get_bn_before_relu(self):
+        raise NotImplementedError('ShuffleNetV2 is not supported as an "Overhaul" (OFD) teacher')
+
+    def get_stage_channels(self):
+        return [24] + list(self.stage_channels[:-1])
+
+    def forward_stem(self, x):
+        return self.bn1(self.conv1(x))
+
+    def get_layers(self):
+        return nn.Sequential(PreactStage(self.layer1), PreactStage(self.layer2), PreactStage(self.layer3))
+
+    def _head(self, out):
+        out, _ = conv_bn_act(out, self.conv2, self.bn2, "relu")
+        return F.adaptive_avg_pool2d(out, 1).reshape(out.size(0), -1)
+
+    def forward_pool(self, x):
+        return self._head(F.relu(x))
+
+    def get_head(self):
+        return self.linear
+
+    def forward(self, x):
+        out, f0_pre = conv_bn_act(x, self.conv1, self.bn1, "relu", want_preact=True)
+        f0 = out
+        out, f1_pre = self.layer1(out)
+        f1 = out
+        out, f2_pre = self.layer2(out)
+        f2 = out
+        out, f3_pre = self.layer3(out)
+        f3 = out
+        avg = self._head(out)
+        return self.linear(avg), {"feats": [f0, f1, f2, f3],
+                                  "preact_feats": [f0_pre, f1_pre, f2_pre, f3_pre],
+                                  "pooled_feat": avg}
+
+
+def ShuffleV2(**kw):
+    return ShuffleNetV2(net_size=1, **kw)

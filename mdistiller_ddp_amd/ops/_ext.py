@@ -1,0 +1,148 @@
+"""ctypes bindings for the native libraries built by :mod:`.build`.
+
+Every device launcher exported by ``libmda_hip.so`` has a plain C ABI:
+``int mda_<name>(<pointers/ints/floats>..., hipStream_t stream)`` returning a
+``hipError_t``.  Signatures are declared once in :data:`SIGNATURES` with a
+compact code per argument:
+
+``p`` device/host pointer (a ``torch.Tensor`` is converted via ``data_ptr()``),
+``i`` int64, ``f`` float32, ``s`` stream (defaults to the current torch stream).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+from . import build as _build
+
+_lock = threading.Lock()
+_LIBS: dict = {}
+_FAILED: dict = {}
+LOADED_PATHS: list = []
+
+_CT = {"p": ctypes.c_void_p, "i": ctypes.c_int64, "f": ctypes.c_float, "s": ctypes.c_void_p,
+       "d": ctypes.c_double}
+
+# name -> argument codes (stream last).  Kept in sync with csrc/*.hip `extern "C"` launchers.
+SIGNATURES = {
+    # losses (csrc/losses.hip)
+    "mda_ce_kd_fwd_bwd": "pppppiiffffffs",
+    "mda_dkd_fwd_bwd": "pppppiifffffffs",
+    "mda_loss_finalize": "ppiis",
+    "mda_at_loss_fwd": "pppiiifs",
+    # elementwise / BN (csrc/bn.hip)
+    "mda_bn_finalize": "pppppppiiiffs",
+    "mda_bn_apply": "ppppppiiiiis",
+    "mda_bn_bwd_reduce": "pppppppiiiis",
+    "mda_bn_bwd_apply": "pppppppppppiiiiis",
+    "mda_affine_act": "pppppiiiis",
+    "mda_pack_weight": "ppiiiiis",
+    "mda_unpack_wgrad": "ppiiiiis",
+    # conv (csrc/conv_igemm.hip)
+    "mda_conv_fwd": "pppppppiiiiiiiiiiiiiiis",
+    "mda_conv_dgrad": "ppppiiiiiiiiiiiiiiiis",
+    "mda_conv_wgrad": "pppiiiiiiiiiiiiiiiiis",
+    # optimizers (csrc/optim.hip)
+    "mda_sgd_step": "ppppiffffis",
+    "mda_dot_step": "pppppppiffffis",
+    "mda_adam_step": "pppppiffffffiis",
+    "mda_scale_inplace": "ppiis",
+    "mda_sq_norm": "ppiis",
+    # data (csrc/aug.hip)
+    "mda_cifar_aug": "ppppiiiiiiiis",
+    # crd (csrc/crd.hip)
+    "mda_crd_scores": "pppppiiifs",
+    "mda_crd_update": "pppiiifs",
+    "mda_crd_sample": "pppiiiis",
+    # depthwise (csrc/dwconv.hip)
+    "mda_dwconv_fwd": "pppiiiiiiiiiis",
+    "mda_dwconv_bwd": "ppppppiiiiiiiiis",
+}
+
+HOST_SIGNATURES = {
+    "mdah_alias_build": "ppi",
+    "mdah_crd_sample": "ppppiiiiii",
+    "mdah_gather_u8": "pppiii",
+}
+
+
+def gpu_box() -> bool:
+    """A GPU is present (without initialising HIP)."""
+    try:
+        return torch.cuda.device_count() > 0
+    except Exception:
+        return False
+
+
+def _declare(lib, table):
+    for name, codes in table.items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            continue
+        fn.argtypes = [_CT[c] for c in codes]
+        fn.restype = ctypes.c_int
+
+
+def load(required: bool = False, kind: str = "hip"):
+    """Load (building first if stale) a native library; returns the ctypes handle or None."""
+    with _lock:
+        if kind in _LIBS:
+            return _LIBS[kind]
+        if kind in _FAILED and not required:
+            return None
+        try:
+            if os.environ.get("MDA_NO_BUILD", "0") != "1":
+                _build.build(kind)
+            path = _build.HIP_LIB if kind == "hip" else _build.HOST_LIB
+            lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+            _declare(lib, SIGNATURES if kind == "hip" else HOST_SIGNATURES)
+            _LIBS[kind] = lib
+            LOADED_PATHS.append(path)
+            return lib
+        except Exception as e:  # pragma: no cover - exercised on broken toolchains
+            _FAILED[kind] = e
+            if required:
+                raise RuntimeError(f"native library '{kind}' unavailable: {e}") from e
+            return None
+
+
+def available(kind: str = "hip") -> bool:
+    return load(required=False, kind=kind) is not None
+
+
+def _arg(a, code):
+    if code in ("p", "s"):
+        if a is None:
+            return None
+        if isinstance(a, torch.Tensor):
+            return a.data_ptr()
+        return int(a)
+    if code == "i":
+        return int(a)
+    return float(a)
+
+
+def call(name: str, *args, stream=None):
+    """Invoke a HIP launcher; ``stream`` defaults to the current torch stream."""
+    lib = load(required=True)
+    fn = getattr(lib, name)
+    codes = SIGNATURES[name]
+    if len(args) != len(codes) - 1:
+        raise TypeError(f"{name}: expected {len(codes) - 1} args, got {len(args)}")
+    if stream is None:
+        stream = torch.cuda.current_stream().cuda_stream
+    conv = [_arg(a, c) for a, c in zip(args, codes[:-1])]
+    err = fn(*conv, stream)
+    if err != 0:
+        raise RuntimeError(f"{name} failed with hipError {err}")
+
+
+def host_call(name: str, *args):
+    lib = load(required=True, kind="host")
+    fn = getattr(lib, name)
+    codes = HOST_SIGNATURES[name]
+    conv = [_arg(a, c) for a, c in zip(args, codes)]
+    return fn(*conv)

@@ -29,37 +29,16 @@ _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int64, "f": ctypes.c_float, "s": ctyp
 # name -> argument codes (stream last).  Kept in sync with csrc/*.hip `extern "C"` launchers.
 SIGNATURES = {
     # losses (csrc/losses.hip)
-    "mda_ce_kd_fwd_bwd": "pppppiiffffffs",
-    "mda_dkd_fwd_bwd": "pppppiifffffffs",
-    "mda_loss_finalize": "ppiis",
-    "mda_at_loss_fwd": "pppiiifs",
-    # elementwise / BN (csrc/bn.hip)
-    "mda_bn_finalize": "pppppppiiiffs",
-    "mda_bn_apply": "ppppppiiiiis",
-    "mda_bn_bwd_reduce": "pppppppiiiis",
-    "mda_bn_bwd_apply": "pppppppppppiiiiis",
-    "mda_affine_act": "pppppiiiis",
-    "mda_pack_weight": "ppiiiiis",
-    "mda_unpack_wgrad": "ppiiiiis",
-    # conv (csrc/conv_igemm.hip)
-    "mda_conv_fwd": "pppppppiiiiiiiiiiiiiiis",
-    "mda_conv_dgrad": "ppppiiiiiiiiiiiiiiiis",
-    "mda_conv_wgrad": "pppiiiiiiiiiiiiiiiiis",
+    "mda_logit_loss": "iiippppppppiifffffs",
+    "mda_axpby": "ipppppis",
+    # convolution (csrc/conv_igemm.hip)
+    "mda_conv_fwd": "ppppppp" + "i" * 14 + "s",
     # optimizers (csrc/optim.hip)
-    "mda_sgd_step": "ppppiffffis",
-    "mda_dot_step": "pppppppiffffis",
-    "mda_adam_step": "pppppiffffffiis",
-    "mda_scale_inplace": "ppiis",
-    "mda_sq_norm": "ppiis",
-    # data (csrc/aug.hip)
-    "mda_cifar_aug": "ppppiiiiiiiis",
-    # crd (csrc/crd.hip)
-    "mda_crd_scores": "pppppiiifs",
-    "mda_crd_update": "pppiiifs",
-    "mda_crd_sample": "pppiiiis",
-    # depthwise (csrc/dwconv.hip)
-    "mda_dwconv_fwd": "pppiiiiiiiiiis",
-    "mda_dwconv_bwd": "ppppppiiiiiiiiis",
+    "mda_sgd_step": "ppppfffpfis",
+    "mda_dot_step": "pppppppffffiis",
+    "mda_adam_step": "ppppppffffifpfis",
+    "mda_sq_norm": "pipppfs",
+    "mda_scale_inplace": "ppis",
 }
 
 HOST_SIGNATURES = {

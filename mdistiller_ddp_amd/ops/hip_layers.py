@@ -1,0 +1,113 @@
+"""HIP paths of the fused layer ops (``ops/nn.py``).
+
+Inference-mode conv+BN(+residual)(+act) -- every teacher layer, and the
+student during validation -- runs as ONE launch of the MFMA implicit-GEMM
+kernel (``csrc/conv_igemm.hip``) with BN folded into the packed bf16 weights
+and a per-channel bias.  Packing/folding happens once per weight version
+(the frozen teacher: once per run) and is cached on the module.
+
+Activations on this path are bf16 NHWC (``torch.channels_last``) end to end.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import _ext
+
+_ACT = {"none": 0, "relu": 1, "relu6": 2}
+
+
+def _autocast_bf16() -> bool:
+    return torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+
+
+def _needs_grad(x, conv, bn) -> bool:
+    if not torch.is_grad_enabled():
+        return False
+    if x.requires_grad or conv.weight.requires_grad:
+        return True
+    if bn is not None and bn.weight is not None and bn.weight.requires_grad:
+        return True
+    return False
+
+
+def conv_supported(x, conv, bn) -> bool:
+    if not (x.is_cuda and x.dim() == 4 and isinstance(conv, nn.Conv2d)):
+        return False
+    if conv.groups != 1 or conv.dilation != (1, 1) or conv.padding_mode != "zeros":
+        return False
+    if conv.stride[0] != conv.stride[1] or not isinstance(conv.padding, tuple):
+        return False
+    if conv.padding[0] != conv.padding[1]:
+        return False
+    if bn is not None and (bn.training or not bn.track_running_stats):
+        return False
+    if x.dtype == torch.bfloat16:
+        pass
+    elif not _autocast_bf16():
+        return False
+    return not _needs_grad(x, conv, bn)
+
+
+def bn_supported(x, bn) -> bool:
+    return False
+
+
+def _version_key(conv, bn):
+    key = [conv.weight._version, conv.weight.data_ptr()]
+    if conv.bias is not None:
+        key += [conv.bias._version]
+    if bn is not None:
+        for t in (bn.weight, bn.bias, bn.running_mean, bn.running_var):
+            if t is not None:
+                key += [t._version, t.data_ptr()]
+    return tuple(key)
+
+
+@torch.no_grad()
+def _packed(conv, bn):
+    key = _version_key(conv, bn)
+    cache = getattr(conv, "_mda_pack", None)
+    if cache is not None and cache[0] == key and cache[1] is bn:
+        return cache[2], cache[3]
+    w = conv.weight.detach().float()
+    cout = w.shape[0]
+    b = conv.bias.detach().float() if conv.bias is not None else torch.zeros(cout, device=w.device)
+    if bn is not None:
+        g = bn.weight.detach().float() if bn.weight is not None else torch.ones(cout, device=w.device)
+        beta = bn.bias.detach().float() if bn.bias is not None else torch.zeros(cout, device=w.device)
+        s = g / torch.sqrt(bn.running_var.float() + bn.eps)
+        w = w * s.reshape(-1, 1, 1, 1)
+        b = beta + (b - bn.running_mean.float()) * s
+    K = w.shape[1] * w.shape[2] * w.shape[3]
+    Kp = (K + 31) // 32 * 32
+    wp = torch.zeros(cout, Kp, dtype=torch.bfloat16, device=w.device)
+    wp[:, :K] = w.permute(0, 2, 3, 1).reshape(cout, K).to(torch.bfloat16)
+    b = b.contiguous()
+    conv._mda_pack = (key, bn, wp, b)
+    return wp, b
+
+
+def _nhwc_bf16(t):
+    if t.dtype != torch.bfloat16:
+        t = t.to(torch.bfloat16)
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+def conv_bn_act(x, conv, bn, act, residual, want_preact):
+    wp, bias = _packed(conv, bn)
+    x = _nhwc_bf16(x)
+    N, Cin, H, W = x.shape
+    Cout = conv.out_channels
+    KH, KW = conv.kernel_size
+    s, p = conv.stride[0], conv.padding[0]
+    Ho = (H + 2 * p - KH) // s + 1
+    Wo = (W + 2 * p - KW) // s + 1
+    y = torch.empty((N, Cout, Ho, Wo), dtype=torch.bfloat16, device=x.device,
+                    memory_format=torch.channels_last)
+    pre = torch.empty_like(y) if want_preact else None
+    res = _nhwc_bf16(residual) if residual is not None else None
+    _ext.call("mda_conv_fwd", x, wp, None, bias, res, y, pre, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
+              s, p, wp.shape[1], _ACT[act], 0)
+    return y, pre

@@ -1,0 +1,155 @@
+"""Bucketed all-reduce of the flat gradient buffer, overlapped with backward.
+
+Replaces ``DistributedDataParallel`` (reference `tools/train.py:86`) for the
+distiller's learnable parameters only:
+
+* only student + distiller-module gradients go on the wire (the teacher is
+  frozen and never registered: 4.7 MB instead of 33 MB per step for DKD
+  res32x4->res8x4);
+* gradients already live in one contiguous buffer
+  (:class:`..engine.optim.FlatParams`), so a bucket is a slice -- no packing
+  copies -- and the collective runs on the native RCCL stream;
+* buckets follow the flat layout (reverse registration order = the order
+  backward produces gradients), and each bucket is launched from a
+  post-accumulate-grad hook as soon as its last gradient lands, so the
+  all-reduce of the head's gradients overlaps the backward of the stem;
+* the 1/world averaging is NOT a separate pass: the optimizer kernel scales
+  by ``grad_scale = 1/world`` while it reads the gradient anyway;
+* DOT's two gradient sets are reduced (the reference's DDP syncs only the
+  first backward).
+
+Bucket size: xGMI is point-to-point (7 links/GPU); RCCL's ring all-reduce of
+an S-byte bucket costs ~latency + 2(N-1)/N * S / link_bw per channel, so a
+few MB per bucket already amortises the ~10-20 us latency while keeping two
+or three buckets in flight behind backward.  ``DIST.BUCKET_MB`` (default 8)
+sets it; the north-star student (4.7 MB fp32) becomes 1-2 buckets.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from .dist import is_dist, get_world_size
+
+
+class GradReducer:
+    def __init__(self, flat, bucket_mb: float = 8.0, overlap: bool = True, group=None,
+                 wire_dtype: str = "fp32"):
+        self.flat = flat
+        self.group = group
+        self.enabled = is_dist()
+        self.world = get_world_size()
+        self.overlap = overlap and self.enabled
+        self.wire_bf16 = wire_dtype == "bf16"
+        self.bytes_reduced = 0  # bytes put on the wire (tests / accounting)
+        self.calls = 0
+        bucket_elems = max(64, int(bucket_mb * (1 << 20) / 4))
+        # buckets aligned to parameter boundaries, in flat (= backward) order
+        order = sorted(range(len(flat.params)), key=lambda i: flat.offsets[i])
+        self.buckets = []  # list of (start, end, [param indices])
+        cur, start, size = [], None, 0
+        for i in order:
+            o, n = flat.offsets[i], flat.params[i].numel()
+            if start is None:
+                start = o
+            cur.append(i)
+            size = o + n - start
+            if size >= bucket_elems:
+                self.buckets.append([start, self._end(o, n), cur])
+                cur, start, size = [], None, 0
+        if cur:
+            self.buckets.append([start, self._end(flat.offsets[cur[-1]], flat.params[cur[-1]].numel()), cur])
+        if self.buckets:
+            self.buckets[-1][1] = flat.numel  # include tail padding
+        self._param_bucket = {}
+        for b, (_, _, idx) in enumerate(self.buckets):
+            for i in idx:
+                self._param_bucket[i] = b
+        self._pending = []
+        self._works = {}
+        self._hooks = []
+        self._armed = False
+        if self.overlap:
+            for i, p in enumerate(flat.params):
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
+
+    @staticmethod
+    def _end(o, n):
+        from ..engine.optim import ALIGN
+        return o + ((n + ALIGN - 1) // ALIGN) * ALIGN
+
+    # ------------------------------------------------------------------
+    def _make_hook(self, i):
+        def hook(_p):
+            if not self._armed:
+                return
+            b = self._param_bucket[i]
+            self._pending[b] -= 1
+            if self._pending[b] == 0:
+                self._launch(b, async_op=True)
+        return hook
+
+    def _slice(self, b):
+        s, e, _ = self.buckets[b]
+        return self.flat.grads[self.flat._bound][s:e]
+
+    def _launch(self, b, async_op):
+        t = self._slice(b)
+        self.bytes_reduced += t.numel() * (2 if self.wire_bf16 else 4)
+        self.calls += 1
+        if self.wire_bf16:
+            tb = t.to(torch.bfloat16)
+            work = dist.all_reduce(tb, group=self.group, async_op=True)
+            self._works[b] = (work, t, tb)
+        else:
+            work = dist.all_reduce(t, group=self.group, async_op=async_op)
+            self._works[b] = (work, None, None)
+
+    def arm(self) -> None:
+        """Call before a backward whose gradients should be reduced on the fly."""
+        if not self.enabled:
+            return
+        self._pending = [len(idx) for (_, _, idx) in self.buckets]
+        self._works = {}
+        self._armed = self.overlap
+
+    def finish(self) -> None:
+        """Launch any bucket not yet launched and wait for all of them."""
+        if not self.enabled:
+            return
+        for b in range(len(self.buckets)):
+            if b not in self._works:
+                self._launch(b, async_op=True)
+        for b, (work, t, tb) in self._works.items():
+            if work is not None:
+                work.wait()
+            if tb is not None:
+                t.copy_(tb)
+        self._works = {}
+        self._armed = False
+
+    def reduce_all(self) -> None:
+        """Non-overlapped reduction of the currently bound gradient set."""
+        if not self.enabled:
+            return
+        self._armed = False
+        self._works = {}
+        self.finish()
+
+    def reduce_sets(self, sets=(0,)) -> None:
+        """Reduce whole gradient sets (DOT: both halves of the [2, n] buffer in one call)."""
+        if not self.enabled:
+            return
+        g = self.flat.grads
+        if len(sets) == g.shape[0]:
+            t = g.view(-1)
+        else:
+            t = g[sets[0]]
+        self.bytes_reduced += t.numel() * 4
+        self.calls += 1
+        dist.all_reduce(t, group=self.group)
+
+    def remove_hooks(self) -> None:
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []

@@ -1,0 +1,69 @@
+"""MFMA implicit-GEMM conv (+folded BN, residual, activation) vs PyTorch fp32."""
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from mdistiller_ddp_amd.ops import hip_layers
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [
+    # N, Cin, H, Cout, k, stride, pad
+    (64, 3, 32, 32, 3, 1, 1),     # r32x4 stem (scalar loader)
+    (64, 32, 32, 64, 3, 1, 1),    # layer1 first conv
+    (64, 64, 32, 64, 3, 1, 1),
+    (64, 64, 32, 128, 3, 2, 1),   # stride-2 transition
+    (64, 128, 16, 128, 3, 1, 1),
+    (64, 128, 16, 256, 3, 2, 1),
+    (64, 256, 8, 256, 3, 1, 1),
+    (64, 64, 32, 128, 1, 2, 0),   # 1x1 shortcut
+    (8, 16, 32, 16, 3, 1, 1),     # resnet20 (vec8 loader)
+    (5, 24, 15, 40, 3, 2, 1),     # odd everything
+    (3, 96, 7, 100, 1, 1, 0),
+]
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("act", ["relu", "none"])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_conv_bn_act_inference(shape, act, with_res):
+    N, Cin, H, Cout, k, s, p = shape
+    torch.manual_seed(0)
+    conv = nn.Conv2d(Cin, Cout, k, s, p, bias=False).cuda()
+    bn = nn.BatchNorm2d(Cout).cuda()
+    with torch.no_grad():
+        bn.running_mean.uniform_(-0.5, 0.5)
+        bn.running_var.uniform_(0.5, 2.0)
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    bn.eval()
+    x = torch.randn(N, Cin, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    Ho = (H + 2 * p - k) // s + 1
+    res = torch.randn(N, Cout, Ho, Ho, device="cuda").to(torch.bfloat16) if with_res else None
+    with torch.no_grad():
+        ref = bn(conv(x.float()))
+        if res is not None:
+            ref = ref + res.float()
+        pre_ref = ref
+        ref = F.relu(ref) if act == "relu" else ref
+        assert hip_layers.conv_supported(x, conv, bn)
+        y, pre = hip_layers.conv_bn_act(x, conv, bn, act, res, True)
+    assert y.dtype == torch.bfloat16 and y.shape == ref.shape
+    tol = 3e-2 * max(1.0, ref.abs().max().item() / 4)
+    torch.testing.assert_close(y.float(), ref, atol=tol, rtol=2e-2)
+    torch.testing.assert_close(pre.float(), pre_ref, atol=tol, rtol=2e-2)
+
+
+def test_teacher_forward_matches_torch():
+    from mdistiller_ddp_amd.models.cifar import resnet32x4
+    from mdistiller_ddp_amd.ops.backend import use_backend
+    torch.manual_seed(0)
+    m = resnet32x4(num_classes=100).cuda().eval()
+    x = torch.randn(16, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        ref, _ = m(x)
+        with torch.autocast("cuda", dtype=torch.bfloat16), use_backend("hip"):
+            out, feats = m(x)
+    rel = (out.float() - ref).norm() / ref.norm()
+    assert rel < 3e-2, rel

@@ -32,7 +32,8 @@ SIGNATURES = {
     "mda_logit_loss": "iiippppppppiifffffs",
     "mda_axpby": "ipppppis",
     # convolution (csrc/conv_igemm.hip)
-    "mda_conv_fwd": "ppppppp" + "i" * 14 + "s",
+    "mda_conv_fwd": "pppppppp" + "i" * 15 + "s",
+    "mda_conv_plan": "iiipp",
     # optimizers (csrc/optim.hip)
     "mda_sgd_step": "ppppfffpfis",
     "mda_dot_step": "pppppppffffiis",
@@ -98,6 +99,8 @@ def _arg(a, code):
             return None
         if isinstance(a, torch.Tensor):
             return a.data_ptr()
+        if isinstance(a, ctypes._SimpleCData):
+            return ctypes.addressof(a)
         return int(a)
     if code == "i":
         return int(a)
@@ -109,12 +112,16 @@ def call(name: str, *args, stream=None):
     lib = load(required=True)
     fn = getattr(lib, name)
     codes = SIGNATURES[name]
-    if len(args) != len(codes) - 1:
-        raise TypeError(f"{name}: expected {len(codes) - 1} args, got {len(args)}")
-    if stream is None:
-        stream = torch.cuda.current_stream().cuda_stream
-    conv = [_arg(a, c) for a, c in zip(args, codes[:-1])]
-    err = fn(*conv, stream)
+    has_stream = codes.endswith("s")
+    nargs = len(codes) - (1 if has_stream else 0)
+    if len(args) != nargs:
+        raise TypeError(f"{name}: expected {nargs} args, got {len(args)}")
+    conv = [_arg(a, c) for a, c in zip(args, codes[:nargs])]
+    if has_stream:
+        if stream is None:
+            stream = torch.cuda.current_stream().cuda_stream
+        conv.append(stream)
+    err = fn(*conv)
     if err != 0:
         raise RuntimeError(f"{name} failed with hipError {err}")
 

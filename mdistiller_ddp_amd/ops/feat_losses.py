@@ -1,0 +1,250 @@
+"""Feature / relation distillation losses.
+
+Formulas follow the reference distillers line by line (cited per function);
+the implementations are written for the device: fp32 math on bf16
+activations, Gram-form kernels instead of materialised B x B x D tensors
+where the algebra allows, and the AT loss as a fused HIP kernel
+(``csrc/feat.hip``) on MI355X.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import _ext
+from .backend import hip_enabled_for
+
+
+def _pool_to_match(f_s, f_t):
+    s_H, t_H = f_s.shape[2], f_t.shape[2]
+    if s_H > t_H:
+        f_s = F.adaptive_avg_pool2d(f_s, (t_H, t_H))
+    elif s_H < t_H:
+        f_t = F.adaptive_avg_pool2d(f_t, (s_H, s_H))
+    return f_s, f_t
+
+
+# ---------------------------------------------------------------- AT (K8)
+def _at_map(feat, p):
+    return F.normalize(feat.float().pow(p).mean(1).reshape(feat.size(0), -1))
+
+
+def single_stage_at_loss_ref(f_s, f_t, p):
+    """`distillers/AT.py:8-18`."""
+    f_s, f_t = _pool_to_match(f_s, f_t)
+    return (_at_map(f_s, p) - _at_map(f_t, p)).pow(2).mean()
+
+
+class _ATLoss(torch.autograd.Function):
+    """Fused: a = mean_c f^p per pixel -> L2-normalise over HW -> mean sq diff.
+
+    Teacher map is constant; the kernel writes the loss and d loss / d f_s.
+    """
+
+    @staticmethod
+    def forward(ctx, f_s, f_t, p):
+        f_s = f_s.contiguous(memory_format=torch.channels_last)
+        f_t = f_t.contiguous(memory_format=torch.channels_last)
+        N, C, H, W = f_s.shape
+        Ct = f_t.shape[1]
+        grad = torch.empty_like(f_s)
+        loss = torch.empty(1, dtype=torch.float32, device=f_s.device)
+        dt_s = 1 if f_s.dtype == torch.bfloat16 else 0
+        dt_t = 1 if f_t.dtype == torch.bfloat16 else 0
+        from .losses import workspace
+        ws = workspace(f_s.device)
+        _ext.call("mda_at_loss", dt_s, dt_t, f_s, f_t, grad, loss, ws.partial, ws.counter, N, C, Ct,
+                  H * W, float(p))
+        ctx.save_for_backward(grad)
+        return loss[0]
+
+    @staticmethod
+    def backward(ctx, go):
+        grad, = ctx.saved_tensors
+        return grad * go.to(grad.dtype), None, None
+
+
+def single_stage_at_loss(f_s, f_t, p):
+    f_s, f_t = _pool_to_match(f_s, f_t)
+    if (hip_enabled_for(f_s) and f_s.dim() == 4 and f_s.shape[2:] == f_t.shape[2:]
+            and f_s.dtype in (torch.float32, torch.bfloat16) and f_t.dtype in (torch.float32, torch.bfloat16)
+            and f_s.shape[2] * f_s.shape[3] <= 4096 and float(p) == 2.0):
+        return _ATLoss.apply(f_s, f_t.detach(), p)
+    return single_stage_at_loss_ref(f_s, f_t, p)
+
+
+def at_loss(g_s, g_t, p):
+    return sum(single_stage_at_loss(f_s, f_t, p) for f_s, f_t in zip(g_s, g_t))
+
+
+# ---------------------------------------------------------------- NST
+def single_stage_nst_loss(f_s, f_t):
+    """`distillers/NST.py:12-35`: polynomial (a.b)^2 kernel MMD.
+
+    mean_{ij} (f_i . g_j)^2 over channel pairs = ||F G^T||_F^2 / C_f C_g,
+    computed as batched Gram products (MFMA GEMMs) instead of broadcasting
+    an (N, C, C, HW) tensor.
+    """
+    f_s, f_t = _pool_to_match(f_s, f_t)
+    f_s = F.normalize(f_s.float().reshape(f_s.shape[0], f_s.shape[1], -1), dim=2)
+    f_t = F.normalize(f_t.float().reshape(f_t.shape[0], f_t.shape[1], -1), dim=2)
+
+    def kmean(a, b):
+        return torch.bmm(a, b.transpose(1, 2)).pow(2).mean()
+
+    return kmean(f_t, f_t).detach() + kmean(f_s, f_s) - 2 * kmean(f_s, f_t)
+
+
+def nst_loss(g_s, g_t):
+    return sum(single_stage_nst_loss(f_s, f_t) for f_s, f_t in zip(g_s, g_t))
+
+
+# ---------------------------------------------------------------- PKT
+def pkt_loss(f_s, f_t, eps=1e-7):
+    """`distillers/PKT.py:8-35`."""
+    f_s = f_s.float().reshape(f_s.shape[0], -1)
+    f_t = f_t.float().reshape(f_t.shape[0], -1)
+    f_s = f_s / (f_s.pow(2).sum(1, keepdim=True).sqrt() + eps)
+    f_s = torch.nan_to_num(f_s, nan=0.0)
+    f_t = f_t / (f_t.pow(2).sum(1, keepdim=True).sqrt() + eps)
+    f_t = torch.nan_to_num(f_t, nan=0.0)
+    ms = (f_s @ f_s.t() + 1.0) / 2.0
+    ts = (f_t @ f_t.t() + 1.0) / 2.0
+    ms = ms / ms.sum(1, keepdim=True)
+    ts = ts / ts.sum(1, keepdim=True)
+    return torch.mean(ts * torch.log((ts + eps) / (ms + eps)))
+
+
+# ---------------------------------------------------------------- SP
+def similarity_loss(f_s, f_t):
+    """`distillers/SP.py:12-24`."""
+    bsz = f_s.shape[0]
+    f_s = f_s.float().reshape(bsz, -1)
+    f_t = f_t.float().reshape(bsz, -1)
+    G_s = F.normalize(f_s @ f_s.t())
+    G_t = F.normalize(f_t @ f_t.t())
+    d = G_t - G_s
+    return (d * d).sum().reshape(1) / (bsz * bsz)
+
+
+def sp_loss(g_s, g_t):
+    return sum(similarity_loss(f_s, f_t) for f_s, f_t in zip(g_s, g_t))
+
+
+# ---------------------------------------------------------------- RKD
+def _pdist(e, squared, eps):
+    e_sq = e.pow(2).sum(dim=1)
+    prod = e @ e.t()
+    res = (e_sq.unsqueeze(1) + e_sq.unsqueeze(0) - 2 * prod).clamp(min=eps)
+    if not squared:
+        res = res.sqrt()
+    n = len(e)
+    return res * (1.0 - torch.eye(n, device=e.device, dtype=res.dtype))
+
+
+def _angles(x):
+    """cos of the angle at i between (j - i) and (k - i), flattened (B^3)."""
+    d = x.unsqueeze(0) - x.unsqueeze(1)
+    d = F.normalize(d, p=2, dim=2)
+    return torch.bmm(d, d.transpose(1, 2)).reshape(-1)
+
+
+def rkd_loss(f_s, f_t, squared=False, eps=1e-12, distance_weight=25, angle_weight=50):
+    """`distillers/RKD.py:21-50`."""
+    stu = f_s.float().reshape(f_s.shape[0], -1)
+    tea = f_t.float().reshape(f_t.shape[0], -1)
+    with torch.no_grad():
+        t_d = _pdist(tea, squared, eps)
+        t_d = t_d / t_d[t_d > 0].mean()
+    d = _pdist(stu, squared, eps)
+    d = d / d[d > 0].mean()
+    loss_d = F.smooth_l1_loss(d, t_d)
+    with torch.no_grad():
+        t_angle = _angles(tea)
+    s_angle = _angles(stu)
+    loss_a = F.smooth_l1_loss(s_angle, t_angle)
+    return distance_weight * loss_d + angle_weight * loss_a
+
+
+# ---------------------------------------------------------------- KDSVD
+def _removenan(x):
+    return torch.where(torch.isfinite(x), x, torch.zeros_like(x))
+
+
+def _svd(feat, n=1):
+    N, C, H, W = feat.shape
+    # reference: view(N, C*H, W) of an NCHW tensor
+    x = feat.float().contiguous().reshape(N, C * H, W)
+    u, s, vh = torch.linalg.svd(x, full_matrices=False)
+    v = vh.transpose(-2, -1)
+    u, s, v = _removenan(u), _removenan(s), _removenan(v)
+    if n > 0:
+        u = F.normalize(u[:, :, :n], dim=1)
+        s = F.normalize(s[:, :n], dim=1)
+        v = F.normalize(v[:, :, :n], dim=1)
+    return u, s, v
+
+
+def _align_rsv(a, b):
+    cosine = torch.matmul(a.transpose(-2, -1), b)
+    max_abs, _ = torch.max(torch.abs(cosine), 1, keepdim=True)
+    mask = torch.where(torch.eq(max_abs, torch.abs(cosine)), torch.sign(cosine),
+                       torch.zeros_like(cosine))
+    return torch.matmul(a, mask), b
+
+
+def kdsvd_loss(g_s, g_t, k):
+    """`distillers/KDSVD.py:8-35` (batched SVD via rocSOLVER through torch)."""
+    v_sb = v_tb = None
+    losses = []
+    for i, (f_s, f_t) in enumerate(zip(g_s, g_t)):
+        _, s_t, v_t = _svd(f_t.detach(), k)
+        _, _, v_s = _svd(f_s, k + 3)
+        v_s, v_t = _align_rsv(v_s, v_t)
+        s_t = s_t.unsqueeze(1)
+        v_t = v_t * s_t
+        v_s = v_s * s_t
+        if i > 0:
+            s_rbf = torch.exp(-(v_s.unsqueeze(2) - v_sb.unsqueeze(1)).pow(2) / 8)
+            t_rbf = torch.exp(-(v_t.unsqueeze(2) - v_tb.unsqueeze(1)).pow(2) / 8)
+            l2 = (s_rbf - t_rbf.detach()).pow(2)
+            l2 = torch.where(torch.isfinite(l2), l2, torch.zeros_like(l2))
+            losses.append(l2.sum())
+        v_tb, v_sb = v_t, v_s
+    bsz = g_s[0].shape[0]
+    return sum(l / bsz for l in losses)
+
+
+# ---------------------------------------------------------------- VID
+def vid_loss(regressor, log_scale, f_s, f_t, eps=1e-5):
+    """`distillers/VID.py:16-30`: Gaussian NLL with softplus variance."""
+    f_s, f_t = _pool_to_match(f_s, f_t)
+    pred_mean = regressor(f_s).float()
+    pred_var = F.softplus(log_scale.float()) + eps
+    pred_var = pred_var.view(1, -1, 1, 1)
+    nlp = 0.5 * ((pred_mean - f_t.float()) ** 2 / pred_var + torch.log(pred_var))
+    return nlp.mean()
+
+
+# ---------------------------------------------------------------- ReviewKD HCL (K9)
+def hcl_loss(fstudent, fteacher):
+    """`distillers/ReviewKD.py:11-28`: MSE at full resolution plus a 4/2/1
+    average-pooled pyramid, weights 1, 1/2, 1/4, ..., normalised."""
+    loss_all = 0.0
+    for fs, ft in zip(fstudent, fteacher):
+        fs = fs.float()
+        ft = ft.float()
+        h = fs.shape[2]
+        loss = F.mse_loss(fs, ft, reduction="mean")
+        cnt, tot = 1.0, 1.0
+        for l in (4, 2, 1):
+            if l >= h:
+                continue
+            tmpfs = F.adaptive_avg_pool2d(fs, (l, l))
+            tmpft = F.adaptive_avg_pool2d(ft, (l, l))
+            cnt /= 2.0
+            loss = loss + F.mse_loss(tmpfs, tmpft, reduction="mean") * cnt
+            tot += cnt
+        loss = loss / tot
+        loss_all = loss_all + loss
+    return loss_all

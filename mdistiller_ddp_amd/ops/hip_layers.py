@@ -81,7 +81,7 @@ def _packed(conv, bn):
         w = w * s.reshape(-1, 1, 1, 1)
         b = beta + (b - bn.running_mean.float()) * s
     K = w.shape[1] * w.shape[2] * w.shape[3]
-    Kp = (K + 31) // 32 * 32
+    Kp = (K + 63) // 64 * 64
     wp = torch.zeros(cout, Kp, dtype=torch.bfloat16, device=w.device)
     wp[:, :K] = w.permute(0, 2, 3, 1).reshape(cout, K).to(torch.bfloat16)
     b = b.contiguous()
@@ -108,6 +108,23 @@ def conv_bn_act(x, conv, bn, act, residual, want_preact):
                     memory_format=torch.channels_last)
     pre = torch.empty_like(y) if want_preact else None
     res = _nhwc_bf16(residual) if residual is not None else None
-    _ext.call("mda_conv_fwd", x, wp, None, bias, res, y, pre, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
-              s, p, wp.shape[1], _ACT[act], 0)
+    M = N * Ho * Wo
+    tile, splits = conv_plan(M, Cout, wp.shape[1])
+    part = torch.empty(splits * M * Cout, dtype=torch.float32, device=x.device) if splits > 1 else None
+    _ext.call("mda_conv_fwd", x, wp, None, bias, res, y, pre, part, N, H, W, Cin, Ho, Wo, Cout,
+              KH, KW, s, p, wp.shape[1], _ACT[act], tile, splits)
     return y, pre
+
+
+_PLANS: dict = {}
+
+
+def conv_plan(M, Cout, Kp):
+    key = (M, Cout, Kp)
+    plan = _PLANS.get(key)
+    if plan is None:
+        import ctypes
+        t, s = ctypes.c_int64(0), ctypes.c_int64(0)
+        _ext.call("mda_conv_plan", M, Cout, Kp, t, s)
+        plan = _PLANS[key] = (t.value, s.value)
+    return plan

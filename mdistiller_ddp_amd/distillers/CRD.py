@@ -1,0 +1,180 @@
+"""Contrastive Representation Distillation (reference `distillers/CRD.py:9-281`).
+
+Student/teacher pooled features -> ``Embed`` (Linear + L2 norm) -> NCE
+scores against K+1 rows of two momentum memory banks (the positive is the
+sample's own row) -> ``ContrastLoss`` for both directions.
+
+MI355X design:
+
+* the gathered score / gradient passes are HIP kernels streaming bank rows
+  (``ops/crd.py``); the B x (K+1) x D gather is never materialised;
+* the normalisation constants Z live on device and are initialised without a
+  host round trip; under data parallelism they are averaged across ranks on
+  the first step so every replica normalises identically;
+* memory updates are exchanged, not broadcast: every rank all-gathers the
+  (index, v_s, v_t) rows of the global batch and applies all of them, so the
+  banks stay bit-identical across ranks at B_global x (1 + 2D) floats per
+  step.  The reference's DDP instead re-broadcasts the whole bank from rank 0
+  every forward (48.8 MB CIFAR / 1.25 GB ImageNet) and drops the other
+  ranks' updates.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.distributed as dist
+
+from ._base import Distiller
+from ..ops import crd as CO
+from ..ops import losses as L
+
+
+class Normalize(nn.Module):
+    def __init__(self, power=2):
+        super().__init__()
+        self.power = power
+
+    def forward(self, x):
+        norm = x.pow(self.power).sum(1, keepdim=True).pow(1.0 / self.power)
+        return x.div(norm)
+
+
+class Embed(nn.Module):
+    def __init__(self, dim_in=1024, dim_out=128):
+        super().__init__()
+        self.linear = nn.Linear(dim_in, dim_out)
+        self.l2norm = Normalize(2)
+
+    def forward(self, x):
+        x = x.reshape(x.shape[0], -1).float()
+        return self.l2norm(nn.functional.linear(x, self.linear.weight, self.linear.bias))
+
+
+class ContrastLoss(nn.Module):
+    """NCE loss with a uniform noise distribution (`CRD.py:116-141`)."""
+
+    def __init__(self, num_data):
+        super().__init__()
+        self.num_data = num_data
+
+    def forward(self, x):
+        eps = 1e-7
+        bsz = x.shape[0]
+        m = x.size(1) - 1
+        c = m / float(self.num_data)
+        p_pos = x[:, 0]
+        log_d1 = torch.log(p_pos / (p_pos + c + eps))
+        p_neg = x[:, 1:]
+        log_d0 = torch.log(c / (p_neg + c + eps))
+        return -(log_d1.sum() + log_d0.sum()) / bsz
+
+
+class ContrastMemory(nn.Module):
+    """Two momentum memory banks + NCE normalisation constants (`CRD.py:144-220`).
+
+    ``params`` = [K, T, Z_v1, Z_v2, momentum] (same buffer layout as the
+    reference, so checkpoints carry the constants).
+    """
+
+    def __init__(self, input_size, output_size, K, T=0.07, momentum=0.5):
+        super().__init__()
+        self.n_lem = output_size
+        self.K = int(K)
+        self.T = float(T)
+        self.momentum = float(momentum)
+        self.register_buffer("params", torch.tensor([K, T, -1.0, -1.0, momentum]))
+        stdv = 1.0 / math.sqrt(input_size / 3)
+        self.register_buffer("memory_v1", torch.rand(output_size, input_size).mul_(2 * stdv).add_(-stdv))
+        self.register_buffer("memory_v2", torch.rand(output_size, input_size).mul_(2 * stdv).add_(-stdv))
+        self._z_ready = False
+
+    def _init_z(self, out_v1, out_v2):
+        z = torch.stack([out_v1.detach().mean(), out_v2.detach().mean()]) * self.n_lem
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            dist.all_reduce(z)
+            z /= dist.get_world_size()
+        cur = self.params[2:4]
+        self.params[2:4] = torch.where(cur < 0, z.to(cur.dtype), cur)
+        self._z_ready = True
+
+    def forward(self, v1, v2, y, idx):
+        if idx is None:
+            idx = torch.randint(0, self.n_lem, (v1.shape[0], self.K + 1), device=v1.device)
+            idx[:, 0] = y
+        out_v2 = CO.scores(self.memory_v1, idx, v2, self.T)
+        out_v1 = CO.scores(self.memory_v2, idx, v1, self.T)
+        if not self._z_ready:
+            if float(self.params[2]) < 0 or float(self.params[3]) < 0:
+                self._init_z(out_v1, out_v2)
+            self._z_ready = True
+        out_v1 = out_v1 / self.params[2]
+        out_v2 = out_v2 / self.params[3]
+        # the bank update is applied after backward (post_backward) so the
+        # gradient sees the same rows as the forward, exactly as the
+        # reference's detached index_select copy does
+        self._pending = (v1.detach(), v2.detach(), y)
+        return out_v1, out_v2
+
+    def apply_pending(self):
+        pend = getattr(self, "_pending", None)
+        if pend is not None:
+            self._pending = None
+            self.update(*pend)
+
+    @torch.no_grad()
+    def update(self, v1, v2, y):
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            ws = dist.get_world_size()
+            packed = torch.cat([y.double().reshape(-1, 1), v1.double(), v2.double()], 1)
+            allp = [torch.empty_like(packed) for _ in range(ws)]
+            dist.all_gather(allp, packed)
+            packed = torch.cat(allp, 0)
+            D = v1.shape[1]
+            y = packed[:, 0].long()
+            v1 = packed[:, 1:1 + D].float()
+            v2 = packed[:, 1 + D:].float()
+        CO.update(self.memory_v1, y, v1, self.momentum)
+        CO.update(self.memory_v2, y, v2, self.momentum)
+
+
+class CRD(Distiller):
+    teacher_needs = ("pooled",)
+    collective_in_forward = True  # memory-update exchange (keeps hipGraph off for world > 1)
+
+    def __init__(self, student, teacher, cfg, num_data):
+        super().__init__(student, teacher)
+        self.ce_loss_weight = cfg.CRD.LOSS.CE_WEIGHT
+        self.feat_loss_weight = cfg.CRD.LOSS.FEAT_WEIGHT
+        self.embed_s = Embed(cfg.CRD.FEAT.STUDENT_DIM, cfg.CRD.FEAT.DIM)
+        self.embed_t = Embed(cfg.CRD.FEAT.TEACHER_DIM, cfg.CRD.FEAT.DIM)
+        self.contrast = ContrastMemory(cfg.CRD.FEAT.DIM, num_data, cfg.CRD.NCE.K,
+                                       cfg.CRD.NCE.TEMPERATURE, cfg.CRD.NCE.MOMENTUM)
+        self.criterion_s = ContrastLoss(num_data)
+        self.criterion_t = ContrastLoss(num_data)
+
+    def get_extra_parameters(self) -> int:
+        n = sum(p.numel() for m in (self.embed_s, self.embed_t) for p in m.parameters())
+        return n + sum(b.numel() for b in self.contrast.buffers())
+
+    def post_backward(self):
+        """Apply this step's memory-bank update (called by the trainer after backward)."""
+        self.contrast.apply_pending()
+
+    def crd_loss(self, f_s, f_t, idx, contrast_idx):
+        f_s = self.embed_s(f_s)
+        f_t = self.embed_t(f_t)
+        out_s, out_t = self.contrast(f_s, f_t, idx, contrast_idx)
+        return self.criterion_s(out_s) + self.criterion_t(out_t)
+
+    def forward_train(self, image, target, index=None, contrastive_index=None, **kwargs):
+        t_out = self.teacher_forward(image)
+        logits_student, feature_student = self.student(image)
+        _, feature_teacher = t_out.get()
+        loss_ce = L.ce(logits_student, target, self.ce_loss_weight)
+        if index is None:
+            raise ValueError("CRD needs the dataset index of every sample (CRD trainer)")
+        loss_crd = self.feat_loss_weight * self.crd_loss(
+            feature_student["pooled_feat"], feature_teacher["pooled_feat"], index, contrastive_index)
+        return logits_student, {"loss_ce": loss_ce, "loss_kd": loss_crd}

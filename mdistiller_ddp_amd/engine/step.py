@@ -120,6 +120,8 @@ class TrainStep:
         self.flat = FlatParams(distiller.get_learnable_parameters(), 2 if self.is_dot else 1)
         self.opt = build_optimizer(cfg, self.flat, grad_scale=1.0 / self.world, trainer=trainer)
         self.use_graph = bool(use_graph) and self.device.type == "cuda"
+        if self.world > 1 and getattr(distiller, "collective_in_forward", False):
+            self.use_graph = False  # its collectives must not be captured
         self.reducer = GradReducer(self.flat, bucket_mb=float(cfg.DIST.BUCKET_MB),
                                    overlap=not self.use_graph, wire_dtype=cfg.DIST.GRAD_DTYPE)
         self.epoch_t = torch.zeros((), dtype=torch.float32, device=self.device)
@@ -183,6 +185,9 @@ class TrainStep:
             if overlap_comm:
                 self.reducer.arm()
             loss.backward()
+        post = getattr(self.distiller, "post_backward", None)
+        if post is not None:
+            post()
         return preds, losses
 
     def _reduce(self):

@@ -34,6 +34,10 @@ SIGNATURES = {
     # convolution (csrc/conv_igemm.hip)
     "mda_conv_fwd": "pppppppp" + "i" * 15 + "s",
     "mda_conv_plan": "iiipp",
+    # CRD memory (csrc/crd.hip)
+    "mda_crd_scores": "ppppiiifs",
+    "mda_crd_grad": "ppppppiiifs",
+    "mda_crd_update": "pppiifs",
     # optimizers (csrc/optim.hip)
     "mda_sgd_step": "ppppfffpfis",
     "mda_dot_step": "pppppppffffiis",

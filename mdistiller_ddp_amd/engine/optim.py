@@ -145,6 +145,28 @@ class FlatOptimizer:
     def zero_grad(self, set_to_none: bool = False) -> None:
         self.flat.zero_grad()
 
+    # torch.optim-format state (checkpoint compatibility with the reference) --
+    def _unflatten(self, buf: torch.Tensor):
+        f = self.flat
+        return [buf[o:o + p.numel()].view_as(p).detach().clone().cpu() for p, o in zip(f.params, f.offsets)]
+
+    def _flatten_into(self, buf: torch.Tensor, tensors) -> None:
+        f = self.flat
+        for p, o, t in zip(f.params, f.offsets, tensors):
+            if t is not None:
+                buf[o:o + p.numel()].copy_(t.reshape(-1).to(buf.device, buf.dtype))
+
+    def _group(self, **extra) -> dict:
+        g = {"lr": self._lr, "weight_decay": self.weight_decay,
+             "params": list(range(len(self.flat.params)))}
+        g.update(extra)
+        return g
+
+    @staticmethod
+    def _per_param(sd: dict, key: str, n: int):
+        st = sd.get("state", {})
+        return [st.get(i, st.get(str(i), {})).get(key) for i in range(n)]
+
     def state_dict(self) -> dict:
         raise NotImplementedError
 
@@ -177,10 +199,13 @@ class FlatSGD(FlatOptimizer):
         f.data.sub_(self.lr_t * d)
 
     def state_dict(self):
-        return {"type": "SGD", "momentum_buffer": self.buf.clone(), "lr": self._lr}
+        bufs = self._unflatten(self.buf)
+        return {"state": {i: {"momentum_buffer": b} for i, b in enumerate(bufs)},
+                "param_groups": [self._group(momentum=self.momentum, dampening=0, nesterov=False,
+                                             maximize=False)]}
 
     def load_state_dict(self, sd):
-        self.buf.copy_(sd["momentum_buffer"].to(self.buf.device))
+        self._flatten_into(self.buf, self._per_param(sd, "momentum_buffer", len(self.flat.params)))
 
 
 class FlatAdam(FlatOptimizer):
@@ -223,13 +248,20 @@ class FlatAdam(FlatOptimizer):
         f.data.sub_((lr / bc1) * self.m1 / denom)
 
     def state_dict(self):
-        return {"type": "AdamW" if self.decoupled else "Adam", "exp_avg": self.m1.clone(),
-                "exp_avg_sq": self.m2.clone(), "step": self.step_t.clone(), "lr": self._lr}
+        m1, m2 = self._unflatten(self.m1), self._unflatten(self.m2)
+        step = self.step_t.detach().cpu().reshape(())
+        return {"state": {i: {"step": step.clone(), "exp_avg": a, "exp_avg_sq": b}
+                          for i, (a, b) in enumerate(zip(m1, m2))},
+                "param_groups": [self._group(betas=(self.b1, self.b2), eps=self.eps, amsgrad=False,
+                                             maximize=False)]}
 
     def load_state_dict(self, sd):
-        self.m1.copy_(sd["exp_avg"].to(self.m1.device))
-        self.m2.copy_(sd["exp_avg_sq"].to(self.m2.device))
-        self.step_t.copy_(sd["step"].to(self.step_t.device))
+        n = len(self.flat.params)
+        self._flatten_into(self.m1, self._per_param(sd, "exp_avg", n))
+        self._flatten_into(self.m2, self._per_param(sd, "exp_avg_sq", n))
+        steps = [s_ for s_ in self._per_param(sd, "step", n) if s_ is not None]
+        if steps:
+            self.step_t.fill_(float(torch.as_tensor(steps[0])))
 
 
 class FlatDOT(FlatOptimizer):
@@ -294,15 +326,22 @@ class FlatDOT(FlatOptimizer):
         p.sub_(torch.where(has_k, lr * self.buf_k, torch.zeros_like(p)))
 
     def state_dict(self):
-        return {"type": "DOT", "momentum_buffer": self.buf_t.clone(),
-                "momentum_kd_buffer": self.buf_k.clone(), "mask": self.mask.clone(),
-                "first": self.first, "lr": self._lr}
+        bt, bk = self._unflatten(self.buf_t), self._unflatten(self.buf_k)
+        return {"state": {i: {"momentum_buffer": a, "momentum_kd_buffer": b}
+                          for i, (a, b) in enumerate(zip(bt, bk))},
+                "param_groups": [self._group(momentum=self.mu_t, momentum_kd=self.mu_k, dampening=0)],
+                "mda_dot": {"mask": self.mask.detach().cpu().clone(), "first": self.first}}
 
     def load_state_dict(self, sd):
-        self.buf_t.copy_(sd["momentum_buffer"].to(self.buf_t.device))
-        self.buf_k.copy_(sd["momentum_kd_buffer"].to(self.buf_k.device))
-        self.mask.copy_(sd["mask"].to(self.mask.device))
-        self.first = bool(sd.get("first", False))
+        n = len(self.flat.params)
+        self._flatten_into(self.buf_t, self._per_param(sd, "momentum_buffer", n))
+        self._flatten_into(self.buf_k, self._per_param(sd, "momentum_kd_buffer", n))
+        extra = sd.get("mda_dot")
+        if extra is not None:
+            self.mask.copy_(extra["mask"].to(self.mask.device))
+            self.first = bool(extra["first"])
+        else:
+            self.first = False
 
 
 def build_optimizer(cfg, flat: FlatParams, grad_scale: float = 1.0, trainer: str = "base"):

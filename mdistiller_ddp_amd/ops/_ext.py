@@ -38,6 +38,8 @@ SIGNATURES = {
     "mda_crd_scores": "ppppiiifs",
     "mda_crd_grad": "ppppppiiifs",
     "mda_crd_update": "pppiifs",
+    # data augmentation (csrc/aug.hip)
+    "mda_crop_flip_norm": "ppppppp" + "iiiiii" + "s",
     # optimizers (csrc/optim.hip)
     "mda_sgd_step": "ppppfffpfis",
     "mda_dot_step": "pppppppffffiis",
@@ -47,9 +49,8 @@ SIGNATURES = {
 }
 
 HOST_SIGNATURES = {
-    "mdah_alias_build": "ppi",
-    "mdah_crd_sample": "ppppiiiiii",
-    "mdah_gather_u8": "pppiii",
+    "mdah_crd_sample": "ppppppiiiii",
+    "mdah_alias_build": "pppi",
 }
 
 

@@ -12,6 +12,7 @@ from ..ops import feat_losses as FL
 
 class KDSVD(Distiller):
     teacher_needs = ("feats",)
+    graph_capturable = False  # rocSOLVER batched SVD synchronises with the host
 
     def __init__(self, student, teacher, cfg):
         super().__init__(student, teacher)

@@ -43,6 +43,9 @@ def warmup_factor(epoch, warmup):
 class Distiller(nn.Module):
     #: which teacher outputs the method consumes ("logits", "feats", "preact")
     teacher_needs = ("logits",)
+    #: False when the training step contains host-synchronising ops (KDSVD's
+    #: batched SVD) and therefore cannot be captured into a hipGraph
+    graph_capturable = True
 
     def __init__(self, student: nn.Module, teacher: nn.Module):
         super().__init__()

@@ -30,6 +30,17 @@ from ..parallel import GradReducer, get_world_size
 from .optim import FlatParams, FlatDOT, build_optimizer
 
 
+def topk_rank(preds: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+    """Number of classes scored strictly above the target class.
+
+    ``rank < k`` is the top-k hit test; computed with one compare + row sum
+    instead of ``topk`` (whose multi-block ROCm path is not capture-safe and
+    needs a sort), so it lives inside the captured step.
+    """
+    t = preds.gather(1, target.reshape(-1, 1))
+    return (preds > t).sum(1)
+
+
 class DeviceMeters:
     """Loss sums and top-k hit counts kept on device; synced on demand."""
 
@@ -48,11 +59,9 @@ class DeviceMeters:
             total = v if total is None else total + v
         b[0] += total
         n = len(self.loss_keys)
-        k = min(5, preds.shape[1])
-        top = preds.detach().topk(k, dim=1).indices
-        hit = top.eq(target.reshape(-1, 1))
-        b[n + 1] += hit[:, :1].sum().double()
-        b[n + 2] += hit.sum().double()
+        rank = topk_rank(preds.detach(), target)
+        b[n + 1] += (rank < 1).sum().double()
+        b[n + 2] += (rank < 5).sum().double()
         b[n + 3] += float(target.shape[0])
         b[n + 4] += 1.0
 
@@ -119,7 +128,12 @@ class TrainStep:
         self.world = get_world_size()
         self.flat = FlatParams(distiller.get_learnable_parameters(), 2 if self.is_dot else 1)
         self.opt = build_optimizer(cfg, self.flat, grad_scale=1.0 / self.world, trainer=trainer)
-        self.use_graph = bool(use_graph) and self.device.type == "cuda"
+        self.use_graph = (bool(use_graph) and self.device.type == "cuda"
+                          and getattr(distiller, "graph_capturable", True))
+        if self.use_graph:
+            # MIOpen find mode: algorithms are chosen during the eager warm-up
+            # steps, so nothing is searched or JIT-built inside a capture
+            torch.backends.cudnn.benchmark = True
         if self.world > 1 and getattr(distiller, "collective_in_forward", False):
             self.use_graph = False  # its collectives must not be captured
         self.reducer = GradReducer(self.flat, bucket_mb=float(cfg.DIST.BUCKET_MB),
@@ -207,33 +221,41 @@ class TrainStep:
         preds, losses = self._fwd_bwd(b, overlap_comm=True)
         self._reduce()
         self._update(preds, b["target"], losses)
-        return preds, losses
+        # hand out detached outputs: a caller holding autograd-attached outputs
+        # of an eager step across the hipGraph capture crashes the capture
+        return preds.detach(), {k: v.detach() for k, v in losses.items()}
 
     def _capture(self, b: dict):
-        """Capture fwd+bwd(+reduce if world==1)+update into hipGraphs."""
+        """Capture fwd+bwd(+reduce if world==1)+update into hipGraphs.
+
+        The warm-up step and the capture run on the SAME dedicated stream:
+        MIOpen / hipBLASLt create their per-stream handles and workspaces on
+        first use, which is not capturable, so that first use must happen
+        eagerly on the capture stream.
+        """
         static = {k: v.clone() for k, v in b.items()}
         pool = torch.cuda.graph_pool_handle()
-        g1 = torch.cuda.CUDAGraph()
-        s = torch.cuda.Stream()
+        s = self._cap_stream = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
-            # one more eager step on the capture stream (allocator warm-up)
-            self._eager(static)
+            for _ in range(2):
+                self._eager(static)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
+        g1 = torch.cuda.CUDAGraph()
         if self.world <= 1:
-            with torch.cuda.graph(g1, pool=pool):
+            with torch.cuda.graph(g1, pool=pool, stream=s):
                 preds, losses = self._fwd_bwd(static, overlap_comm=False)
                 self._update(preds, static["target"], losses)
             g2 = None
         else:
-            with torch.cuda.graph(g1, pool=pool):
+            with torch.cuda.graph(g1, pool=pool, stream=s):
                 preds, losses = self._fwd_bwd(static, overlap_comm=False)
             g2 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g2, pool=pool):
+            with torch.cuda.graph(g2, pool=pool, stream=s):
                 self._update(preds, static["target"], losses)
         self._graphs = (g1, g2)
-        self._static = (static, preds, losses)
+        self._static = (static, preds.detach(), {k: v.detach() for k, v in losses.items()})
 
     def step(self, batch: dict):
         """Run one step; returns device ``(preds, losses)`` (no host sync)."""
@@ -243,10 +265,25 @@ class TrainStep:
             self.steps_done += 1
             return out
         if self._graphs is None:
-            self._capture(b)
+            try:
+                self._capture(b)
+            except RuntimeError as e:  # a non-capturable op: stay eager for good
+                import warnings
+                warnings.warn(f"hipGraph capture failed ({e}); continuing without graphs")
+                self.use_graph = False
+                self._graphs = self._static = None
+                torch.cuda.synchronize()
+                out = self._eager(b)
+                self.steps_done += 1
+                return out
             self.steps_done += 1
             return self._static[1], self._static[2]
         static, preds, losses = self._static
+        if any(static[k].shape != v.shape for k, v in b.items()):
+            # e.g. the last partial batch of an epoch: run it eagerly
+            out = self._eager(b)
+            self.steps_done += 1
+            return out
         for k, v in b.items():
             static[k].copy_(v, non_blocking=True)
         g1, g2 = self._graphs

@@ -82,6 +82,7 @@ def validate(val_loader, distiller, device=None, dtype=None):
     """Global top-1 / top-5 / CE over the (rank-sharded) validation set."""
     from ..parallel import dist_fn
     from ..parallel.dist import is_master
+    from .step import topk_rank
     distiller.eval()
     if device is None:
         device = next(distiller.parameters()).device
@@ -102,12 +103,10 @@ def validate(val_loader, distiller, device=None, dtype=None):
         with torch.autocast("cuda", dtype=dtype, enabled=amp):
             out = distiller(image=image)
         out = out.float()
-        k = min(5, out.shape[1])
-        top = out.topk(k, 1).indices
-        hit = top.eq(target.reshape(-1, 1))
+        rank = topk_rank(out, target)
         acc[0] += F.cross_entropy(out, target, reduction="sum").double()
-        acc[1] += hit[:, :1].sum().double()
-        acc[2] += hit.sum().double()
+        acc[1] += (rank < 1).sum().double()
+        acc[2] += (rank < 5).sum().double()
         acc[3] += target.numel()
         if pbar is not None:
             pbar.update()

@@ -31,6 +31,8 @@ SIGNATURES = {
     # losses (csrc/losses.hip)
     "mda_logit_loss": "iiippppppppiifffffs",
     "mda_axpby": "ipppppis",
+    # feature losses (csrc/feat.hip)
+    "mda_at_loss": "iipppppp" + "iiii" + "fs",
     # convolution (csrc/conv_igemm.hip)
     "mda_conv_fwd": "pppppppp" + "i" * 15 + "s",
     "mda_conv_plan": "iiipp",

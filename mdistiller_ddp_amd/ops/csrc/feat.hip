@@ -1,0 +1,110 @@
+// Attention-transfer loss, fused forward + backward (survey K8; reference
+// distillers/AT.py:8-21, p = 2):
+//
+//   a[n, p]  = mean_c f[n, c, p]^2                (per pixel attention map)
+//   â[n, :]  = a[n, :] / max(||a[n, :]||_2, 1e-12)
+//   loss     = mean_{n, p} (â_s - â_t)^2
+//   dL/df_s[n, c, p] = 2 f_s[n, c, p] / C * (g_p - â_p <g, â>) / ||a_s||,
+//                      g = 2 (â_s - â_t) / (N * HW)
+//
+// One workgroup per sample; NHWC features so each pixel's channels are one
+// contiguous run (16-byte loads).  The two maps live in LDS (HW <= 4096), the
+// student feature is read twice (map, then gradient) and the teacher once;
+// nothing of size C x HW is ever materialised.  Per-sample loss partials are
+// summed by the last-arriving workgroup in a fixed order (deterministic).
+#include "common.h"
+
+namespace {
+
+constexpr int MAXHW = 4096;
+
+template <typename TS>
+__device__ __forceinline__ float sumsq_pixel(const TS* __restrict__ f, int C) {
+  float s = 0.f;
+  for (int c = 0; c < C; ++c) {
+    float v = io<TS>::ld(f, c);
+    s += v * v;
+  }
+  return s;
+}
+
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += red[i];
+  return t;
+}
+
+template <typename TS, typename TT>
+__global__ void __launch_bounds__(256)
+at_loss_kernel(const TS* __restrict__ fs, const TT* __restrict__ ft, TS* __restrict__ grad,
+               float* __restrict__ loss, float* __restrict__ partial, unsigned* __restrict__ counter,
+               int N, int C, int Ct, int HW) {
+  __shared__ float as_[MAXHW];
+  __shared__ float at_[MAXHW];
+  __shared__ float red[8];
+  const int n = blockIdx.x;
+  const TS* fsn = fs + (int64_t)n * HW * C;
+  const TT* ftn = ft + (int64_t)n * HW * Ct;
+  float ss = 0.f, st = 0.f;
+  for (int p = threadIdx.x; p < HW; p += blockDim.x) {
+    float a = sumsq_pixel<TS>(fsn + (int64_t)p * C, C) / C;
+    float b = sumsq_pixel<TT>(ftn + (int64_t)p * Ct, Ct) / Ct;
+    as_[p] = a;
+    at_[p] = b;
+    ss += a * a;
+    st += b * b;
+  }
+  const float ns = fmaxf(sqrtf(block_sum(ss, red)), 1e-12f);
+  const float nt = fmaxf(sqrtf(block_sum(st, red)), 1e-12f);
+  const float inv_ns = 1.f / ns, inv_nt = 1.f / nt;
+  const float gscale = 2.f / ((float)N * HW);
+  float l = 0.f, gdot = 0.f;
+  for (int p = threadIdx.x; p < HW; p += blockDim.x) {
+    float d = as_[p] * inv_ns - at_[p] * inv_nt;
+    l += d * d;
+    gdot += gscale * d * as_[p] * inv_ns;
+  }
+  l = block_sum(l, red);
+  gdot = block_sum(gdot, red);
+  for (int p = threadIdx.x; p < HW; p += blockDim.x) {
+    float ah = as_[p] * inv_ns;
+    float g = gscale * (ah - at_[p] * inv_nt);
+    float dLda = (g - ah * gdot) * inv_ns * (2.f / C);
+    const TS* src = fsn + (int64_t)p * C;
+    TS* dst = grad + ((int64_t)n * HW + p) * C;
+    for (int c = 0; c < C; ++c) io<TS>::st(dst, c, dLda * io<TS>::ld(src, c));
+  }
+  if (threadIdx.x == 0) partial[n] = l;
+  if (mda_arrive(counter, gridDim.x)) {
+    if (threadIdx.x < 64) {
+      float t = 0.f;
+      for (int i = threadIdx.x; i < (int)gridDim.x; i += 64) t += partial[i];
+      t = wave_sum(t);
+      if (threadIdx.x == 0) loss[0] = t / ((float)N * HW);
+    }
+  }
+}
+
+}  // namespace
+
+// fs [N, HW, C] (NHWC), ft [N, HW, Ct]; grad like fs; loss[1]; partial >= N floats.
+MDA_API int mda_at_loss(int64_t dts, int64_t dtt, const void* fs, const void* ft, void* grad,
+                        float* loss, float* partial, unsigned* counter, int64_t N, int64_t C,
+                        int64_t Ct, int64_t HW, float p, hipStream_t st) {
+  if (HW > MAXHW || p != 2.f) return (int)hipErrorInvalidValue;
+#define AT_L(TS, TT)                                                                            \
+  hipLaunchKernelGGL((at_loss_kernel<TS, TT>), dim3((int)N), dim3(256), 0, st, (const TS*)fs,   \
+                     (const TT*)ft, (TS*)grad, loss, partial, counter, (int)N, (int)C, (int)Ct, \
+                     (int)HW)
+  if (dts == DT_F32 && dtt == DT_F32) AT_L(float, float);
+  else if (dts == DT_BF16 && dtt == DT_BF16) AT_L(bf16_t, bf16_t);
+  else if (dts == DT_BF16 && dtt == DT_F32) AT_L(bf16_t, float);
+  else AT_L(float, bf16_t);
+#undef AT_L
+  MDA_CHECK_LAUNCH();
+}

@@ -149,15 +149,21 @@ def _angles(x):
     return torch.bmm(d, d.transpose(1, 2)).reshape(-1)
 
 
+def _positive_mean(x):
+    """``x[x > 0].mean()`` without a data-dependent shape (capture-safe)."""
+    pos = (x > 0).to(x.dtype)
+    return (x * pos).sum() / pos.sum()
+
+
 def rkd_loss(f_s, f_t, squared=False, eps=1e-12, distance_weight=25, angle_weight=50):
     """`distillers/RKD.py:21-50`."""
     stu = f_s.float().reshape(f_s.shape[0], -1)
     tea = f_t.float().reshape(f_t.shape[0], -1)
     with torch.no_grad():
         t_d = _pdist(tea, squared, eps)
-        t_d = t_d / t_d[t_d > 0].mean()
+        t_d = t_d / _positive_mean(t_d)
     d = _pdist(stu, squared, eps)
-    d = d / d[d > 0].mean()
+    d = d / _positive_mean(d)
     loss_d = F.smooth_l1_loss(d, t_d)
     with torch.no_grad():
         t_angle = _angles(tea)

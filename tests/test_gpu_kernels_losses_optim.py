@@ -110,3 +110,24 @@ def test_optimizers_hip_vs_torch(kind):
             o.set_lr(0.1 / (it + 1))
             o.step()
     torch.testing.assert_close(flats[0][0].data, flats[1][0].data, atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("shape_s,shape_t", [((8, 64, 32, 32), (8, 256, 32, 32)),
+                                             ((4, 16, 8, 8), (4, 48, 8, 8)),
+                                             ((3, 32, 56, 56), (3, 64, 56, 56))])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_at_loss_kernel(shape_s, shape_t, dtype):
+    from mdistiller_ddp_amd.ops import feat_losses as FL
+    torch.manual_seed(4)
+    fs = torch.randn(*shape_s, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    ft = torch.randn(*shape_t, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    a = fs.clone().requires_grad_(True)
+    with use_backend("hip"):
+        l1 = FL.single_stage_at_loss(a, ft, 2)
+    l1.backward()
+    b = fs.float().clone().requires_grad_(True)
+    l2 = FL.single_stage_at_loss_ref(b, ft.float(), 2)
+    l2.backward()
+    tol = 1e-4 if dtype == torch.float32 else 3e-2
+    torch.testing.assert_close(l1.float(), l2, rtol=tol, atol=1e-7)
+    torch.testing.assert_close(a.grad.float(), b.grad, rtol=tol, atol=tol * b.grad.abs().max().item())

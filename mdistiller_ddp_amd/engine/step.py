@@ -238,8 +238,9 @@ class TrainStep:
         s = self._cap_stream = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
-            for _ in range(2):
-                self._eager(static)
+            # this batch's real (eager) step doubles as the capture-stream warm-up;
+            # capturing records kernels without executing them
+            out = self._eager(static)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         g1 = torch.cuda.CUDAGraph()
@@ -256,6 +257,7 @@ class TrainStep:
                 self._update(preds, static["target"], losses)
         self._graphs = (g1, g2)
         self._static = (static, preds.detach(), {k: v.detach() for k, v in losses.items()})
+        return out
 
     def step(self, batch: dict):
         """Run one step; returns device ``(preds, losses)`` (no host sync)."""
@@ -266,7 +268,7 @@ class TrainStep:
             return out
         if self._graphs is None:
             try:
-                self._capture(b)
+                out = self._capture(b)
             except RuntimeError as e:  # a non-capturable op: stay eager for good
                 import warnings
                 warnings.warn(f"hipGraph capture failed ({e}); continuing without graphs")
@@ -277,7 +279,7 @@ class TrainStep:
                 self.steps_done += 1
                 return out
             self.steps_done += 1
-            return self._static[1], self._static[2]
+            return out
         static, preds, losses = self._static
         if any(static[k].shape != v.shape for k, v in b.items()):
             # e.g. the last partial batch of an epoch: run it eagerly

@@ -1,0 +1,74 @@
+"""Model zoo: stem-inclusive feature contract, staged forward, parameter counts."""
+import pytest
+import torch
+
+from mdistiller_ddp_amd.models import (cifar_model_dict, tiny_imagenet_model_dict,
+                                       imagenet_model_dict, check_staged_forward)
+
+# parameter counts measured on the reference models
+PARAMS_M = {"resnet32x4": 7.43, "resnet8x4": 1.23, "resnet56": 0.86, "resnet20": 0.28,
+            "resnet110": 1.74, "wrn_40_2": 2.26, "wrn_16_2": 0.70, "vgg13": 9.46, "vgg8": 3.97,
+            "MobileNetV2": 0.81, "ShuffleV1": 0.95, "ShuffleV2": 1.36, "ResNet50": 23.71,
+            "ResNet18": 11.22}
+
+
+@pytest.mark.parametrize("name", sorted(cifar_model_dict))
+def test_cifar_model_contract(name):
+    torch.manual_seed(0)
+    m = cifar_model_dict[name][0](num_classes=100).eval()
+    x = torch.randn(2, 3, 32, 32)
+    with torch.no_grad():
+        logits, f = m(x)
+    assert logits.shape == (2, 100)
+    feats, pre = f["feats"], f["preact_feats"]
+    assert len(feats) == len(pre) and len(feats) >= 4
+    chans = m.get_stage_channels()
+    assert len(chans) == len(feats), (name, chans, [t.shape for t in feats])
+    for t, c in zip(feats, chans):
+        assert t.shape[0] == 2 and t.shape[1] == c
+    assert f["pooled_feat"].shape[0] == 2
+    if name in PARAMS_M:
+        n = sum(p.numel() for p in m.parameters()) / 1e6
+        assert abs(n - PARAMS_M[name]) < 0.01, (name, n)
+
+
+@pytest.mark.parametrize("name", sorted(cifar_model_dict))
+def test_staged_forward_equivalence(name):
+    torch.manual_seed(0)
+    m = cifar_model_dict[name][0](num_classes=100)
+    res = check_staged_forward(m, torch.randn(2, 3, 32, 32))
+    assert res["all"], res
+
+
+def test_bn_before_relu_matches_stages():
+    m = cifar_model_dict["resnet32x4"][0](num_classes=100)
+    bns = m.get_bn_before_relu()
+    assert [b.num_features for b in bns] == m.get_stage_channels()[1:]
+
+
+@pytest.mark.parametrize("name", sorted(tiny_imagenet_model_dict))
+def test_tiny_imagenet_models(name):
+    m = tiny_imagenet_model_dict[name][0](num_classes=200).eval()
+    with torch.no_grad():
+        logits, f = m(torch.randn(2, 3, 64, 64))
+    assert logits.shape == (2, 200)  # ShuffleV2 at 64^2 works (reference D8 crashes)
+
+
+@pytest.mark.parametrize("name", ["ResNet18", "ResNet34", "ResNet50", "MobileNetV1"])
+def test_imagenet_cnns(name):
+    m = imagenet_model_dict[name](pretrained=False, num_classes=1000).eval()
+    with torch.no_grad():
+        logits, f = m(torch.randn(1, 3, 224, 224))
+    assert logits.shape == (1, 1000)
+    assert len(f["feats"]) == 5  # stem + 4 stages
+    assert [t.shape[1] for t in f["feats"]] == m.get_stage_channels()
+    res = check_staged_forward(m, torch.randn(1, 3, 96, 96))
+    assert res["all"], res
+
+
+def test_vit_tiny_forward():
+    m = imagenet_model_dict["vit_tiny"](pretrained=False, num_classes=1000).eval()
+    with torch.no_grad():
+        logits, f = m(torch.randn(1, 3, 224, 224))
+    assert logits.shape == (1, 1000)
+    assert m.get_arch() == "transformer"

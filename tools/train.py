@@ -27,9 +27,12 @@ def experiment_name_of(cfg, opts):
     name = cfg.EXPERIMENT.NAME or cfg.EXPERIMENT.TAG
     tags = cfg.EXPERIMENT.TAG.split(",")
     if opts:
-        extra = ["{}:{}".format(k, v) for k, v in zip(opts[::2], opts[1::2])]
+        extra = ["{}:{}".format(k, str(v).replace(os.sep, "_")) for k, v in zip(opts[::2], opts[1::2])]
         tags += extra
         name += ",".join(extra)
+    if len(name) > 160:  # keep the directory name within filesystem limits
+        import hashlib
+        name = name[:140] + "-" + hashlib.sha1(name.encode()).hexdigest()[:12]
     return os.path.join(cfg.EXPERIMENT.PROJECT, name), tags
 
 

@@ -36,6 +36,15 @@ SIGNATURES = {
     # convolution (csrc/conv_igemm.hip)
     "mda_conv_fwd": "pppppppp" + "i" * 15 + "s",
     "mda_conv_plan": "iiipp",
+    "mda_conv_dgrad": "pppp" + "i" * 14 + "s",
+    "mda_conv_wgrad": "pppp" + "i" * 13 + "fis",
+    "mda_wgrad_plan": "iiip",
+    "mda_pack_conv_weights": "ppp" + "i" * 6 + "s",
+    # training-mode BatchNorm (csrc/bn.hip)
+    "mda_bn_stats": "pii" + "pp" + "pppp" + "pppp" + "ffs",
+    "mda_bn_apply": "pppppp" + "iii" + "s",
+    "mda_bn_bwd_reduce": "pppppppp" + "iii" + "ppppp" + "s",
+    "mda_bn_bwd_apply": "p" * 11 + "iii" + "s",
     # CRD memory (csrc/crd.hip)
     "mda_crd_scores": "ppppiiifs",
     "mda_crd_grad": "ppppppiiifs",

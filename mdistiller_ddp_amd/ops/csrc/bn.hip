@@ -1,0 +1,286 @@
+// Training-mode BatchNorm (+ residual + activation) around the MFMA convs
+// (survey K1, student side).  NHWC bf16 activations viewed as [M, C] with
+// M = N*H*W; fp32 statistics.
+//
+// forward:   stats   (y -> mean, rstd, scale = g*rstd, shift = b - mean*scale,
+//                     running-stat update)               one launch, last
+//                                                          arriver finalises
+//            apply   z = y*scale + shift (+ res) ; out = act(z) (+ preact z)
+// backward:  reduce  dz = dout * act'(z) (+ dpreact) ; dbeta = sum dz,
+//                     dgamma = sum dz*xhat  -> accumulated into the flat
+//                     gradient buffer, last arriver finalises
+//            apply   dy = scale * (dz - (dbeta + xhat*dgamma)/M) ; dres = dz
+//
+// versus MIOpen's 4 forward + 3 backward BN kernels plus separate add / ReLU
+// (and its backward) launches per layer in the reference stack.
+// Reductions are deterministic: fixed per-block partials in fp32, combined
+// in a fixed order in fp64 by the last-arriving block.
+#include "common.h"
+
+namespace {
+
+constexpr int CBLK = 64;    // channels per block (one per lane)
+constexpr int RWAVES = 4;   // row-parallel waves per block
+
+enum { ACT_NONE = 0, ACT_RELU = 1, ACT_RELU6 = 2 };
+
+__device__ __forceinline__ float act_f(float v, int act) {
+  if (act == ACT_RELU) return fmaxf(v, 0.f);
+  if (act == ACT_RELU6) return fminf(fmaxf(v, 0.f), 6.f);
+  return v;
+}
+__device__ __forceinline__ float act_grad(float z, int act) {
+  if (act == ACT_RELU) return z > 0.f ? 1.f : 0.f;
+  if (act == ACT_RELU6) return (z > 0.f && z < 6.f) ? 1.f : 0.f;
+  return 1.f;
+}
+
+// grid: (ceil(C/64), RB row-blocks). Each thread: one channel, strided rows.
+__global__ void __launch_bounds__(256)
+bn_stats_kernel(const bf16_t* __restrict__ y, int M, int C, float* __restrict__ partial,
+                unsigned* __restrict__ counter, const float* __restrict__ gamma,
+                const float* __restrict__ beta, float* __restrict__ running_mean,
+                float* __restrict__ running_var, float* __restrict__ mean_out,
+                float* __restrict__ rstd_out, float* __restrict__ scale_out,
+                float* __restrict__ shift_out, float momentum, float eps) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * CBLK + lane;
+  const int rb = blockIdx.y, nrb = gridDim.y;
+  float s = 0.f, ss = 0.f;
+  if (c < C) {
+    for (int m = rb * RWAVES + w; m < M; m += nrb * RWAVES) {
+      float v = bf2f(y[(int64_t)m * C + c]);
+      s += v;
+      ss += v * v;
+    }
+  }
+  __shared__ float red[2][RWAVES][CBLK];
+  red[0][w][lane] = s;
+  red[1][w][lane] = ss;
+  __syncthreads();
+  if (w == 0) {
+    float a = 0.f, b = 0.f;
+    for (int i = 0; i < RWAVES; ++i) { a += red[0][i][lane]; b += red[1][i][lane]; }
+    if (c < C) {
+      partial[((int64_t)rb * 2 + 0) * C + c] = a;
+      partial[((int64_t)rb * 2 + 1) * C + c] = b;
+    }
+  }
+  // last row-block of this channel group finalises (counter per channel group)
+  if (mda_arrive(counter + blockIdx.x, nrb)) {
+    if (w == 0 && c < C) {
+      double a = 0.0, b = 0.0;
+      for (int r = 0; r < nrb; ++r) {
+        a += partial[((int64_t)r * 2 + 0) * C + c];
+        b += partial[((int64_t)r * 2 + 1) * C + c];
+      }
+      const double mean = a / M;
+      double var = b / M - mean * mean;
+      if (var < 0) var = 0;
+      const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+      const float g = gamma ? gamma[c] : 1.f;
+      const float bb = beta ? beta[c] : 0.f;
+      mean_out[c] = (float)mean;
+      rstd_out[c] = rstd;
+      scale_out[c] = g * rstd;
+      shift_out[c] = bb - (float)mean * g * rstd;
+      if (running_mean) {
+        const double unbiased = M > 1 ? var * M / (M - 1) : var;
+        running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+        running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unbiased;
+      }
+    }
+  }
+}
+
+// 8 channels (16 bytes) per thread-iteration; C % 8 == 0.
+__global__ void __launch_bounds__(256)
+bn_apply_kernel(const bf16_t* __restrict__ y, const float* __restrict__ scale,
+                const float* __restrict__ shift, const bf16_t* __restrict__ res,
+                bf16_t* __restrict__ out, bf16_t* __restrict__ preact, int64_t M, int C, int act) {
+  const int64_t total = M * C / 8;
+  const int c8 = C / 8;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % c8) * 8;
+    uint4 yv = ((const uint4*)y)[i];
+    uint4 rv = res ? ((const uint4*)res)[i] : make_uint4(0, 0, 0, 0);
+    const bf16_t* yp = (const bf16_t*)&yv;
+    const bf16_t* rp = (const bf16_t*)&rv;
+    bf16_t o[8], z[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float v = bf2f(yp[k]) * scale[c0 + k] + shift[c0 + k];
+      if (res) v += bf2f(rp[k]);
+      z[k] = f2bf(v);
+      o[k] = f2bf(act_f(v, act));
+    }
+    ((uint4*)out)[i] = *(uint4*)o;
+    if (preact) ((uint4*)preact)[i] = *(uint4*)z;
+  }
+}
+
+// dz = dout * act'(z) (+ dpre); partial sums of dz and dz*xhat per channel.
+// z is recovered from y: z = y*scale + shift (+ res); so the mask needs y,
+// scale, shift and res, not a stored z.
+__global__ void __launch_bounds__(256)
+bn_bwd_reduce_kernel(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ dpre,
+                     const bf16_t* __restrict__ y, const bf16_t* __restrict__ res,
+                     const float* __restrict__ scale, const float* __restrict__ shift,
+                     const float* __restrict__ mean, const float* __restrict__ rstd, int M, int C,
+                     int act, float* __restrict__ partial, unsigned* __restrict__ counter,
+                     float* __restrict__ sums, float* __restrict__ dgamma,
+                     float* __restrict__ dbeta) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * CBLK + lane;
+  const int rb = blockIdx.y, nrb = gridDim.y;
+  float sdz = 0.f, sdzx = 0.f;
+  if (c < C) {
+    const float sc = scale[c], sh = shift[c], mu = mean[c], rs = rstd[c];
+    for (int m = rb * RWAVES + w; m < M; m += nrb * RWAVES) {
+      const int64_t o = (int64_t)m * C + c;
+      const float yv = bf2f(y[o]);
+      float dz = dout ? bf2f(dout[o]) : 0.f;
+      if (act != ACT_NONE) {
+        float z = yv * sc + sh;
+        if (res) z += bf2f(res[o]);
+        dz *= act_grad(z, act);
+      }
+      if (dpre) dz += bf2f(dpre[o]);
+      sdz += dz;
+      sdzx += dz * (yv - mu) * rs;
+    }
+  }
+  __shared__ float red[2][RWAVES][CBLK];
+  red[0][w][lane] = sdz;
+  red[1][w][lane] = sdzx;
+  __syncthreads();
+  if (w == 0) {
+    float a = 0.f, b = 0.f;
+    for (int i = 0; i < RWAVES; ++i) { a += red[0][i][lane]; b += red[1][i][lane]; }
+    if (c < C) {
+      partial[((int64_t)rb * 2 + 0) * C + c] = a;
+      partial[((int64_t)rb * 2 + 1) * C + c] = b;
+    }
+  }
+  if (mda_arrive(counter + blockIdx.x, nrb)) {
+    if (w == 0 && c < C) {
+      double a = 0.0, b = 0.0;
+      for (int r = 0; r < nrb; ++r) {
+        a += partial[((int64_t)r * 2 + 0) * C + c];
+        b += partial[((int64_t)r * 2 + 1) * C + c];
+      }
+      sums[c] = (float)a;          // sum dz      (= dbeta)
+      sums[C + c] = (float)b;      // sum dz*xhat (= dgamma)
+      if (dbeta) dbeta[c] += (float)a;
+      if (dgamma) dgamma[c] += (float)b;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256)
+bn_bwd_apply_kernel(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ dpre,
+                    const bf16_t* __restrict__ y, const bf16_t* __restrict__ res,
+                    const float* __restrict__ scale, const float* __restrict__ shift,
+                    const float* __restrict__ mean, const float* __restrict__ rstd,
+                    const float* __restrict__ sums, bf16_t* __restrict__ dy,
+                    bf16_t* __restrict__ dres, int64_t M, int C, int act) {
+  const int64_t total = M * C / 8;
+  const int c8 = C / 8;
+  const float invM = 1.f / (float)M;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % c8) * 8;
+    uint4 yv = ((const uint4*)y)[i];
+    uint4 dv = dout ? ((const uint4*)dout)[i] : make_uint4(0, 0, 0, 0);
+    uint4 pv = dpre ? ((const uint4*)dpre)[i] : make_uint4(0, 0, 0, 0);
+    uint4 rv = (res && act != ACT_NONE) ? ((const uint4*)res)[i] : make_uint4(0, 0, 0, 0);
+    const bf16_t* yp = (const bf16_t*)&yv;
+    const bf16_t* dp = (const bf16_t*)&dv;
+    const bf16_t* pp = (const bf16_t*)&pv;
+    const bf16_t* rp = (const bf16_t*)&rv;
+    bf16_t o[8], r[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = c0 + k;
+      const float yf = bf2f(yp[k]);
+      float dz = bf2f(dp[k]);
+      if (act != ACT_NONE) {
+        float z = yf * scale[c] + shift[c];
+        if (res) z += bf2f(rp[k]);
+        dz *= act_grad(z, act);
+      }
+      if (dpre) dz += bf2f(pp[k]);
+      const float xhat = (yf - mean[c]) * rstd[c];
+      const float g = scale[c] * (dz - (sums[c] + xhat * sums[C + c]) * invM);
+      o[k] = f2bf(g);
+      r[k] = f2bf(dz);
+    }
+    ((uint4*)dy)[i] = *(uint4*)o;
+    if (dres) ((uint4*)dres)[i] = *(uint4*)r;
+  }
+}
+
+inline int row_blocks(int64_t M) {
+  // ~ 2048 rows per row-block, capped so partials stay small
+  int64_t rb = (M + 2047) / 2048;
+  if (rb < 1) rb = 1;
+  if (rb > 256) rb = 256;
+  return (int)rb;
+}
+
+inline int ew_blocks(int64_t n8) {
+  int64_t b = (n8 + 255) / 256;
+  if (b > 4096) b = 4096;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+}  // namespace
+
+// Workspace: partial >= 2*C*256 floats; counter >= ceil(C/64) zeroed uints.
+MDA_API int mda_bn_stats(const void* y, int64_t M, int64_t C, float* partial, unsigned* counter,
+                         const float* gamma, const float* beta, float* running_mean,
+                         float* running_var, float* mean, float* rstd, float* scale,
+                         float* shift, float momentum, float eps, hipStream_t st) {
+  dim3 grid((int)((C + CBLK - 1) / CBLK), row_blocks(M));
+  hipLaunchKernelGGL(bn_stats_kernel, grid, dim3(256), 0, st, (const bf16_t*)y, (int)M, (int)C,
+                     partial, counter, gamma, beta, running_mean, running_var, mean, rstd, scale,
+                     shift, momentum, eps);
+  MDA_CHECK_LAUNCH();
+}
+
+MDA_API int mda_bn_apply(const void* y, const float* scale, const float* shift, const void* res,
+                         void* out, void* preact, int64_t M, int64_t C, int64_t act,
+                         hipStream_t st) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_blocks(M * C / 8)), dim3(256), 0, st,
+                     (const bf16_t*)y, scale, shift, (const bf16_t*)res, (bf16_t*)out,
+                     (bf16_t*)preact, M, (int)C, (int)act);
+  MDA_CHECK_LAUNCH();
+}
+
+// sums: 2*C floats out (sum dz, sum dz*xhat); dgamma/dbeta accumulated (may be null).
+MDA_API int mda_bn_bwd_reduce(const void* dout, const void* dpre, const void* y, const void* res,
+                              const float* scale, const float* shift, const float* mean,
+                              const float* rstd, int64_t M, int64_t C, int64_t act,
+                              float* partial, unsigned* counter, float* sums, float* dgamma,
+                              float* dbeta, hipStream_t st) {
+  dim3 grid((int)((C + CBLK - 1) / CBLK), row_blocks(M));
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, grid, dim3(256), 0, st, (const bf16_t*)dout,
+                     (const bf16_t*)dpre, (const bf16_t*)y, (const bf16_t*)res, scale, shift,
+                     mean, rstd, (int)M, (int)C, (int)act, partial, counter, sums, dgamma, dbeta);
+  MDA_CHECK_LAUNCH();
+}
+
+MDA_API int mda_bn_bwd_apply(const void* dout, const void* dpre, const void* y, const void* res,
+                             const float* scale, const float* shift, const float* mean,
+                             const float* rstd, const float* sums, void* dy, void* dres,
+                             int64_t M, int64_t C, int64_t act, hipStream_t st) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_blocks(M * C / 8)), dim3(256), 0, st,
+                     (const bf16_t*)dout, (const bf16_t*)dpre, (const bf16_t*)y,
+                     (const bf16_t*)res, scale, shift, mean, rstd, sums, (bf16_t*)dy,
+                     (bf16_t*)dres, M, (int)C, (int)act);
+  MDA_CHECK_LAUNCH();
+}

@@ -39,7 +39,7 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 constexpr int BK = 64;
 constexpr int LDS_ROW = 72;  // bf16 elements per LDS row (64 + 8 pad = 144 B)
 
-enum { LOAD_FAST = 0, LOAD_VEC8 = 1, LOAD_SCALAR = 2 };
+enum { LOAD_FAST = 0, LOAD_VEC8 = 1, LOAD_SCALAR = 2, LOAD_DGRAD_FAST = 3, LOAD_DGRAD_VEC8 = 4 };
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_RELU6 = 2 };
 
 struct ConvParams {
@@ -102,8 +102,15 @@ conv_fwd_kernel(const ConvParams p) {
     int oh = r / p.Wo;
     int ow = r - oh * p.Wo;
     a_n[j] = n;
-    a_ih0[j] = oh * p.stride - p.pad;
-    a_iw0[j] = ow * p.stride - p.pad;
+    if (MODE == LOAD_DGRAD_FAST || MODE == LOAD_DGRAD_VEC8) {
+      // dgrad: output row = input-gradient pixel (ih, iw); taps gather dy at
+      // oh = (ih + pad - kh) / stride when divisible and in range
+      a_ih0[j] = oh + p.pad;
+      a_iw0[j] = ow + p.pad;
+    } else {
+      a_ih0[j] = oh * p.stride - p.pad;
+      a_iw0[j] = ow * p.stride - p.pad;
+    }
   }
 
   uint4 ra[AROWS];
@@ -135,6 +142,34 @@ conv_fwd_kernel(const ConvParams p) {
       for (int j = 0; j < AROWS; ++j) {
         int ih = a_ih0[j] + kh, iw = a_iw0[j] + kw;
         bool ok = kok && a_ok[j] && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+        ra[j] = ok ? *(const uint4*)(p.x + (((int64_t)a_n[j] * p.H + ih) * p.W + iw) * p.Cin + c0)
+                   : make_uint4(0, 0, 0, 0);
+      }
+    } else if (MODE == LOAD_DGRAD_FAST || MODE == LOAD_DGRAD_VEC8) {
+      int tap, c0;
+      bool kok = true;
+      if (MODE == LOAD_DGRAD_FAST) {
+        tap = s / cin_blocks;
+        c0 = (s - tap * cin_blocks) * BK + chunk * 8;
+      } else {
+        const int k0 = s * BK + chunk * 8;
+        tap = k0 / p.Cin;
+        c0 = k0 - tap * p.Cin;
+        kok = k0 < p.K;
+      }
+      const int kh = tap / p.KW, kw = tap - kh * p.KW;
+#pragma unroll
+      for (int j = 0; j < AROWS; ++j) {
+        const int nh = a_ih0[j] - kh, nw = a_iw0[j] - kw;
+        bool ok = kok && a_ok[j] && nh >= 0 && nw >= 0;
+        int ih = 0, iw = 0;
+        if (p.stride == 1) {
+          ih = nh; iw = nw;
+        } else {
+          ok = ok && (nh % p.stride == 0) && (nw % p.stride == 0);
+          ih = nh / p.stride; iw = nw / p.stride;
+        }
+        ok = ok && ih < p.H && iw < p.W;
         ra[j] = ok ? *(const uint4*)(p.x + (((int64_t)a_n[j] * p.H + ih) * p.W + iw) * p.Cin + c0)
                    : make_uint4(0, 0, 0, 0);
       }
@@ -256,6 +291,10 @@ int launch_tile(const ConvParams& p, int mode, int splits, hipStream_t st) {
     hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, LOAD_FAST>), grid, dim3(256), 0, st, p);
   else if (mode == LOAD_VEC8)
     hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, LOAD_VEC8>), grid, dim3(256), 0, st, p);
+  else if (mode == LOAD_DGRAD_FAST)
+    hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, LOAD_DGRAD_FAST>), grid, dim3(256), 0, st, p);
+  else if (mode == LOAD_DGRAD_VEC8)
+    hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, LOAD_DGRAD_VEC8>), grid, dim3(256), 0, st, p);
   else
     hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, LOAD_SCALAR>), grid, dim3(256), 0, st, p);
   return (int)hipGetLastError();
@@ -281,6 +320,33 @@ MDA_API int mda_conv_plan(int64_t M, int64_t Cout, int64_t Kp, int64_t* tile, in
   return 0;
 }
 
+namespace {
+
+int dispatch(ConvParams& p, int mode, int64_t tile, int64_t splits, hipStream_t st) {
+  if (p.Kp % BK || p.Kp < p.K) return (int)hipErrorInvalidValue;
+  if (tile == 0 || splits == 0) mda_conv_plan(p.M, p.Cout, p.Kp, &tile, &splits);
+  if (splits > 1 && p.partial == nullptr) return (int)hipErrorInvalidValue;
+  const int steps = p.Kp / BK;
+  p.steps_per_split = (int)((steps + splits - 1) / splits);
+  int rc;
+  switch (tile) {
+    case 128128: rc = launch_tile<128, 128>(p, mode, splits, st); break;
+    case 128064: rc = launch_tile<128, 64>(p, mode, splits, st); break;
+    case 128032: rc = launch_tile<128, 32>(p, mode, splits, st); break;
+    case 64128: rc = launch_tile<64, 128>(p, mode, splits, st); break;
+    case 64064: rc = launch_tile<64, 64>(p, mode, splits, st); break;
+    case 64032: rc = launch_tile<64, 32>(p, mode, splits, st); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  if (rc || splits <= 1) return rc;
+  int64_t total = (int64_t)p.M * p.Cout;
+  int blocks = (int)std::min<int64_t>((total + 255) / 256, 2048);
+  hipLaunchKernelGGL(conv_splitk_epilogue, dim3(blocks), dim3(256), 0, st, p, (int)splits);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
 // tile/splits: 0 = auto (mda_conv_plan).  partial: fp32 workspace of
 // splits*M*Cout floats (may be null when splits == 1).
 MDA_API int mda_conv_fwd(const void* x, const void* w, const float* scale, const float* bias,
@@ -294,25 +360,26 @@ MDA_API int mda_conv_fwd(const void* x, const void* w, const float* scale, const
   p.N = N; p.H = H; p.W = W; p.Cin = Cin; p.Ho = Ho; p.Wo = Wo; p.Cout = Cout; p.KH = KH;
   p.KW = KW; p.stride = stride; p.pad = pad; p.K = KH * KW * Cin; p.Kp = Kp; p.M = N * Ho * Wo;
   p.act = act;
-  if (Kp % BK || Kp < p.K) return (int)hipErrorInvalidValue;
   int mode = (Cin % BK == 0) ? LOAD_FAST : (Cin % 8 == 0 ? LOAD_VEC8 : LOAD_SCALAR);
-  if (tile == 0 || splits == 0) mda_conv_plan(p.M, Cout, Kp, &tile, &splits);
-  if (splits > 1 && partial == nullptr) return (int)hipErrorInvalidValue;
-  const int steps = Kp / BK;
-  p.steps_per_split = (int)((steps + splits - 1) / splits);
-  int rc;
-  switch (tile) {
-    case 128128: rc = launch_tile<128, 128>(p, mode, splits, st); break;
-    case 128064: rc = launch_tile<128, 64>(p, mode, splits, st); break;
-    case 128032: rc = launch_tile<128, 32>(p, mode, splits, st); break;
-    case 64128: rc = launch_tile<64, 128>(p, mode, splits, st); break;
-    case 64064: rc = launch_tile<64, 64>(p, mode, splits, st); break;
-    case 64032: rc = launch_tile<64, 32>(p, mode, splits, st); break;
-    default: return (int)hipErrorInvalidValue;
-  }
-  if (rc || splits <= 1) return rc;
-  int64_t total = p.M * Cout;
-  int blocks = (int)std::min<int64_t>((total + 255) / 256, 2048);
-  hipLaunchKernelGGL(conv_splitk_epilogue, dim3(blocks), dim3(256), 0, st, p, (int)splits);
-  MDA_CHECK_LAUNCH();
+  return dispatch(p, mode, tile, splits, st);
+}
+
+// Input gradient of a convolution (any stride): dx[N, H, W, Cin] =
+// sum_{kh,kw,co} dy[N, (ih+pad-kh)/s, (iw+pad-kw)/s, co] * w[co, ci, kh, kw].
+// wt: weights packed [Cin][Kp] with k = (kh*KW + kw)*Cout + co (mda_pack_conv_weights).
+// dy: [N, Ho, Wo, Cout]; requires Cout % 8 == 0.
+MDA_API int mda_conv_dgrad(const void* dy, const void* wt, void* dx, float* partial, int64_t N,
+                           int64_t H, int64_t W, int64_t Cin, int64_t Ho, int64_t Wo,
+                           int64_t Cout, int64_t KH, int64_t KW, int64_t stride, int64_t pad,
+                           int64_t Kp, int64_t tile, int64_t splits, hipStream_t st) {
+  if (Cout % 8) return (int)hipErrorInvalidValue;
+  ConvParams p;
+  p.x = (const bf16_t*)dy; p.w = (const bf16_t*)wt; p.scale = nullptr; p.bias = nullptr;
+  p.res = nullptr; p.y = (bf16_t*)dx; p.preact = nullptr; p.partial = partial;
+  // GEMM view: rows = dx pixels, cols = Cin, k = (tap, co); "input" image = dy
+  p.N = N; p.H = Ho; p.W = Wo; p.Cin = Cout; p.Ho = H; p.Wo = W; p.Cout = Cin; p.KH = KH;
+  p.KW = KW; p.stride = stride; p.pad = pad; p.K = KH * KW * Cout; p.Kp = Kp; p.M = N * H * W;
+  p.act = 0;
+  int mode = (Cout % BK == 0) ? LOAD_DGRAD_FAST : LOAD_DGRAD_VEC8;
+  return dispatch(p, mode, tile, splits, st);
 }

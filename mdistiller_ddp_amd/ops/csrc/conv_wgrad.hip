@@ -1,0 +1,282 @@
+// Convolution weight gradient on MFMA + fp32 master-weight plumbing.
+//
+// wgrad:  dW[co, k] = sum_m dy[m, co] * A[m, k]     (A = im2col(x), k = (kh*KW+kw)*Cin + ci)
+//
+// The reduction runs over output pixels m, which is the OUTER (row) index of
+// both NHWC operands, so both tiles are staged into LDS as natural
+// [m][channel] rows (16-byte global loads) and the MFMA fragments -- which
+// want 8 consecutive m per lane -- are read with the CDNA4 transposing LDS
+// read ds_read_b64_tr_b16 (two per fragment).  Block tile 64 co x 64 k,
+// 4 waves as 2x2 (32x32 per wave, 16x16x32 bf16 MFMA), 64 pixels per stage,
+// register-prefetched double buffer.  The pixel range is split over
+// gridDim.z (M = N*Ho*Wo is 65536 for a 32x32 stage at batch 64) and the
+// fp32 partials are combined by mda_wgrad_reduce in a fixed order, which
+// also scatters into the OIHW fp32 gradient and ACCUMULATES into it (the
+// flat gradient buffer the optimizer reads) -- no separate grad cast/add.
+//
+// pack:   fp32 OIHW master weights -> bf16 [Cout][Kp] (forward operand) and,
+//         optionally, bf16 [Cin][KpT] with k = (kh*KW+kw)*Cout + co (dgrad
+//         operand), in one launch per conv per step.
+#include "common.h"
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+constexpr int TM = 64;       // pixels per stage
+constexpr int TC = 64;       // co per block
+constexpr int TK = 64;       // k per block
+constexpr int ROW = 72;      // LDS row length (bf16), 144 B
+
+enum { WG_FAST = 0, WG_VEC8 = 1, WG_SCALAR = 2 };
+
+struct WgParams {
+  const bf16_t* x;   // [N, H, W, Cin]
+  const bf16_t* dy;  // [N, Ho, Wo, Cout]
+  float* partial;    // [splits, Cout, Kp]
+  int N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, K, Kp, M, m_per_split;
+};
+
+__device__ __forceinline__ bf16x8 tr_frag(const bf16_t* tile, int r0, int c0, int lane) {
+  // lane 16g + 4q + p supplies &tile[r0 + 8g + q (+4)][c0 + 4p]; receives column (lane & 15)
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  const bf16_t* a0 = tile + (r0 + 8 * g + q) * ROW + c0 + 4 * p;
+  const bf16_t* a1 = a0 + 4 * ROW;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1));
+  bf16x8 out;
+  short* o = (short*)&out;
+  o[0] = lo[0]; o[1] = lo[1]; o[2] = lo[2]; o[3] = lo[3];
+  o[4] = hi[0]; o[5] = hi[1]; o[6] = hi[2]; o[7] = hi[3];
+  return out;
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(256)
+conv_wgrad_kernel(const WgParams p) {
+  __shared__ __attribute__((aligned(16))) bf16_t Ds[2][TM * ROW];  // dy tile [m][co]
+  __shared__ __attribute__((aligned(16))) bf16_t Xs[2][TM * ROW];  // im2col tile [m][k]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int co0 = blockIdx.x * TC;
+  const int k0 = blockIdx.y * TK;
+  const int m_begin = blockIdx.z * p.m_per_split;
+  const int m_end = min(p.M, m_begin + p.m_per_split);
+  const int chunk = tid & 7, row = tid >> 3;  // 32 rows x 8 chunks per pass, 2 passes
+  const int HoWo = p.Ho * p.Wo;
+
+  // FAST mode: the whole 64-wide k tile is one tap
+  int tap_fast = 0, c_fast = 0;
+  if (MODE == WG_FAST) {
+    tap_fast = k0 / p.Cin;
+    c_fast = k0 - tap_fast * p.Cin;
+  }
+
+  uint4 rd[2], rx[2];
+  auto load = [&](int mb) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int r = row + 32 * j;
+      const int m = mb + r;
+      const bool mok = m < m_end;
+      const int co = co0 + chunk * 8;
+      rd[j] = (mok && co < p.Cout) ? *(const uint4*)(p.dy + (int64_t)m * p.Cout + co)
+                                   : make_uint4(0, 0, 0, 0);
+      int n = 0, oh = 0, ow = 0;
+      if (mok) {
+        n = m / HoWo;
+        int rr = m - n * HoWo;
+        oh = rr / p.Wo;
+        ow = rr - oh * p.Wo;
+      }
+      if (MODE == WG_FAST || MODE == WG_VEC8) {
+        int tap, c;
+        bool kok = true;
+        if (MODE == WG_FAST) {
+          tap = tap_fast;
+          c = c_fast + chunk * 8;
+        } else {
+          const int kk = k0 + chunk * 8;
+          tap = kk / p.Cin;
+          c = kk - tap * p.Cin;
+          kok = kk < p.K;
+        }
+        const int kh = tap / p.KW, kw = tap - kh * p.KW;
+        const int ih = oh * p.stride - p.pad + kh, iw = ow * p.stride - p.pad + kw;
+        const bool ok = kok && mok && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+        rx[j] = ok ? *(const uint4*)(p.x + (((int64_t)n * p.H + ih) * p.W + iw) * p.Cin + c)
+                   : make_uint4(0, 0, 0, 0);
+      } else {
+        bf16_t v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int kk = k0 + chunk * 8 + e;
+          const int tap = kk / p.Cin;
+          const int c = kk - tap * p.Cin;
+          const int kh = tap / p.KW, kw = tap - kh * p.KW;
+          const int ih = oh * p.stride - p.pad + kh, iw = ow * p.stride - p.pad + kw;
+          const bool ok = kk < p.K && mok && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+          v[e] = ok ? p.x[(((int64_t)n * p.H + ih) * p.W + iw) * p.Cin + c] : (bf16_t)0;
+        }
+        rx[j] = *(uint4*)v;
+      }
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int r = row + 32 * j;
+      *(uint4*)&Ds[buf][r * ROW + chunk * 8] = rd[j];
+      *(uint4*)&Xs[buf][r * ROW + chunk * 8] = rx[j];
+    }
+  };
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nst = (m_end - m_begin + TM - 1) / TM;
+  if (nst > 0) {
+    load(m_begin);
+    store(0);
+  }
+  __syncthreads();
+  for (int s = 0; s < nst; ++s) {
+    const int buf = s & 1;
+    const bool more = s + 1 < nst;
+    if (more) load(m_begin + (s + 1) * TM);
+#pragma unroll
+    for (int kk = 0; kk < TM; kk += 32) {
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = tr_frag(Ds[buf], kk, wm * 32 + i * 16, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bfr[j] = tr_frag(Xs[buf], kk, wn * 32 + j * 16, lane);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) store(buf ^ 1);
+    __syncthreads();
+  }
+  const int ecol = lane & 15, erow = (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + wm * 32 + i * 16 + erow + r;
+        const int k = k0 + wn * 32 + j * 16 + ecol;
+        if (co < p.Cout && k < p.Kp)
+          p.partial[((int64_t)blockIdx.z * p.Cout + co) * p.Kp + k] = acc[i][j][r];
+      }
+}
+
+// grad[co][ci][kh][kw] += scale * sum_s partial[s][co][(kh*KW+kw)*Cin+ci]
+__global__ void __launch_bounds__(256)
+wgrad_reduce_kernel(const float* __restrict__ partial, float* __restrict__ grad, int splits,
+                    int Cout, int Cin, int KH, int KW, int Kp, float scale, int accumulate) {
+  const int K = Cin * KH * KW;
+  const int64_t total = (int64_t)Cout * K;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int co = (int)(i / K);
+    const int r = (int)(i - (int64_t)co * K);        // OIHW order: ci, kh, kw
+    const int ci = r / (KH * KW);
+    const int t = r - ci * KH * KW;
+    const int k = t * Cin + ci;                      // packed order
+    float a = 0.f;
+    for (int s = 0; s < splits; ++s) a += partial[((int64_t)s * Cout + co) * Kp + k];
+    grad[i] = (accumulate ? grad[i] : 0.f) + scale * a;
+  }
+}
+
+__global__ void __launch_bounds__(256)
+pack_kernel(const float* __restrict__ w, bf16_t* __restrict__ wf, bf16_t* __restrict__ wt,
+            int Cout, int Cin, int KH, int KW, int Kp, int KpT) {
+  // one thread per packed-forward element (including the zero padding)
+  const int64_t total = (int64_t)Cout * Kp;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int co = (int)(i / Kp);
+    const int k = (int)(i - (int64_t)co * Kp);
+    float v = 0.f;
+    if (k < KH * KW * Cin) {
+      const int tap = k / Cin, ci = k - (k / Cin) * Cin;
+      const int kh = tap / KW, kw = tap - kh * KW;
+      v = w[(((int64_t)co * Cin + ci) * KH + kh) * KW + kw];
+      if (wt) wt[(int64_t)ci * KpT + tap * Cout + co] = f2bf(v);
+    }
+    wf[i] = f2bf(v);
+  }
+  if (wt) {  // zero the dgrad padding columns
+    const int64_t pad = (int64_t)Cin * (KpT - KH * KW * Cout);
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < pad;
+         i += (int64_t)gridDim.x * blockDim.x) {
+      const int w_ = KpT - KH * KW * Cout;
+      const int ci = (int)(i / w_);
+      const int j = (int)(i - (int64_t)ci * w_);
+      wt[(int64_t)ci * KpT + KH * KW * Cout + j] = 0;
+    }
+  }
+}
+
+}  // namespace
+
+MDA_API int mda_wgrad_plan(int64_t M, int64_t Cout, int64_t Kp, int64_t* splits) {
+  int64_t tiles = ((Cout + TC - 1) / TC) * ((Kp + TK - 1) / TK);
+  int64_t sp = 1;
+  // aim for >= 512 workgroups, keep >= 4 stages (256 pixels) per split
+  while (tiles * sp < 512 && (M / (sp * 2)) >= 4 * TM && sp < 256) sp *= 2;
+  *splits = sp;
+  return 0;
+}
+
+// partial: splits*Cout*Kp floats.  grad: fp32 OIHW, accumulated when accumulate != 0.
+MDA_API int mda_conv_wgrad(const void* x, const void* dy, float* partial, float* grad, int64_t N,
+                           int64_t H, int64_t W, int64_t Cin, int64_t Ho, int64_t Wo, int64_t Cout,
+                           int64_t KH, int64_t KW, int64_t stride, int64_t pad, int64_t Kp,
+                           int64_t splits, float scale, int64_t accumulate, hipStream_t st) {
+  if (Cout % 8 || Kp % TK) return (int)hipErrorInvalidValue;
+  WgParams p;
+  p.x = (const bf16_t*)x; p.dy = (const bf16_t*)dy; p.partial = partial;
+  p.N = N; p.H = H; p.W = W; p.Cin = Cin; p.Ho = Ho; p.Wo = Wo; p.Cout = Cout; p.KH = KH;
+  p.KW = KW; p.stride = stride; p.pad = pad; p.K = KH * KW * Cin; p.Kp = Kp; p.M = N * Ho * Wo;
+  if (splits <= 0) mda_wgrad_plan(p.M, Cout, Kp, &splits);
+  p.m_per_split = (int)(((p.M + splits - 1) / splits + TM - 1) / TM * TM);
+  dim3 grid((int)((Cout + TC - 1) / TC), (int)(Kp / TK), (int)splits);
+  const int mode = (Cin % TK == 0) ? WG_FAST : (Cin % 8 == 0 ? WG_VEC8 : WG_SCALAR);
+  if (mode == WG_FAST)
+    hipLaunchKernelGGL(conv_wgrad_kernel<WG_FAST>, grid, dim3(256), 0, st, p);
+  else if (mode == WG_VEC8)
+    hipLaunchKernelGGL(conv_wgrad_kernel<WG_VEC8>, grid, dim3(256), 0, st, p);
+  else
+    hipLaunchKernelGGL(conv_wgrad_kernel<WG_SCALAR>, grid, dim3(256), 0, st, p);
+  int rc = (int)hipGetLastError();
+  if (rc) return rc;
+  int64_t total = Cout * KH * KW * Cin;
+  int blocks = (int)std::min<int64_t>((total + 255) / 256, 1024);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, partial, grad,
+                     (int)splits, (int)Cout, (int)Cin, (int)KH, (int)KW, (int)Kp, scale,
+                     (int)accumulate);
+  MDA_CHECK_LAUNCH();
+}
+
+// w fp32 [Cout, Cin, KH, KW] -> wf bf16 [Cout, Kp]; wt (optional) bf16 [Cin, KpT]
+MDA_API int mda_pack_conv_weights(const float* w, void* wf, void* wt, int64_t Cout, int64_t Cin,
+                                  int64_t KH, int64_t KW, int64_t Kp, int64_t KpT,
+                                  hipStream_t st) {
+  int64_t total = Cout * Kp;
+  int blocks = (int)std::min<int64_t>((total + 255) / 256, 1024);
+  hipLaunchKernelGGL(pack_kernel, dim3(blocks), dim3(256), 0, st, w, (bf16_t*)wf, (bf16_t*)wt,
+                     (int)Cout, (int)Cin, (int)KH, (int)KW, (int)Kp, (int)KpT);
+  MDA_CHECK_LAUNCH();
+}

@@ -1,0 +1,182 @@
+"""Training-mode conv + BatchNorm (+ residual) (+ activation) on the native kernels.
+
+One autograd node per layer:
+
+forward   pack weights (fp32 OIHW -> bf16 GEMM operands, 1 launch)
+          conv          (MFMA implicit GEMM, raw output y)
+          bn_stats      (batch mean / rstd, scale/shift, running-stat update)
+          bn_apply      (z = y*scale + shift + res, out = act(z), optional preact)
+backward  bn_bwd_reduce (dgamma / dbeta accumulated straight into the flat grad buffer)
+          bn_bwd_apply  (dy, and dz for the residual branch)
+          conv dgrad    (MFMA implicit GEMM over dy, any stride)
+          conv wgrad    (MFMA with ds_read_b64_tr_b16 fragments, accumulated into
+                         the fp32 OIHW grad view of the flat buffer)
+
+Reference numerics are PyTorch's ``F.conv2d`` + ``F.batch_norm(training=True)``
+(+ add + ReLU); ``tests/test_gpu_train_layers.py`` checks values and
+gradients against them.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+import torch.nn as nn
+
+from . import _ext
+
+_ACT = {"none": 0, "relu": 1, "relu6": 2}
+
+
+class _WS:
+    """Per-device scratch for the BN reductions (partials + arrival counters)."""
+
+    def __init__(self, device):
+        self.partial = torch.zeros(2 * 2048 * 256, dtype=torch.float32, device=device)
+        self.counter = torch.zeros(64, dtype=torch.int32, device=device)
+
+
+_WSS: dict = {}
+
+
+def _ws(device):
+    key = torch.device(device).index or 0
+    w = _WSS.get(key)
+    if w is None:
+        w = _WSS[key] = _WS(device)
+    return w
+
+
+_WG_PLANS: dict = {}
+
+
+def _wgrad_splits(M, Cout, Kp):
+    key = (M, Cout, Kp)
+    v = _WG_PLANS.get(key)
+    if v is None:
+        s = ctypes.c_int64(0)
+        _ext.call("mda_wgrad_plan", M, Cout, Kp, s)
+        v = _WG_PLANS[key] = s.value
+    return v
+
+
+def _cl_bf16(t):
+    if t.dtype != torch.bfloat16:
+        t = t.to(torch.bfloat16)
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+def train_supported(x, conv, bn) -> bool:
+    if not (x.is_cuda and x.dim() == 4 and isinstance(conv, nn.Conv2d)):
+        return False
+    if bn is None or not bn.training or not bn.track_running_stats or bn.momentum is None:
+        return False
+    if conv.groups != 1 or conv.dilation != (1, 1) or conv.padding_mode != "zeros" or conv.bias is not None:
+        return False
+    if conv.stride[0] != conv.stride[1] or not isinstance(conv.padding, tuple) or conv.padding[0] != conv.padding[1]:
+        return False
+    if conv.kernel_size[0] != conv.kernel_size[1]:
+        return False
+    if conv.out_channels % 8 or (conv.in_channels % 8 and x.requires_grad):
+        return False
+    if bn.weight is None or bn.bias is None:
+        return False
+    if x.dtype != torch.bfloat16 and not (torch.is_autocast_enabled("cuda")
+                                          and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+        return False
+    return torch.is_grad_enabled()
+
+
+class _ConvBNActTrain(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, gamma, beta, residual, meta, bn, want_preact):
+        stride, pad, act = meta
+        x = _cl_bf16(x)
+        N, Cin, H, W = x.shape
+        Cout, _, KH, KW = weight.shape
+        Ho = (H + 2 * pad - KH) // stride + 1
+        Wo = (W + 2 * pad - KW) // stride + 1
+        M = N * Ho * Wo
+        K = KH * KW * Cin
+        Kp = (K + 63) // 64 * 64
+        need_dx = ctx.needs_input_grad[0]
+        KpT = (KH * KW * Cout + 63) // 64 * 64
+        dev = x.device
+        wf = torch.empty(Cout, Kp, dtype=torch.bfloat16, device=dev)
+        wt = torch.empty(Cin, KpT, dtype=torch.bfloat16, device=dev) if need_dx else None
+        _ext.call("mda_pack_conv_weights", weight.detach().contiguous(), wf, wt, Cout, Cin, KH, KW,
+                  Kp, KpT)
+        from .hip_layers import conv_plan
+        tile, splits = conv_plan(M, Cout, Kp)
+        part = torch.empty(splits * M * Cout, dtype=torch.float32, device=dev) if splits > 1 else None
+        y = torch.empty((N, Cout, Ho, Wo), dtype=torch.bfloat16, device=dev,
+                        memory_format=torch.channels_last)
+        _ext.call("mda_conv_fwd", x, wf, None, None, None, y, None, part, N, H, W, Cin, Ho, Wo,
+                  Cout, KH, KW, stride, pad, Kp, 0, tile, splits)
+        ws = _ws(dev)
+        stats = torch.empty(4, Cout, dtype=torch.float32, device=dev)  # mean, rstd, scale, shift
+        _ext.call("mda_bn_stats", y, M, Cout, ws.partial, ws.counter, gamma.detach(), beta.detach(),
+                  bn.running_mean, bn.running_var, stats[0], stats[1], stats[2], stats[3],
+                  float(bn.momentum), float(bn.eps))
+        if bn.num_batches_tracked is not None:
+            bn.num_batches_tracked.add_(1)
+        res = _cl_bf16(residual) if residual is not None else None
+        out = torch.empty_like(y)
+        pre = torch.empty_like(y) if want_preact else None
+        _ext.call("mda_bn_apply", y, stats[2], stats[3], res, out, pre, M, Cout, act)
+        ctx.save_for_backward(x, wt, weight, gamma, beta, y, res, stats)
+        ctx.meta = (N, Cin, H, W, Cout, Ho, Wo, KH, KW, stride, pad, Kp, KpT, act)
+        ctx.has_res = residual is not None
+        if want_preact:
+            return out, pre
+        return out, None
+
+    @staticmethod
+    def backward(ctx, dout, dpre):
+        x, wt, weight, gamma, beta, y, res, stats = ctx.saved_tensors
+        N, Cin, H, W, Cout, Ho, Wo, KH, KW, stride, pad, Kp, KpT, act = ctx.meta
+        M = N * Ho * Wo
+        dev = y.device
+        dout = _cl_bf16(dout) if dout is not None else None
+        dpre = _cl_bf16(dpre) if dpre is not None else None
+        ws = _ws(dev)
+        sums = torch.empty(2, Cout, dtype=torch.float32, device=dev)
+        # dgamma / dbeta straight into existing .grad buffers (flat views), else returned
+        direct_gb = gamma.grad is not None and beta.grad is not None
+        dg = gamma.grad if direct_gb else None
+        db = beta.grad if direct_gb else None
+        _ext.call("mda_bn_bwd_reduce", dout, dpre, y, res, stats[2], stats[3], stats[0], stats[1],
+                  M, Cout, act, ws.partial, ws.counter, sums, dg, db)
+        need_res = ctx.has_res and ctx.needs_input_grad[4]
+        dy = torch.empty_like(y)
+        dres = torch.empty_like(y) if need_res else None
+        _ext.call("mda_bn_bwd_apply", dout, dpre, y, res, stats[2], stats[3], stats[0], stats[1],
+                  sums, dy, dres, M, Cout, act)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty((N, Cin, H, W), dtype=torch.bfloat16, device=dev,
+                             memory_format=torch.channels_last)
+            from .hip_layers import conv_plan
+            tile, splits = conv_plan(N * H * W, Cin, KpT)
+            part = torch.empty(splits * N * H * W * Cin, dtype=torch.float32, device=dev) if splits > 1 else None
+            _ext.call("mda_conv_dgrad", dy, wt, dx, part, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
+                      stride, pad, KpT, tile, splits)
+        dw = None
+        if ctx.needs_input_grad[1]:
+            sp = _wgrad_splits(M, Cout, Kp)
+            part = torch.empty(sp * Cout * Kp, dtype=torch.float32, device=dev)
+            direct_w = weight.grad is not None and weight.grad.is_contiguous()
+            target = weight.grad if direct_w else torch.empty_like(weight, memory_format=torch.contiguous_format)
+            _ext.call("mda_conv_wgrad", x, dy, part, target, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
+                      stride, pad, Kp, sp, 1.0, 1 if direct_w else 0)
+            dw = None if direct_w else target
+        dgamma = None if direct_gb else sums[1].clone()
+        dbeta = None if direct_gb else sums[0].clone()
+        return dx, dw, dgamma, dbeta, dres, None, None, None
+
+
+def conv_bn_act_train(x, conv, bn, act, residual, want_preact):
+    meta = (conv.stride[0], conv.padding[0], _ACT[act])
+    out, pre = _ConvBNActTrain.apply(x, conv.weight, bn.weight, bn.bias, residual, meta, bn,
+                                     bool(want_preact))
+    return out, pre

@@ -19,6 +19,12 @@ import torch.nn.functional as F
 from .backend import hip_enabled_for
 
 _ACTS = ("relu", "relu6", "none")
+# training-mode native conv+BN path (ops/hip_train.py); switchable for A/B runs
+_TRAIN_KERNELS = {"on": True}
+
+
+def set_train_kernels(flag: bool) -> None:
+    _TRAIN_KERNELS["on"] = bool(flag)
 
 
 def activate(x: torch.Tensor, act: str) -> torch.Tensor:
@@ -43,6 +49,9 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d | None = No
         from . import hip_layers
         if hip_layers.conv_supported(x, conv, bn):
             return hip_layers.conv_bn_act(x, conv, bn, act, residual, want_preact)
+        from . import hip_train
+        if _TRAIN_KERNELS["on"] and hip_train.train_supported(x, conv, bn):
+            return hip_train.conv_bn_act_train(x, conv, bn, act, residual, want_preact)
     y = conv(x)
     if bn is not None:
         y = _bn(y, bn)

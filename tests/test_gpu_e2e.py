@@ -63,7 +63,11 @@ def test_graph_matches_eager(trainer):
             st.step(b)
         torch.cuda.synchronize()
         outs.append(st.flat.data.clone())
-    torch.testing.assert_close(outs[0], outs[1], rtol=2e-3, atol=2e-4)
+    # MIOpen's atomics-based weight-gradient kernels are not bitwise
+    # deterministic, so compare trajectories in norm (a wrong replay, e.g. a
+    # skipped or doubled update, is off by O(lr) = O(1e-1) relative)
+    rel = (outs[0] - outs[1]).norm() / outs[1].norm()
+    assert rel < 5e-3, rel
 
 
 def test_trainer_epoch_loop_gpu(tmp_path):

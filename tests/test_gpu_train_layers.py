@@ -1,0 +1,99 @@
+"""Training-mode conv + BN (+res) (+ReLU) native kernels vs PyTorch fp32:
+forward values, running statistics, and gradients of x, weight, gamma,
+beta and the residual."""
+import copy
+
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from mdistiller_ddp_amd.ops import hip_train
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [
+    # N, Cin, H, Cout, k, stride, pad, x_grad
+    (16, 3, 32, 32, 3, 1, 1, False),    # stem
+    (16, 32, 32, 64, 3, 1, 1, True),
+    (16, 64, 32, 64, 3, 1, 1, True),
+    (16, 64, 32, 128, 3, 2, 1, True),   # stride 2 dgrad
+    (16, 128, 16, 256, 3, 2, 1, True),
+    (16, 64, 32, 128, 1, 2, 0, True),   # 1x1 shortcut
+    (16, 256, 8, 256, 3, 1, 1, True),
+    (8, 16, 32, 16, 3, 1, 1, True),     # vec8 loaders (resnet20 widths)
+    (4, 24, 15, 40, 3, 2, 1, True),
+]
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("act,with_res", [("relu", True), ("relu", False), ("none", False)])
+def test_conv_bn_act_train(shape, act, with_res):
+    N, Cin, H, Cout, k, s, p, xg = shape
+    torch.manual_seed(0)
+    conv = nn.Conv2d(Cin, Cout, k, s, p, bias=False).cuda()
+    bn = nn.BatchNorm2d(Cout).cuda()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    conv_r, bn_r = copy.deepcopy(conv), copy.deepcopy(bn)
+    x = torch.randn(N, Cin, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    Ho = (H + 2 * p - k) // s + 1
+    res = torch.randn(N, Cout, Ho, Ho, device="cuda").to(torch.bfloat16) if with_res else None
+    # ours
+    x1 = x.clone().requires_grad_(xg)
+    r1 = res.clone().requires_grad_(True) if with_res else None
+    assert hip_train.train_supported(x1, conv, bn)
+    out, pre = hip_train.conv_bn_act_train(x1, conv, bn, act, r1, True)
+    # incoming gradients are bf16 tensors in the native path; give the fp32
+    # reference the same rounded values
+    g = torch.randn_like(out.float()).to(torch.bfloat16).float()
+    gp = (torch.randn_like(out.float()) * 0.1).to(torch.bfloat16).float()
+    torch.autograd.backward([out.float(), pre.float()], [g, gp])
+    # reference (fp32 on the same bf16 inputs)
+    x2 = x.float().clone().requires_grad_(xg)
+    r2 = res.float().clone().requires_grad_(True) if with_res else None
+    z = bn_r(conv_r(x2))
+    if with_res:
+        z = z + r2
+    o = F.relu(z) if act == "relu" else z
+    torch.autograd.backward([o, z], [g, gp])
+    tol = 4e-2
+    torch.testing.assert_close(out.float(), o, atol=tol, rtol=tol)
+    torch.testing.assert_close(pre.float(), z, atol=tol, rtol=tol)
+    torch.testing.assert_close(bn.running_mean, bn_r.running_mean, atol=1e-3, rtol=1e-3)
+    torch.testing.assert_close(bn.running_var, bn_r.running_var, atol=1e-2, rtol=1e-2)
+
+    def rel(a, b):
+        return ((a.float() - b).norm() / (b.norm() + 1e-12)).item()
+
+    # per-channel sums over N*H*W terms that largely cancel: bf16 storage of y
+    # flips a few ReLU-mask decisions near z = 0, hence the looser bound
+    assert rel(bn.weight.grad, bn_r.weight.grad) < 5e-2
+    assert rel(bn.bias.grad, bn_r.bias.grad) < 5e-2
+    assert rel(conv.weight.grad, conv_r.weight.grad) < 2e-2
+    if xg:
+        assert rel(x1.grad, x2.grad) < 2e-2
+    if with_res:
+        assert rel(r1.grad, r2.grad) < 2e-2
+
+
+def test_student_train_step_uses_native_path():
+    """A full resnet8x4 training forward/backward through the native path matches
+    the PyTorch path in loss and (in norm) in parameter gradients."""
+    from mdistiller_ddp_amd.models.cifar import resnet8x4
+    from mdistiller_ddp_amd.ops.backend import use_backend
+    torch.manual_seed(0)
+    m1 = resnet8x4(num_classes=100).cuda().to(memory_format=torch.channels_last)
+    m2 = copy.deepcopy(m1)
+    x = torch.randn(32, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 100, (32,), device="cuda")
+    grads = []
+    for m, be in ((m1, "hip"), (m2, "torch")):
+        with use_backend(be), torch.autocast("cuda", dtype=torch.bfloat16):
+            logits, _ = m(x)
+            loss = F.cross_entropy(logits.float(), y)
+        loss.backward()
+        grads.append(torch.cat([p.grad.float().reshape(-1) for p in m.parameters()]))
+    rel = (grads[0] - grads[1]).norm() / grads[1].norm()
+    assert rel < 5e-2, rel

@@ -1,0 +1,60 @@
+#!/usr/bin/env python
+"""Throughput of every BASELINE.json configuration (one JSON row per config).
+
+    python benchmarks/throughput.py [--configs all|dkd_cifar,...] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N benchmarks/throughput.py ...
+
+Rows: config name, images/s for the whole job, ms/step, per-GPU batch,
+world size.  All synthetic data of the dataset's shape, random-init weights.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: (yaml, per-GPU batch, extra opts, dataset)
+    "kd_cifar_res56_res20": ("configs/cifar100/kd.yaml", 64,
+                             ["DISTILLER.TEACHER", "resnet56", "DISTILLER.STUDENT", "resnet20"], None),
+    "dkd_cifar_res32x4_res8x4": ("configs/cifar100/dkd/res32x4_res8x4.yaml", 64, [], None),
+    "dot_cifar_res32x4_res8x4": ("configs/cifar100/dot/res32x4_res8x4.yaml", 64, [], None),
+    "kd_cifar_res32x4_res8x4": ("configs/cifar100/kd.yaml", 64, [], None),
+    "crd_cifar_res32x4_res8x4": ("configs/cifar100/crd.yaml", 64, [], None),
+    "reviewkd_cifar_res32x4_res8x4": ("configs/cifar100/reviewkd.yaml", 64, [], None),
+    "reviewkd_imagenet_r34_r18": ("configs/imagenet/r34_r18/reviewkd.yaml", 32, [], None),
+    "dkd_imagenet_r50_mv1": ("configs/imagenet/r50_mv1/dkd.yaml", 64, [], None),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="all")
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--out", default=None, help="append JSON rows to this file")
+    args = ap.parse_args()
+    from mdistiller_ddp_amd import benchmark
+    names = list(CONFIGS) if args.configs == "all" else args.configs.split(",")
+    for name in names:
+        yaml, bs, opts, ds = CONFIGS[name]
+        r = benchmark.run(os.path.join(ROOT, yaml), bs, args.steps, args.warmup, opts=opts,
+                          use_graph=not args.no_graph, dataset=ds)
+        if r["rank"] == 0:
+            row = {"config": name, "images_per_s": round(r["images_per_s"], 1),
+                   "ms_per_step": round(r["ms_per_step"], 3), "per_gpu_batch": bs,
+                   "n_gpus": r["n_gpus"], "graph": r["graph"], "dtype": r["dtype"],
+                   "final_loss": round(r["final_loss"], 4)}
+            print(json.dumps(row), flush=True)
+            if args.out:
+                with open(args.out, "a") as f:
+                    f.write(json.dumps(row) + "\n")
+
+
+if __name__ == "__main__":
+    main()

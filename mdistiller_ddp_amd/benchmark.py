@@ -1,0 +1,92 @@
+"""Throughput measurement of a full distillation training step.
+
+Shared by ``bench.py`` (the headline metric) and
+``benchmarks/throughput.py`` (all BASELINE configs).  One timed step is the
+framework's real ``TrainStep``: batch copy into the step's input buffers,
+teacher forward (no grad, own stream), student forward, losses, backward,
+gradient all-reduce (world > 1), optimizer update, BN running-stat updates
+and on-device metrics.  Timing: W untimed warm-up steps, then K steps
+bracketed by a barrier and a device synchronisation on both sides; the
+slowest rank's time is reported.
+"""
+from __future__ import annotations
+
+import time
+
+import torch
+
+
+def run(cfg_file: str, per_gpu_batch: int, steps: int, warmup: int, opts=(), use_graph=True,
+        backend="auto", dtype="bf16", teacher_stream=True, dataset=None, crd_k=None):
+    from .ops.backend import set_backend
+    from .parallel import dist as D
+    from .config import get_cfg
+    from .engine.build import build_distiller
+    from .engine.step import TrainStep
+    from .engine.trainer import BATCH_KEYS
+    from .data.synthetic import SyntheticLoader, dataset_shape
+    from .runtime import streams
+
+    set_backend(backend)
+    streams.set_enabled(teacher_stream)
+    info = D.init_distributed() if not D.is_dist() else D.info()
+    dev = info.device
+    if dev.type == "cuda":
+        torch.backends.cudnn.benchmark = True
+    cfg = get_cfg()
+    cfg.merge_from_file(cfg_file)
+    if opts:
+        cfg.merge_from_list(list(opts))
+    cfg.DISTILLER.RANDOM_TEACHER = True
+    cfg.freeze()
+    ds = dataset or cfg.DATASET.TYPE
+    _, ncls, ntrain, _ = dataset_shape(ds)
+    torch.manual_seed(1234 + info.rank)
+    distiller = build_distiller(cfg, num_classes=ncls, device=dev, num_data=ntrain)
+    dt = torch.bfloat16 if (dtype == "bf16" and dev.type == "cuda") else torch.float32
+    trainer = cfg.SOLVER.TRAINER
+    step = TrainStep(distiller, cfg, dev, trainer=trainer, use_graph=use_graph, dtype=dt,
+                     batch_keys=BATCH_KEYS[trainer])
+    distiller.train()
+    # past any warm-up ramp (DKD / ReviewKD): full loss
+    step.set_epoch(float(max(cfg.DKD.WARMUP, cfg.REVIEWKD.WARMUP_EPOCHS) + 1))
+    step.set_lr(cfg.SOLVER.LR)
+    k = (crd_k if crd_k is not None else cfg.CRD.NCE.K) if cfg.DISTILLER.TYPE == "CRD" else 0
+    loader = SyntheticLoader(ds, per_gpu_batch, dev, steps_per_epoch=10 ** 9, pool=4,
+                             seed=info.rank, crd_k=k, num_data=ntrain,
+                             channels_last=(dev.type == "cuda"))
+    it = iter(loader)
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+
+    for _ in range(warmup):
+        step.step(next(it))
+    sync()
+    D.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step.step(next(it))
+    sync()
+    D.barrier()
+    sync()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    if D.is_dist():
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    el = float(t.item())
+    m = step.meters.summary(reduce=True)
+    n = info.world_size
+    return {
+        "seconds": el,
+        "ms_per_step": 1000.0 * el / steps,
+        "images_per_s": n * per_gpu_batch * steps / el,
+        "n_gpus": n,
+        "global_batch": n * per_gpu_batch,
+        "final_loss": m["loss"],
+        "graph": step.use_graph,
+        "dtype": "bf16" if dt == torch.bfloat16 else "fp32",
+        "rank": info.rank,
+    }

@@ -19,8 +19,6 @@
 
 namespace {
 
-constexpr int CBLK = 64;    // channels per block (one per lane)
-constexpr int RWAVES = 4;   // row-parallel waves per block
 
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_RELU6 = 2 };
 
@@ -35,7 +33,45 @@ __device__ __forceinline__ float act_grad(float z, int act) {
   return 1.f;
 }
 
-// grid: (ceil(C/64), RB row-blocks). Each thread: one channel, strided rows.
+// Block-level per-channel partial sums of two quantities over rows, 8
+// channels (16 bytes) per thread: thread t owns channel group t % C8 and row
+// offset t / C8; rows are strided over the grid.  Writes partial[blk][2][C].
+__device__ __forceinline__ void block_channel_partials(float (&a)[8], float (&b)[8], int C,
+                                                       int rpi, float* __restrict__ partial) {
+  __shared__ float sm[2][256 * 8];
+  const int tid = threadIdx.x;
+  const int C8 = C / 8;
+  const int cg = tid % C8, r0 = tid / C8;
+  if (r0 < rpi) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      sm[0][r0 * C + cg * 8 + k] = a[k];
+      sm[1][r0 * C + cg * 8 + k] = b[k];
+    }
+  }
+  __syncthreads();
+  for (int t = tid; t < 2 * C; t += blockDim.x) {
+    const int q = t / C, c = t - q * C;
+    float acc = 0.f;
+    for (int r = 0; r < rpi; ++r) acc += sm[q][r * C + c];
+    partial[((int64_t)blockIdx.x * 2 + q) * C + c] = acc;
+  }
+}
+
+// Sum partial[0..nblk)[q][c] in a fixed order (fp64), for all 2C (q, c) pairs.
+// 8 independent accumulators per thread keep the loads in flight.
+__device__ __forceinline__ double sum_blocks(const float* __restrict__ partial, int nblk, int C,
+                                             int q, int c) {
+  double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int b = 0;
+  for (; b + 8 <= nblk; b += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc[u] += partial[((int64_t)(b + u) * 2 + q) * C + c];
+  }
+  for (; b < nblk; ++b) acc[0] += partial[((int64_t)b * 2 + q) * C + c];
+  return ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+}
+
 __global__ void __launch_bounds__(256)
 bn_stats_kernel(const bf16_t* __restrict__ y, int M, int C, float* __restrict__ partial,
                 unsigned* __restrict__ counter, const float* __restrict__ gamma,
@@ -43,39 +79,33 @@ bn_stats_kernel(const bf16_t* __restrict__ y, int M, int C, float* __restrict__ 
                 float* __restrict__ running_var, float* __restrict__ mean_out,
                 float* __restrict__ rstd_out, float* __restrict__ scale_out,
                 float* __restrict__ shift_out, float momentum, float eps) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = blockIdx.x * CBLK + lane;
-  const int rb = blockIdx.y, nrb = gridDim.y;
-  float s = 0.f, ss = 0.f;
-  if (c < C) {
-    for (int m = rb * RWAVES + w; m < M; m += nrb * RWAVES) {
-      float v = bf2f(y[(int64_t)m * C + c]);
-      s += v;
-      ss += v * v;
-    }
-  }
-  __shared__ float red[2][RWAVES][CBLK];
-  red[0][w][lane] = s;
-  red[1][w][lane] = ss;
-  __syncthreads();
-  if (w == 0) {
-    float a = 0.f, b = 0.f;
-    for (int i = 0; i < RWAVES; ++i) { a += red[0][i][lane]; b += red[1][i][lane]; }
-    if (c < C) {
-      partial[((int64_t)rb * 2 + 0) * C + c] = a;
-      partial[((int64_t)rb * 2 + 1) * C + c] = b;
-    }
-  }
-  // last row-block of this channel group finalises (counter per channel group)
-  if (mda_arrive(counter + blockIdx.x, nrb)) {
-    if (w == 0 && c < C) {
-      double a = 0.0, b = 0.0;
-      for (int r = 0; r < nrb; ++r) {
-        a += partial[((int64_t)r * 2 + 0) * C + c];
-        b += partial[((int64_t)r * 2 + 1) * C + c];
+  const int C8 = C / 8;
+  const int rpi = 256 / C8;  // rows per block-iteration
+  const int cg = threadIdx.x % C8, r0 = threadIdx.x / C8;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ss[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (r0 < rpi) {
+    for (int m = blockIdx.x * rpi + r0; m < M; m += gridDim.x * rpi) {
+      uint4 v = *(const uint4*)(y + (int64_t)m * C + cg * 8);
+      const bf16_t* e = (const bf16_t*)&v;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float f = bf2f(e[k]);
+        s[k] += f;
+        ss[k] += f * f;
       }
-      const double mean = a / M;
-      double var = b / M - mean * mean;
+    }
+  }
+  block_channel_partials(s, ss, C, rpi, partial);
+  if (mda_arrive(counter, gridDim.x)) {
+    __shared__ double tot[2 * 2048];
+    for (int t = threadIdx.x; t < 2 * C; t += blockDim.x) {
+      const int q = t / C, c = t - q * C;
+      tot[t] = sum_blocks(partial, gridDim.x, C, q, c);
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      const double mean = tot[c] / M;
+      double var = tot[C + c] / M - mean * mean;
       if (var < 0) var = 0;
       const float rstd = (float)(1.0 / sqrt(var + (double)eps));
       const float g = gamma ? gamma[c] : 1.f;
@@ -120,9 +150,9 @@ bn_apply_kernel(const bf16_t* __restrict__ y, const float* __restrict__ scale,
   }
 }
 
-// dz = dout * act'(z) (+ dpre); partial sums of dz and dz*xhat per channel.
-// z is recovered from y: z = y*scale + shift (+ res); so the mask needs y,
-// scale, shift and res, not a stored z.
+// dz = dout * act'(z) (+ dpre); sums of dz and dz*xhat per channel.
+// z is recovered from y: z = y*scale + shift (+ res), so the ReLU mask needs
+// no stored pre-activation.
 __global__ void __launch_bounds__(256)
 bn_bwd_reduce_kernel(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ dpre,
                      const bf16_t* __restrict__ y, const bf16_t* __restrict__ res,
@@ -131,49 +161,50 @@ bn_bwd_reduce_kernel(const bf16_t* __restrict__ dout, const bf16_t* __restrict__
                      int act, float* __restrict__ partial, unsigned* __restrict__ counter,
                      float* __restrict__ sums, float* __restrict__ dgamma,
                      float* __restrict__ dbeta) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = blockIdx.x * CBLK + lane;
-  const int rb = blockIdx.y, nrb = gridDim.y;
-  float sdz = 0.f, sdzx = 0.f;
-  if (c < C) {
-    const float sc = scale[c], sh = shift[c], mu = mean[c], rs = rstd[c];
-    for (int m = rb * RWAVES + w; m < M; m += nrb * RWAVES) {
-      const int64_t o = (int64_t)m * C + c;
-      const float yv = bf2f(y[o]);
-      float dz = dout ? bf2f(dout[o]) : 0.f;
-      if (act != ACT_NONE) {
-        float z = yv * sc + sh;
-        if (res) z += bf2f(res[o]);
-        dz *= act_grad(z, act);
+  const int C8 = C / 8;
+  const int rpi = 256 / C8;
+  const int cg = threadIdx.x % C8, r0 = threadIdx.x / C8;
+  float sdz[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sdzx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (r0 < rpi) {
+    float sc[8], sh[8], mu[8], rs[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = cg * 8 + k;
+      sc[k] = scale[c]; sh[k] = shift[c]; mu[k] = mean[c]; rs[k] = rstd[c];
+    }
+    for (int m = blockIdx.x * rpi + r0; m < M; m += gridDim.x * rpi) {
+      const int64_t o = (int64_t)m * C + cg * 8;
+      uint4 yv = *(const uint4*)(y + o);
+      uint4 dv = dout ? *(const uint4*)(dout + o) : make_uint4(0, 0, 0, 0);
+      uint4 pv = dpre ? *(const uint4*)(dpre + o) : make_uint4(0, 0, 0, 0);
+      uint4 rv = (res && act != ACT_NONE) ? *(const uint4*)(res + o) : make_uint4(0, 0, 0, 0);
+      const bf16_t* ye = (const bf16_t*)&yv;
+      const bf16_t* de = (const bf16_t*)&dv;
+      const bf16_t* pe = (const bf16_t*)&pv;
+      const bf16_t* re = (const bf16_t*)&rv;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float yf = bf2f(ye[k]);
+        float dz = bf2f(de[k]);
+        if (act != ACT_NONE) {
+          float z = yf * sc[k] + sh[k];
+          if (res) z += bf2f(re[k]);
+          dz *= act_grad(z, act);
+        }
+        if (dpre) dz += bf2f(pe[k]);
+        sdz[k] += dz;
+        sdzx[k] += dz * (yf - mu[k]) * rs[k];
       }
-      if (dpre) dz += bf2f(dpre[o]);
-      sdz += dz;
-      sdzx += dz * (yv - mu) * rs;
     }
   }
-  __shared__ float red[2][RWAVES][CBLK];
-  red[0][w][lane] = sdz;
-  red[1][w][lane] = sdzx;
-  __syncthreads();
-  if (w == 0) {
-    float a = 0.f, b = 0.f;
-    for (int i = 0; i < RWAVES; ++i) { a += red[0][i][lane]; b += red[1][i][lane]; }
-    if (c < C) {
-      partial[((int64_t)rb * 2 + 0) * C + c] = a;
-      partial[((int64_t)rb * 2 + 1) * C + c] = b;
-    }
-  }
-  if (mda_arrive(counter + blockIdx.x, nrb)) {
-    if (w == 0 && c < C) {
-      double a = 0.0, b = 0.0;
-      for (int r = 0; r < nrb; ++r) {
-        a += partial[((int64_t)r * 2 + 0) * C + c];
-        b += partial[((int64_t)r * 2 + 1) * C + c];
-      }
-      sums[c] = (float)a;          // sum dz      (= dbeta)
-      sums[C + c] = (float)b;      // sum dz*xhat (= dgamma)
-      if (dbeta) dbeta[c] += (float)a;
-      if (dgamma) dgamma[c] += (float)b;
+  block_channel_partials(sdz, sdzx, C, rpi, partial);
+  if (mda_arrive(counter, gridDim.x)) {
+    for (int t = threadIdx.x; t < 2 * C; t += blockDim.x) {
+      const int q = t / C, c = t - q * C;
+      const float v = (float)sum_blocks(partial, gridDim.x, C, q, c);
+      sums[t] = v;  // [0, C): sum dz (= dbeta), [C, 2C): sum dz*xhat (= dgamma)
+      if (q == 0 && dbeta) dbeta[c] += v;
+      if (q == 1 && dgamma) dgamma[c] += v;
     }
   }
 }
@@ -221,12 +252,12 @@ bn_bwd_apply_kernel(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ 
   }
 }
 
-inline int row_blocks(int64_t M) {
-  // ~ 2048 rows per row-block, capped so partials stay small
-  int64_t rb = (M + 2047) / 2048;
-  if (rb < 1) rb = 1;
-  if (rb > 256) rb = 256;
-  return (int)rb;
+inline int reduce_blocks(int64_t M, int64_t C) {
+  // ~16 sixteen-byte vectors per thread, at most 256 blocks (partials stay small)
+  int64_t b = (M * (C / 8) + 256 * 16 - 1) / (256 * 16);
+  if (b < 1) b = 1;
+  if (b > 256) b = 256;
+  return (int)b;
 }
 
 inline int ew_blocks(int64_t n8) {
@@ -238,12 +269,13 @@ inline int ew_blocks(int64_t n8) {
 
 }  // namespace
 
-// Workspace: partial >= 2*C*256 floats; counter >= ceil(C/64) zeroed uints.
+// Workspace: partial >= 2*C*256 floats; counter: one zeroed uint.  C % 8 == 0, C <= 2048.
 MDA_API int mda_bn_stats(const void* y, int64_t M, int64_t C, float* partial, unsigned* counter,
                          const float* gamma, const float* beta, float* running_mean,
                          float* running_var, float* mean, float* rstd, float* scale,
                          float* shift, float momentum, float eps, hipStream_t st) {
-  dim3 grid((int)((C + CBLK - 1) / CBLK), row_blocks(M));
+  if (C % 8 || C / 8 > 256 || C > 2048) return (int)hipErrorInvalidValue;
+  dim3 grid(reduce_blocks(M, C));
   hipLaunchKernelGGL(bn_stats_kernel, grid, dim3(256), 0, st, (const bf16_t*)y, (int)M, (int)C,
                      partial, counter, gamma, beta, running_mean, running_var, mean, rstd, scale,
                      shift, momentum, eps);
@@ -266,7 +298,8 @@ MDA_API int mda_bn_bwd_reduce(const void* dout, const void* dpre, const void* y,
                               const float* rstd, int64_t M, int64_t C, int64_t act,
                               float* partial, unsigned* counter, float* sums, float* dgamma,
                               float* dbeta, hipStream_t st) {
-  dim3 grid((int)((C + CBLK - 1) / CBLK), row_blocks(M));
+  if (C % 8 || C / 8 > 256 || C > 2048) return (int)hipErrorInvalidValue;
+  dim3 grid(reduce_blocks(M, C));
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, grid, dim3(256), 0, st, (const bf16_t*)dout,
                      (const bf16_t*)dpre, (const bf16_t*)y, (const bf16_t*)res, scale, shift,
                      mean, rstd, (int)M, (int)C, (int)act, partial, counter, sums, dgamma, dbeta);

@@ -180,22 +180,33 @@ conv_wgrad_kernel(const WgParams p) {
       }
 }
 
-// grad[co][ci][kh][kw] += scale * sum_s partial[s][co][(kh*KW+kw)*Cin+ci]
+// grad[co][ci][kh][kw] (+)= scale * sum_s partial[s][co][(kh*KW+kw)*Cin+ci]
+// Threads walk the packed (co, k) order so the split partials are read
+// coalesced; the OIHW write is the only scattered access.
 __global__ void __launch_bounds__(256)
 wgrad_reduce_kernel(const float* __restrict__ partial, float* __restrict__ grad, int splits,
                     int Cout, int Cin, int KH, int KW, int Kp, float scale, int accumulate) {
   const int K = Cin * KH * KW;
   const int64_t total = (int64_t)Cout * K;
+  const int64_t sstride = (int64_t)Cout * Kp;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int co = (int)(i / K);
-    const int r = (int)(i - (int64_t)co * K);        // OIHW order: ci, kh, kw
-    const int ci = r / (KH * KW);
-    const int t = r - ci * KH * KW;
-    const int k = t * Cin + ci;                      // packed order
-    float a = 0.f;
-    for (int s = 0; s < splits; ++s) a += partial[((int64_t)s * Cout + co) * Kp + k];
-    grad[i] = (accumulate ? grad[i] : 0.f) + scale * a;
+    const int k = (int)(i - (int64_t)co * K);        // packed order: (kh*KW + kw)*Cin + ci
+    const int tap = k / Cin, ci = k - tap * Cin;
+    const int64_t src = (int64_t)co * Kp + k;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int s = 0;
+    for (; s + 4 <= splits; s += 4) {
+      a0 += partial[src + (s + 0) * sstride];
+      a1 += partial[src + (s + 1) * sstride];
+      a2 += partial[src + (s + 2) * sstride];
+      a3 += partial[src + (s + 3) * sstride];
+    }
+    for (; s < splits; ++s) a0 += partial[src + s * sstride];
+    const float a = (a0 + a1) + (a2 + a3);
+    const int64_t dst = ((int64_t)co * Cin + ci) * KH * KW + tap;
+    grad[dst] = (accumulate ? grad[dst] : 0.f) + scale * a;
   }
 }
 
@@ -235,7 +246,7 @@ MDA_API int mda_wgrad_plan(int64_t M, int64_t Cout, int64_t Kp, int64_t* splits)
   int64_t tiles = ((Cout + TC - 1) / TC) * ((Kp + TK - 1) / TK);
   int64_t sp = 1;
   // aim for >= 512 workgroups, keep >= 4 stages (256 pixels) per split
-  while (tiles * sp < 512 && (M / (sp * 2)) >= 4 * TM && sp < 256) sp *= 2;
+  while (tiles * sp < 256 && (M / (sp * 2)) >= 4 * TM && sp < 64) sp *= 2;
   *splits = sp;
   return 0;
 }

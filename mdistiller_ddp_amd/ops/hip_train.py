@@ -175,6 +175,52 @@ class _ConvBNActTrain(torch.autograd.Function):
         return dx, dw, dgamma, dbeta, dres, None, None, None
 
 
+def pack_weights(weight, dgrad=True):
+    """fp32 OIHW -> (bf16 [Cout][Kp], bf16 [Cin][KpT] or None, Kp, KpT)."""
+    Cout, Cin, KH, KW = weight.shape
+    Kp = (KH * KW * Cin + 63) // 64 * 64
+    KpT = (KH * KW * Cout + 63) // 64 * 64
+    wf = torch.empty(Cout, Kp, dtype=torch.bfloat16, device=weight.device)
+    wt = torch.empty(Cin, KpT, dtype=torch.bfloat16, device=weight.device) if dgrad else None
+    _ext.call("mda_pack_conv_weights", weight.detach().float().contiguous(), wf, wt, Cout, Cin, KH,
+              KW, Kp, KpT)
+    return wf, wt, Kp, KpT
+
+
+def conv_dgrad(dy, weight, x_shape, stride, pad):
+    """Input gradient of conv2d (bf16 NHWC in/out) on the MFMA dgrad kernel."""
+    from .hip_layers import conv_plan
+    N, Cin, H, W = x_shape
+    Cout, _, KH, KW = weight.shape
+    dy = _cl_bf16(dy)
+    Ho, Wo = dy.shape[2], dy.shape[3]
+    _, wt, _, KpT = pack_weights(weight, True)
+    dx = torch.empty((N, Cin, H, W), dtype=torch.bfloat16, device=dy.device,
+                     memory_format=torch.channels_last)
+    tile, splits = conv_plan(N * H * W, Cin, KpT)
+    part = torch.empty(splits * N * H * W * Cin, dtype=torch.float32, device=dy.device) if splits > 1 else None
+    _ext.call("mda_conv_dgrad", dy, wt, dx, part, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
+              KpT, tile, splits)
+    return dx
+
+
+def conv_wgrad(x, dy, weight_shape, stride, pad):
+    """Weight gradient of conv2d (fp32 OIHW) on the MFMA wgrad kernel."""
+    Cout, Cin, KH, KW = weight_shape
+    x = _cl_bf16(x)
+    dy = _cl_bf16(dy)
+    N, _, H, W = x.shape
+    Ho, Wo = dy.shape[2], dy.shape[3]
+    Kp = (KH * KW * Cin + 63) // 64 * 64
+    M = N * Ho * Wo
+    sp = _wgrad_splits(M, Cout, Kp)
+    part = torch.empty(sp * Cout * Kp, dtype=torch.float32, device=x.device)
+    out = torch.empty(weight_shape, dtype=torch.float32, device=x.device)
+    _ext.call("mda_conv_wgrad", x, dy, part, out, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
+              Kp, sp, 1.0, 0)
+    return out
+
+
 def conv_bn_act_train(x, conv, bn, act, residual, want_preact):
     meta = (conv.stride[0], conv.padding[0], _ACT[act])
     out, pre = _ConvBNActTrain.apply(x, conv.weight, bn.weight, bn.bias, residual, meta, bn,

@@ -71,29 +71,54 @@ def test_conv_bn_act_train(shape, act, with_res):
     # flips a few ReLU-mask decisions near z = 0, hence the looser bound
     assert rel(bn.weight.grad, bn_r.weight.grad) < 5e-2
     assert rel(bn.bias.grad, bn_r.bias.grad) < 5e-2
-    assert rel(conv.weight.grad, conv_r.weight.grad) < 2e-2
+    assert rel(conv.weight.grad, conv_r.weight.grad) < 5e-2
     if xg:
-        assert rel(x1.grad, x2.grad) < 2e-2
+        assert rel(x1.grad, x2.grad) < 5e-2
     if with_res:
-        assert rel(r1.grad, r2.grad) < 2e-2
+        assert rel(r1.grad, r2.grad) < 5e-2
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_dgrad_wgrad_kernels_exact_inputs(shape):
+    """The MFMA dgrad / wgrad kernels alone, on bf16 inputs given to both sides."""
+    N, Cin, H, Cout, k, s, p, xg = shape
+    torch.manual_seed(1)
+    x = torch.randn(N, Cin, H, H, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(Cout, Cin, k, k, device="cuda") * 0.1).to(torch.bfloat16).float()
+    Ho = (H + 2 * p - k) // s + 1
+    dy = torch.randn(N, Cout, Ho, Ho, device="cuda").to(torch.bfloat16)
+    xr = x.float().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    F.conv2d(xr, wr, stride=s, padding=p).backward(dy.float())
+    dw = hip_train.conv_wgrad(x, dy, tuple(w.shape), s, p)
+    rel_w = ((dw - wr.grad).norm() / wr.grad.norm()).item()
+    assert rel_w < 1e-2, rel_w
+    if Cout % 8 == 0:
+        dx = hip_train.conv_dgrad(dy, w, tuple(x.shape), s, p)
+        rel_x = ((dx.float() - xr.grad).norm() / xr.grad.norm()).item()
+        assert rel_x < 1e-2, rel_x
 
 
 def test_student_train_step_uses_native_path():
-    """A full resnet8x4 training forward/backward through the native path matches
-    the PyTorch path in loss and (in norm) in parameter gradients."""
+    """A full resnet8x4 training forward/backward through the native path vs an
+    fp32 PyTorch reference: its gradient error must be in the same band as the
+    stock bf16 (MIOpen) path's."""
     from mdistiller_ddp_amd.models.cifar import resnet8x4
     from mdistiller_ddp_amd.ops.backend import use_backend
     torch.manual_seed(0)
     m1 = resnet8x4(num_classes=100).cuda().to(memory_format=torch.channels_last)
     m2 = copy.deepcopy(m1)
+    m3 = copy.deepcopy(m1)
     x = torch.randn(32, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
     y = torch.randint(0, 100, (32,), device="cuda")
     grads = []
-    for m, be in ((m1, "hip"), (m2, "torch")):
-        with use_backend(be), torch.autocast("cuda", dtype=torch.bfloat16):
+    for m, be, amp in ((m1, "hip", True), (m2, "torch", True), (m3, "torch", False)):
+        with use_backend(be), torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
             logits, _ = m(x)
             loss = F.cross_entropy(logits.float(), y)
         loss.backward()
         grads.append(torch.cat([p.grad.float().reshape(-1) for p in m.parameters()]))
-    rel = (grads[0] - grads[1]).norm() / grads[1].norm()
-    assert rel < 5e-2, rel
+    ref = grads[2]
+    e_native = ((grads[0] - ref).norm() / ref.norm()).item()
+    e_miopen = ((grads[1] - ref).norm() / ref.norm()).item()
+    assert e_native < max(2.0 * e_miopen, 0.05), (e_native, e_miopen)

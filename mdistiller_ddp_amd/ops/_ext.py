@@ -41,7 +41,7 @@ SIGNATURES = {
     "mda_wgrad_plan": "iiip",
     "mda_pack_conv_weights": "ppp" + "i" * 6 + "s",
     # training-mode BatchNorm (csrc/bn.hip)
-    "mda_bn_stats": "pii" + "pp" + "pppp" + "pppp" + "ffs",
+    "mda_bn_stats": "pii" + "pp" + "pppp" + "pppp" + "ffps",
     "mda_bn_apply": "pppppp" + "iii" + "s",
     "mda_bn_bwd_reduce": "pppppppp" + "iii" + "ppppp" + "s",
     "mda_bn_bwd_apply": "p" * 11 + "iii" + "s",

@@ -52,25 +52,78 @@ __device__ __forceinline__ void block_channel_partials(float (&a)[8], float (&b)
   __syncthreads();
   for (int t = tid; t < 2 * C; t += blockDim.x) {
     const int q = t / C, c = t - q * C;
-    float acc = 0.f;
-    for (int r = 0; r < rpi; ++r) acc += sm[q][r * C + c];
-    partial[((int64_t)blockIdx.x * 2 + q) * C + c] = acc;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    int r = 0;
+    for (; r + 4 <= rpi; r += 4) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] += sm[q][(r + u) * C + c];
+    }
+    for (; r < rpi; ++r) acc[0] += sm[q][r * C + c];
+    partial[(int64_t)blockIdx.x * 2 * C + t] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   }
 }
 
-// Sum partial[0..nblk)[q][c] in a fixed order (fp64), for all 2C (q, c) pairs.
-// 8 independent accumulators per thread keep the loads in flight.
-__device__ __forceinline__ double sum_blocks(const float* __restrict__ partial, int nblk, int C,
-                                             int q, int c) {
-  double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  int b = 0;
-  for (; b + 8 <= nblk; b += 8) {
+// Deterministic two-level combine of the per-block partials partial[blk][V]
+// (V = 2C): blocks arrive in groups of RED_GROUP; the last arriver of a group
+// sums its group's rows in block order into gpart[group][V]; the last group
+// to finish sums the group rows (fp64, fixed order) into tot[V] (LDS).  Every
+// thread of the final block issues its <= 16 loads together, so the serial
+// tail is two L2 round trips instead of one block walking nblk*V values.
+// counters: [0] = top level, [1 + g] = group g (>= 1 + 256/RED_GROUP zeroed uints).
+constexpr int RED_GROUP = 16;
+constexpr int RED_MAX_BLOCKS = 256;
+
+__device__ __forceinline__ bool combine_partials(float* __restrict__ partial, int V,
+                                                 unsigned* __restrict__ counters,
+                                                 double* __restrict__ tot) {
+  const int nblk = gridDim.x;
+  const int ngrp = (nblk + RED_GROUP - 1) / RED_GROUP;
+  const int g = blockIdx.x / RED_GROUP;
+  const int gsize = min(RED_GROUP, nblk - g * RED_GROUP);
+  float* gpart = partial + (int64_t)nblk * V;
+  if (!mda_arrive(counters + 1 + g, gsize)) return false;
+  for (int v = threadIdx.x; v < V; v += blockDim.x) {
+    float x[RED_GROUP];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) acc[u] += partial[((int64_t)(b + u) * 2 + q) * C + c];
+    for (int i = 0; i < RED_GROUP; ++i)
+      x[i] = i < gsize ? partial[(int64_t)(g * RED_GROUP + i) * V + v] : 0.f;
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < RED_GROUP; ++i) acc += x[i];
+    gpart[(int64_t)g * V + v] = acc;
   }
-  for (; b < nblk; ++b) acc[0] += partial[((int64_t)b * 2 + q) * C + c];
-  return ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  if (!mda_arrive(counters, ngrp)) return false;
+  for (int v = threadIdx.x; v < V; v += blockDim.x) {
+    float x[RED_MAX_BLOCKS / RED_GROUP];
+#pragma unroll
+    for (int i = 0; i < RED_MAX_BLOCKS / RED_GROUP; ++i)
+      x[i] = i < ngrp ? gpart[(int64_t)i * V + v] : 0.f;
+    double acc = 0.0;
+#pragma unroll
+    for (int i = 0; i < RED_MAX_BLOCKS / RED_GROUP; ++i) acc += (double)x[i];
+    tot[v] = acc;
+  }
+  __syncthreads();
+  return true;
 }
+
+// Per-thread row loop over [M, C] bf16 rows: thread owns channel group cg
+// and rows r0, r0 + rstride, ...; four 16-byte loads in flight per stream.
+#define MDA_ROW_LOOP(...)                                                    \
+  {                                                                          \
+    const int rstride = gridDim.x * rpi;                                     \
+    int m = blockIdx.x * rpi + r0;                                           \
+    for (; m + 3 * rstride < M; m += 4 * rstride) {                          \
+      _Pragma("unroll") for (int u = 0; u < 4; ++u) {                        \
+        const int64_t o = (int64_t)(m + u * rstride) * C + cg * 8;           \
+        __VA_ARGS__                                                          \
+      }                                                                      \
+    }                                                                        \
+    for (; m < M; m += rstride) {                                            \
+      const int64_t o = (int64_t)m * C + cg * 8;                             \
+      __VA_ARGS__                                                            \
+    }                                                                        \
+  }
 
 __global__ void __launch_bounds__(256)
 bn_stats_kernel(const bf16_t* __restrict__ y, int M, int C, float* __restrict__ partial,
@@ -78,31 +131,28 @@ bn_stats_kernel(const bf16_t* __restrict__ y, int M, int C, float* __restrict__ 
                 const float* __restrict__ beta, float* __restrict__ running_mean,
                 float* __restrict__ running_var, float* __restrict__ mean_out,
                 float* __restrict__ rstd_out, float* __restrict__ scale_out,
-                float* __restrict__ shift_out, float momentum, float eps) {
+                float* __restrict__ shift_out, float momentum, float eps,
+                int64_t* __restrict__ nbt) {
   const int C8 = C / 8;
   const int rpi = 256 / C8;  // rows per block-iteration
   const int cg = threadIdx.x % C8, r0 = threadIdx.x / C8;
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ss[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (r0 < rpi) {
-    for (int m = blockIdx.x * rpi + r0; m < M; m += gridDim.x * rpi) {
-      uint4 v = *(const uint4*)(y + (int64_t)m * C + cg * 8);
-      const bf16_t* e = (const bf16_t*)&v;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        float f = bf2f(e[k]);
-        s[k] += f;
-        ss[k] += f * f;
+    MDA_ROW_LOOP({
+      const uint4 v = *(const uint4*)(y + o);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+_Pragma("unroll")
+      for (int k = 0; k < 4; ++k) {
+        const float f0 = __uint_as_float(w[k] << 16), f1 = __uint_as_float(w[k] & 0xffff0000u);
+        s[2 * k] += f0; ss[2 * k] += f0 * f0;
+        s[2 * k + 1] += f1; ss[2 * k + 1] += f1 * f1;
       }
-    }
+    })
   }
   block_channel_partials(s, ss, C, rpi, partial);
-  if (mda_arrive(counter, gridDim.x)) {
-    __shared__ double tot[2 * 2048];
-    for (int t = threadIdx.x; t < 2 * C; t += blockDim.x) {
-      const int q = t / C, c = t - q * C;
-      tot[t] = sum_blocks(partial, gridDim.x, C, q, c);
-    }
-    __syncthreads();
+  __shared__ double tot[2 * 2048];
+  if (combine_partials(partial, 2 * C, counter, tot)) {
+    if (threadIdx.x == 0 && nbt) nbt[0] += 1;
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
       const double mean = tot[c] / M;
       double var = tot[C + c] / M - mean * mean;
@@ -130,9 +180,21 @@ bn_apply_kernel(const bf16_t* __restrict__ y, const float* __restrict__ scale,
                 bf16_t* __restrict__ out, bf16_t* __restrict__ preact, int64_t M, int C, int act) {
   const int64_t total = M * C / 8;
   const int c8 = C / 8;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int c0 = (int)(i % c8) * 8;
+  // the grid stride is a multiple of C/8 (both powers of two or the launch
+  // makes it so), so every thread keeps one channel group: load its params once
+  const int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int c0 = (int)(i0 % c8) * 8;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { sc[k] = scale[c0 + k]; sh[k] = shift[c0 + k]; }
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const bool fixed = (stride % c8) == 0;
+  for (int64_t i = i0; i < total; i += stride) {
+    if (!fixed) {
+      const int cc = (int)(i % c8) * 8;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { sc[k] = scale[cc + k]; sh[k] = shift[cc + k]; }
+    }
     uint4 yv = ((const uint4*)y)[i];
     uint4 rv = res ? ((const uint4*)res)[i] : make_uint4(0, 0, 0, 0);
     const bf16_t* yp = (const bf16_t*)&yv;
@@ -140,7 +202,7 @@ bn_apply_kernel(const bf16_t* __restrict__ y, const float* __restrict__ scale,
     bf16_t o[8], z[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      float v = bf2f(yp[k]) * scale[c0 + k] + shift[c0 + k];
+      float v = bf2f(yp[k]) * sc[k] + sh[k];
       if (res) v += bf2f(rp[k]);
       z[k] = f2bf(v);
       o[k] = f2bf(act_f(v, act));
@@ -172,8 +234,7 @@ bn_bwd_reduce_kernel(const bf16_t* __restrict__ dout, const bf16_t* __restrict__
       const int c = cg * 8 + k;
       sc[k] = scale[c]; sh[k] = shift[c]; mu[k] = mean[c]; rs[k] = rstd[c];
     }
-    for (int m = blockIdx.x * rpi + r0; m < M; m += gridDim.x * rpi) {
-      const int64_t o = (int64_t)m * C + cg * 8;
+    MDA_ROW_LOOP({
       uint4 yv = *(const uint4*)(y + o);
       uint4 dv = dout ? *(const uint4*)(dout + o) : make_uint4(0, 0, 0, 0);
       uint4 pv = dpre ? *(const uint4*)(dpre + o) : make_uint4(0, 0, 0, 0);
@@ -182,7 +243,7 @@ bn_bwd_reduce_kernel(const bf16_t* __restrict__ dout, const bf16_t* __restrict__
       const bf16_t* de = (const bf16_t*)&dv;
       const bf16_t* pe = (const bf16_t*)&pv;
       const bf16_t* re = (const bf16_t*)&rv;
-#pragma unroll
+_Pragma("unroll")
       for (int k = 0; k < 8; ++k) {
         const float yf = bf2f(ye[k]);
         float dz = bf2f(de[k]);
@@ -195,13 +256,14 @@ bn_bwd_reduce_kernel(const bf16_t* __restrict__ dout, const bf16_t* __restrict__
         sdz[k] += dz;
         sdzx[k] += dz * (yf - mu[k]) * rs[k];
       }
-    }
+    })
   }
   block_channel_partials(sdz, sdzx, C, rpi, partial);
-  if (mda_arrive(counter, gridDim.x)) {
+  __shared__ double tot[2 * 2048];
+  if (combine_partials(partial, 2 * C, counter, tot)) {
     for (int t = threadIdx.x; t < 2 * C; t += blockDim.x) {
       const int q = t / C, c = t - q * C;
-      const float v = (float)sum_blocks(partial, gridDim.x, C, q, c);
+      const float v = (float)tot[t];
       sums[t] = v;  // [0, C): sum dz (= dbeta), [C, 2C): sum dz*xhat (= dgamma)
       if (q == 0 && dbeta) dbeta[c] += v;
       if (q == 1 && dgamma) dgamma[c] += v;
@@ -219,9 +281,27 @@ bn_bwd_apply_kernel(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ 
   const int64_t total = M * C / 8;
   const int c8 = C / 8;
   const float invM = 1.f / (float)M;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int c0 = (int)(i % c8) * 8;
+  const int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int c0 = (int)(i0 % c8) * 8;
+  float sc[8], sh[8], mu[8], rs[8], s0[8], s1[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int c = c0 + k;
+    sc[k] = scale[c]; sh[k] = shift[c]; mu[k] = mean[c]; rs[k] = rstd[c];
+    s0[k] = sums[c] * invM; s1[k] = sums[C + c] * invM;
+  }
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const bool fixed = (stride % c8) == 0;
+  for (int64_t i = i0; i < total; i += stride) {
+    if (!fixed) {
+      const int cc = (int)(i % c8) * 8;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int c = cc + k;
+        sc[k] = scale[c]; sh[k] = shift[c]; mu[k] = mean[c]; rs[k] = rstd[c];
+        s0[k] = sums[c] * invM; s1[k] = sums[C + c] * invM;
+      }
+    }
     uint4 yv = ((const uint4*)y)[i];
     uint4 dv = dout ? ((const uint4*)dout)[i] : make_uint4(0, 0, 0, 0);
     uint4 pv = dpre ? ((const uint4*)dpre)[i] : make_uint4(0, 0, 0, 0);
@@ -233,17 +313,16 @@ bn_bwd_apply_kernel(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ 
     bf16_t o[8], r[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const int c = c0 + k;
       const float yf = bf2f(yp[k]);
       float dz = bf2f(dp[k]);
       if (act != ACT_NONE) {
-        float z = yf * scale[c] + shift[c];
+        float z = yf * sc[k] + sh[k];
         if (res) z += bf2f(rp[k]);
         dz *= act_grad(z, act);
       }
       if (dpre) dz += bf2f(pp[k]);
-      const float xhat = (yf - mean[c]) * rstd[c];
-      const float g = scale[c] * (dz - (sums[c] + xhat * sums[C + c]) * invM);
+      const float xhat = (yf - mu[k]) * rs[k];
+      const float g = sc[k] * (dz - (s0[k] + xhat * s1[k]));
       o[k] = f2bf(g);
       r[k] = f2bf(dz);
     }
@@ -253,32 +332,35 @@ bn_bwd_apply_kernel(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ 
 }
 
 inline int reduce_blocks(int64_t M, int64_t C) {
-  // ~16 sixteen-byte vectors per thread, at most 256 blocks (partials stay small)
-  int64_t b = (M * (C / 8) + 256 * 16 - 1) / (256 * 16);
+  // ~8 sixteen-byte vectors per thread (issued 4 at a time), up to one block
+  // per CU; the two-level combine keeps the tail short at any block count
+  int64_t b = (M * (C / 8) + 256 * 8 - 1) / (256 * 8);
   if (b < 1) b = 1;
-  if (b > 256) b = 256;
+  if (b > RED_MAX_BLOCKS) b = RED_MAX_BLOCKS;
   return (int)b;
 }
 
 inline int ew_blocks(int64_t n8) {
-  int64_t b = (n8 + 255) / 256;
-  if (b > 4096) b = 4096;
-  if (b < 1) b = 1;
+  // power of two, so the grid stride is a multiple of C/8 (hoisted per-channel params)
+  int64_t want = (n8 + 255) / 256;
+  int64_t b = 1;
+  while (b < want && b < 2048) b <<= 1;
   return (int)b;
 }
 
 }  // namespace
 
-// Workspace: partial >= 2*C*256 floats; counter: one zeroed uint.  C % 8 == 0, C <= 2048.
+// Workspace: partial >= 2*C*(256+16) floats; counter: 17 zeroed uints.  C % 8 == 0, C <= 2048.
 MDA_API int mda_bn_stats(const void* y, int64_t M, int64_t C, float* partial, unsigned* counter,
                          const float* gamma, const float* beta, float* running_mean,
                          float* running_var, float* mean, float* rstd, float* scale,
-                         float* shift, float momentum, float eps, hipStream_t st) {
+                         float* shift, float momentum, float eps, int64_t* nbt,
+                         hipStream_t st) {
   if (C % 8 || C / 8 > 256 || C > 2048) return (int)hipErrorInvalidValue;
   dim3 grid(reduce_blocks(M, C));
   hipLaunchKernelGGL(bn_stats_kernel, grid, dim3(256), 0, st, (const bf16_t*)y, (int)M, (int)C,
                      partial, counter, gamma, beta, running_mean, running_var, mean, rstd, scale,
-                     shift, momentum, eps);
+                     shift, momentum, eps, nbt);
   MDA_CHECK_LAUNCH();
 }
 

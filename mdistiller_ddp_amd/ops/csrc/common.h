@@ -14,11 +14,15 @@ struct bf16x { bf16_t v; };  // tag type for templates
 __device__ __forceinline__ float bf2f(bf16_t b) {
   return __uint_as_float(((uint32_t)b) << 16);
 }
+// gfx950 converts natively (v_cvt_pk_bf16_f32: round-to-nearest-even, NaN kept)
 __device__ __forceinline__ bf16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return (bf16_t)((u >> 16) | 0x40);  // NaN
-  u += 0x7fffu + ((u >> 16) & 1u);  // round to nearest even
-  return (bf16_t)(u >> 16);
+  return __builtin_bit_cast(bf16_t, (__bf16)f);
+}
+typedef __attribute__((ext_vector_type(2))) __bf16 mda_bf16x2;
+// two floats -> packed bf16 pair (lo = a), one instruction
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  mda_bf16x2 v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
 }
 
 template <typename T> struct io;

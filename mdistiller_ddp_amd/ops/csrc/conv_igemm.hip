@@ -15,11 +15,14 @@
 //
 // Tiling: 256 threads = 4 waves as 2x2; block tile BM x BN x 64, wave tile
 // (BM/2) x (BN/2) built from 16x16x32 bf16 MFMAs (2 k-substeps per stage).
-// A/B K-slices are staged global -> VGPR -> LDS with a register prefetch of
-// stage s+1 while stage s computes; two LDS buffers, one barrier per stage.
-// LDS rows are 144 B (64 bf16 + 16 B pad): row starts land on 16 distinct
-// 4-bank slots, so every 16-lane group of a ds_read_b128 fragment read is
-// conflict-free.
+// A/B K-slices are staged global -> VGPR -> LDS with two register sets
+// (stage s+2 in flight while s+1 is written and s computed), two LDS
+// buffers, one barrier per stage.  Global reads are buffer loads with 32-bit
+// offsets; padding taps / tails read as zero through the descriptor range
+// check instead of branching.  LDS rows are 144 B (64 bf16 + 16 B pad): row
+// starts land on 16 distinct 4-bank slots, so every 16-lane group of a
+// ds_read_b128 fragment read is conflict-free.  The epilogue goes through
+// an fp32 LDS C tile so each thread stores 8 channels (16 B) per row.
 //
 // Narrow-M layers (the 8x8 / 16x16 CIFAR stages at small batch) do not fill
 // 256 CUs with output tiles alone, so the K loop is split over gridDim.z;
@@ -53,7 +56,22 @@ struct ConvParams {
   float* partial;        // [splits, M, Cout] when split-K
   int N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, K, Kp, M, act;
   int steps_per_split;
+  int x_bytes, w_bytes;  // buffer-descriptor ranges (< 2 GiB, checked on the host)
 };
+
+// Buffer loads: 32-bit per-lane byte offsets against a wave-uniform
+// descriptor; an offset past the range returns zeros, which is how padding
+// taps, tail rows and tail channels are zero-filled without exec-mask
+// branches around every load.
+constexpr uint32_t OOB = 0x80000000u;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* ptr, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(ptr), (short)0, bytes, 0x00020000);
+}
+__device__ __forceinline__ uint4 ld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
 
 __device__ __forceinline__ float apply_act(float v, int act) {
   if (act == ACT_RELU) return fmaxf(v, 0.f);
@@ -69,16 +87,67 @@ __device__ __forceinline__ void epilogue_store(const ConvParams& p, int m, int c
   p.y[o] = f2bf(apply_act(v, p.act));
 }
 
+// 8 consecutive channels [co, co+8) of row m (Cout % 8 == 0): 16-byte
+// residual load, preact and output stores; sc/bi already hold the channels'
+// scale and bias.
+__device__ __forceinline__ void epilogue_store8(const ConvParams& p, int m, int co, const float* v,
+                                                const float* sc, const float* bi) {
+  const int64_t o = (int64_t)m * p.Cout + co;
+  float t[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) t[e] = v[e] * sc[e] + bi[e];
+  if (p.res) {
+    const uint4 r = *(const uint4*)(p.res + o);
+    const uint32_t rr[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      t[2 * e] += __uint_as_float(rr[e] << 16);
+      t[2 * e + 1] += __uint_as_float(rr[e] & 0xffff0000u);
+    }
+  }
+  if (p.preact)
+    *(uint4*)(p.preact + o) = make_uint4(pack_bf16x2(t[0], t[1]), pack_bf16x2(t[2], t[3]),
+                                         pack_bf16x2(t[4], t[5]), pack_bf16x2(t[6], t[7]));
+#pragma unroll
+  for (int e = 0; e < 8; ++e) t[e] = apply_act(t[e], p.act);
+  *(uint4*)(p.y + o) = make_uint4(pack_bf16x2(t[0], t[1]), pack_bf16x2(t[2], t[3]),
+                                  pack_bf16x2(t[4], t[5]), pack_bf16x2(t[6], t[7]));
+}
+
+__device__ __forceinline__ void load_scale_bias8(const ConvParams& p, int co, float* sc, float* bi) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sc[e] = p.scale ? p.scale[co + e] : 1.f;
+    bi[e] = p.bias ? p.bias[co + e] : 0.f;
+  }
+}
+
+template <int BM, int BN>
+struct ConvSmem {
+  static constexpr int STAGE = 2 * (BM + BN) * LDS_ROW * 2;  // bytes, double-buffered A+B
+  static constexpr int CS = BN + 4;                          // fp32 C-tile row (floats)
+  static constexpr int CTILE = BM * CS * 4;
+  static constexpr int BYTES = STAGE > CTILE ? STAGE : CTILE;
+};
+
+// Occupancy hint: without it the compiler spends up to 512 registers on a
+// 256-thread block (1 block per CU); two 4-wave blocks per CU keep the
+// register budget at 256 (no spills except the 128x128 tile, left free).
+template <int BM, int BN>
+struct ConvOcc { static constexpr int W = (BM * BN >= 16384) ? 1 : 2; };
+
 template <int BM, int BN, int MODE>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ConvOcc<BM, BN>::W)))
 conv_fwd_kernel(const ConvParams p) {
   constexpr int MI = BM / 32;  // 16-row MFMA tiles per wave (wave tile = BM/2 rows)
   constexpr int NI = BN / 32;
   constexpr int AROWS = BM / 32;  // A rows loaded per thread per stage (8 chunks per row)
   constexpr int BLOADS = (BN * 8 + 255) / 256;
+  constexpr bool DGRAD = (MODE == LOAD_DGRAD_FAST || MODE == LOAD_DGRAD_VEC8);
 
-  __shared__ __attribute__((aligned(16))) bf16_t As[2][BM][LDS_ROW];
-  __shared__ __attribute__((aligned(16))) bf16_t Bs[2][BN][LDS_ROW];
+  __shared__ __attribute__((aligned(16))) char smem[ConvSmem<BM, BN>::BYTES];
+  bf16_t* const As = (bf16_t*)smem;                 // [2][BM][LDS_ROW]
+  bf16_t* const Bs = As + 2 * BM * LDS_ROW;         // [2][BN][LDS_ROW]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -89,20 +158,22 @@ conv_fwd_kernel(const ConvParams p) {
   const int chunk = tid & 7;
   const int arow = tid >> 3;
   const int HoWo = p.Ho * p.Wo;
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(p.x, p.x_bytes);
+  const __amdgpu_buffer_rsrc_t wr = make_rsrc(p.w, p.w_bytes);
 
-  int a_n[AROWS], a_ih0[AROWS], a_iw0[AROWS];
-  bool a_ok[AROWS];
+  // per A row: element offset of the image (n) and the window origin
+  int a_img[AROWS], a_ih0[AROWS], a_iw0[AROWS];
 #pragma unroll
   for (int j = 0; j < AROWS; ++j) {
     int m = m0 + arow + 32 * j;
-    a_ok[j] = m < p.M;
-    int mm = a_ok[j] ? m : 0;
+    const bool ok = m < p.M;
+    int mm = ok ? m : 0;
     int n = mm / HoWo;
     int r = mm - n * HoWo;
     int oh = r / p.Wo;
     int ow = r - oh * p.Wo;
-    a_n[j] = n;
-    if (MODE == LOAD_DGRAD_FAST || MODE == LOAD_DGRAD_VEC8) {
+    a_img[j] = n * p.H * p.W * p.Cin;
+    if (DGRAD) {
       // dgrad: output row = input-gradient pixel (ih, iw); taps gather dy at
       // oh = (ih + pad - kh) / stride when divisible and in range
       a_ih0[j] = oh + p.pad;
@@ -111,41 +182,47 @@ conv_fwd_kernel(const ConvParams p) {
       a_ih0[j] = oh * p.stride - p.pad;
       a_iw0[j] = ow * p.stride - p.pad;
     }
+    if (!ok) a_ih0[j] = -(1 << 28);  // every tap out of range -> zero row
+  }
+  // B (weights) rows: per-lane byte offsets, OOB past Cout
+  uint32_t b_off[BLOADS];
+#pragma unroll
+  for (int j = 0; j < BLOADS; ++j) {
+    int idx = tid + 256 * j;
+    int row = idx >> 3, ch = idx & 7;
+    int co = n0 + row;
+    b_off[j] = (row < BN && co < p.Cout) ? (uint32_t)((co * p.Kp + ch * 8) * 2) : OOB;
   }
 
-  uint4 ra[AROWS];
-  uint4 rb[BLOADS];
+  // two register staging sets: stage s+2 is in flight while stage s+1 is
+  // being written to LDS and stage s is computed
+  uint4 ra0[AROWS], rb0[BLOADS], ra1[AROWS], rb1[BLOADS];
   const int total_steps = p.Kp / BK;
   const int s_begin = blockIdx.z * p.steps_per_split;
   const int s_end = min(total_steps, s_begin + p.steps_per_split);
-  const int cin_blocks = p.Cin / BK;  // FAST mode only
+  const int cin_blocks = p.Cin / BK;  // FAST modes only
 
-  auto load_step = [&](int s) {
-    if (MODE == LOAD_FAST) {
-      const int tap = s / cin_blocks;
-      const int c0 = (s - tap * cin_blocks) * BK + chunk * 8;
+  auto load_step = [&](int s, uint4 (&ra)[AROWS], uint4 (&rb)[BLOADS]) {
+    if (MODE == LOAD_FAST || MODE == LOAD_VEC8) {
+      int tap, c0;
+      bool kok = true;
+      if (MODE == LOAD_FAST) {
+        tap = s / cin_blocks;  // wave-uniform
+        c0 = (s - tap * cin_blocks) * BK + chunk * 8;
+      } else {
+        const int k0 = s * BK + chunk * 8;
+        tap = k0 / p.Cin;
+        c0 = k0 - tap * p.Cin;
+        kok = k0 < p.K;
+      }
       const int kh = tap / p.KW, kw = tap - kh * p.KW;
 #pragma unroll
       for (int j = 0; j < AROWS; ++j) {
-        int ih = a_ih0[j] + kh, iw = a_iw0[j] + kw;
-        bool ok = a_ok[j] && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-        ra[j] = ok ? *(const uint4*)(p.x + (((int64_t)a_n[j] * p.H + ih) * p.W + iw) * p.Cin + c0)
-                   : make_uint4(0, 0, 0, 0);
+        const int ih = a_ih0[j] + kh, iw = a_iw0[j] + kw;
+        const bool ok = kok && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+        ra[j] = ld16(xr, ok ? (uint32_t)((a_img[j] + (ih * p.W + iw) * p.Cin + c0) * 2) : OOB);
       }
-    } else if (MODE == LOAD_VEC8) {
-      const int k0 = s * BK + chunk * 8;
-      const int tap = k0 / p.Cin;
-      const int c0 = k0 - tap * p.Cin;
-      const int kh = tap / p.KW, kw = tap - kh * p.KW;
-      const bool kok = k0 < p.K;
-#pragma unroll
-      for (int j = 0; j < AROWS; ++j) {
-        int ih = a_ih0[j] + kh, iw = a_iw0[j] + kw;
-        bool ok = kok && a_ok[j] && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-        ra[j] = ok ? *(const uint4*)(p.x + (((int64_t)a_n[j] * p.H + ih) * p.W + iw) * p.Cin + c0)
-                   : make_uint4(0, 0, 0, 0);
-      }
-    } else if (MODE == LOAD_DGRAD_FAST || MODE == LOAD_DGRAD_VEC8) {
+    } else if (DGRAD) {
       int tap, c0;
       bool kok = true;
       if (MODE == LOAD_DGRAD_FAST) {
@@ -161,54 +238,54 @@ conv_fwd_kernel(const ConvParams p) {
 #pragma unroll
       for (int j = 0; j < AROWS; ++j) {
         const int nh = a_ih0[j] - kh, nw = a_iw0[j] - kw;
-        bool ok = kok && a_ok[j] && nh >= 0 && nw >= 0;
-        int ih = 0, iw = 0;
-        if (p.stride == 1) {
-          ih = nh; iw = nw;
-        } else {
+        bool ok = kok && nh >= 0 && nw >= 0;
+        int ih = nh, iw = nw;
+        if (p.stride != 1) {
           ok = ok && (nh % p.stride == 0) && (nw % p.stride == 0);
-          ih = nh / p.stride; iw = nw / p.stride;
+          ih = nh / p.stride;
+          iw = nw / p.stride;
         }
         ok = ok && ih < p.H && iw < p.W;
-        ra[j] = ok ? *(const uint4*)(p.x + (((int64_t)a_n[j] * p.H + ih) * p.W + iw) * p.Cin + c0)
-                   : make_uint4(0, 0, 0, 0);
+        ra[j] = ld16(xr, ok ? (uint32_t)((a_img[j] + (ih * p.W + iw) * p.Cin + c0) * 2) : OOB);
       }
     } else {
 #pragma unroll
       for (int j = 0; j < AROWS; ++j) {
-        bf16_t v[8];
+        uint32_t v[4];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          int k = s * BK + chunk * 8 + e;
-          int tap = k / p.Cin;
-          int c = k - tap * p.Cin;
-          int kh = tap / p.KW, kw = tap - kh * p.KW;
-          int ih = a_ih0[j] + kh, iw = a_iw0[j] + kw;
-          bool ok = k < p.K && a_ok[j] && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-          v[e] = ok ? p.x[(((int64_t)a_n[j] * p.H + ih) * p.W + iw) * p.Cin + c] : (bf16_t)0;
+        for (int e2 = 0; e2 < 4; ++e2) {
+          uint32_t pair = 0;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int k = s * BK + chunk * 8 + 2 * e2 + h;
+            const int tap = k / p.Cin;
+            const int c = k - tap * p.Cin;
+            const int kh = tap / p.KW, kw = tap - kh * p.KW;
+            const int ih = a_ih0[j] + kh, iw = a_iw0[j] + kw;
+            const bool ok = k < p.K && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+            const uint32_t e = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(
+                xr, ok ? (int)((a_img[j] + (ih * p.W + iw) * p.Cin + c) * 2) : (int)OOB, 0, 0);
+            pair |= e << (16 * h);
+          }
+          v[e2] = pair;
         }
-        ra[j] = *(uint4*)v;
+        ra[j] = make_uint4(v[0], v[1], v[2], v[3]);
       }
     }
 #pragma unroll
-    for (int j = 0; j < BLOADS; ++j) {
-      int idx = tid + 256 * j;
-      int row = idx >> 3, ch = idx & 7;
-      int co = n0 + row;
-      rb[j] = (row < BN && co < p.Cout)
-                  ? *(const uint4*)(p.w + (int64_t)co * p.Kp + s * BK + ch * 8)
-                  : make_uint4(0, 0, 0, 0);
-    }
+    for (int j = 0; j < BLOADS; ++j)
+      rb[j] = ld16(wr, b_off[j] == OOB ? OOB : b_off[j] + s * BK * 2);
   };
 
-  auto store_step = [&](int buf) {
+  auto store_step = [&](int buf, const uint4 (&ra)[AROWS], const uint4 (&rb)[BLOADS]) {
 #pragma unroll
-    for (int j = 0; j < AROWS; ++j) *(uint4*)&As[buf][arow + 32 * j][chunk * 8] = ra[j];
+    for (int j = 0; j < AROWS; ++j)
+      *(uint4*)&As[(buf * BM + arow + 32 * j) * LDS_ROW + chunk * 8] = ra[j];
 #pragma unroll
     for (int j = 0; j < BLOADS; ++j) {
       int idx = tid + 256 * j;
       int row = idx >> 3, ch = idx & 7;
-      if (row < BN) *(uint4*)&Bs[buf][row][ch * 8] = rb[j];
+      if (row < BN) *(uint4*)&Bs[(buf * BN + row) * LDS_ROW + ch * 8] = rb[j];
     }
   };
 
@@ -218,62 +295,125 @@ conv_fwd_kernel(const ConvParams p) {
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  if (s_begin < s_end) {
-    load_step(s_begin);
-    store_step(0);
-  }
-  __syncthreads();
-
   const int frow = lane & 15;
   const int fk = (lane >> 4) * 8;
-  for (int s = s_begin; s < s_end; ++s) {
-    const int buf = (s - s_begin) & 1;
-    const bool more = s + 1 < s_end;
-    if (more) load_step(s + 1);
+  auto compute = [&](int buf) {
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 32) {
       bf16x8 af[MI], bfr[NI];
 #pragma unroll
       for (int i = 0; i < MI; ++i)
-        af[i] = *(const bf16x8*)&As[buf][wm * (BM / 2) + i * 16 + frow][kk + fk];
+        af[i] = *(const bf16x8*)&As[(buf * BM + wm * (BM / 2) + i * 16 + frow) * LDS_ROW + kk + fk];
 #pragma unroll
       for (int j = 0; j < NI; ++j)
-        bfr[j] = *(const bf16x8*)&Bs[buf][wn * (BN / 2) + j * 16 + frow][kk + fk];
+        bfr[j] = *(const bf16x8*)&Bs[(buf * BN + wn * (BN / 2) + j * 16 + frow) * LDS_ROW + kk + fk];
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NI; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (more) store_step(buf ^ 1);
+  };
+
+  const int n = s_end - s_begin;
+  if (n > 0) load_step(s_begin, ra0, rb0);
+  if (n > 1) load_step(s_begin + 1, ra1, rb1);
+  if (n > 0) store_step(0, ra0, rb0);
+  __syncthreads();
+  // unrolled by two so both register sets stay statically indexed
+  for (int t = 0; t < n; t += 2) {
+    if (t + 2 < n) load_step(s_begin + t + 2, ra0, rb0);
+    compute(0);
+    if (t + 1 < n) store_step(1, ra1, rb1);
+    __syncthreads();
+    if (t + 1 >= n) break;
+    if (t + 3 < n) load_step(s_begin + t + 3, ra1, rb1);
+    compute(1);
+    if (t + 2 < n) store_step(0, ra0, rb0);
     __syncthreads();
   }
 
-  const int ecol = lane & 15;
-  const int erow = (lane >> 4) * 4;
+  // Epilogue through LDS: the fp32 C tile is written in MFMA layout, then
+  // each thread owns 8 consecutive channels of a row -> 16-byte residual
+  // loads and output stores, scale/bias loaded once per thread.
+  constexpr int CS = ConvSmem<BM, BN>::CS;
+  float* const Cs = (float*)smem;
+  {
+    const int ecol = lane & 15;
+    const int erow = (lane >> 4) * 4;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          Cs[(wm * (BM / 2) + i * 16 + erow + r) * CS + wn * (BN / 2) + j * 16 + ecol] = acc[i][j][r];
+  }
+  __syncthreads();
+  constexpr int TPR = BN / 8;    // threads per row
+  constexpr int RPP = 256 / TPR; // rows per pass
+  const int c8 = tid % TPR;
+  const int rr = tid / TPR;
+  const int co = n0 + c8 * 8;
   const bool split = gridDim.z > 1;
-#pragma unroll
-  for (int j = 0; j < NI; ++j) {
-    const int co = n0 + wn * (BN / 2) + j * 16 + ecol;
-    if (co >= p.Cout) continue;
-#pragma unroll
-    for (int i = 0; i < MI; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * (BM / 2) + i * 16 + erow + r;
-        if (m >= p.M) continue;
+  if ((p.Cout & 7) == 0) {
+    if (co >= p.Cout) return;
+    float sc[8], bi[8];
+    if (!split) load_scale_bias8(p, co, sc, bi);
+#pragma unroll 2
+    for (int r0 = rr; r0 < BM; r0 += RPP) {
+      const int m = m0 + r0;
+      if (m >= p.M) break;
+      const float4 lo = *(const float4*)&Cs[r0 * CS + c8 * 8];
+      const float4 hi = *(const float4*)&Cs[r0 * CS + c8 * 8 + 4];
+      if (split) {
+        float* dst = p.partial + ((int64_t)blockIdx.z * p.M + m) * p.Cout + co;
+        *(float4*)dst = lo;
+        *(float4*)(dst + 4) = hi;
+      } else {
+        const float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        epilogue_store8(p, m, co, v, sc, bi);
+      }
+    }
+  } else {
+    for (int r0 = rr; r0 < BM; r0 += RPP) {
+      const int m = m0 + r0;
+      if (m >= p.M) break;
+      for (int e = 0; e < 8; ++e) {
+        if (co + e >= p.Cout) break;
+        const float a = Cs[r0 * CS + c8 * 8 + e];
         if (split)
-          p.partial[((int64_t)blockIdx.z * p.M + m) * p.Cout + co] = acc[i][j][r];
+          p.partial[((int64_t)blockIdx.z * p.M + m) * p.Cout + co + e] = a;
         else
-          epilogue_store(p, m, co, acc[i][j][r]);
+          epilogue_store(p, m, co + e, a);
       }
     }
   }
 }
 
 // Split-K combine: y = epilogue(sum_z partial[z]) in fixed z order.
+// Cout % 8 == 0: one thread per 8 channels (16-byte traffic).
 __global__ void __launch_bounds__(256) conv_splitk_epilogue(const ConvParams p, int splits) {
   const int64_t total = (int64_t)p.M * p.Cout;
+  if ((p.Cout & 7) == 0) {
+    const int64_t t8 = total >> 3;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < t8;
+         i += (int64_t)gridDim.x * blockDim.x) {
+      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int z = 0; z < splits; ++z) {
+        const float* src = p.partial + (int64_t)z * total + i * 8;
+        const float4 lo = *(const float4*)src, hi = *(const float4*)(src + 4);
+        v[0] += lo.x; v[1] += lo.y; v[2] += lo.z; v[3] += lo.w;
+        v[4] += hi.x; v[5] += hi.y; v[6] += hi.z; v[7] += hi.w;
+      }
+      const int m = (int)((i * 8) / p.Cout);
+      const int co = (int)(i * 8 - (int64_t)m * p.Cout);
+      float sc[8], bi[8];
+      load_scale_bias8(p, co, sc, bi);
+      epilogue_store8(p, m, co, v, sc, bi);
+    }
+    return;
+  }
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
     float a = 0.f;
@@ -324,6 +464,11 @@ namespace {
 
 int dispatch(ConvParams& p, int mode, int64_t tile, int64_t splits, hipStream_t st) {
   if (p.Kp % BK || p.Kp < p.K) return (int)hipErrorInvalidValue;
+  const int64_t xb = (int64_t)p.N * p.H * p.W * p.Cin * 2, wb = (int64_t)p.Cout * p.Kp * 2;
+  if (xb >= ((int64_t)1 << 31) || wb >= ((int64_t)1 << 31) || (int64_t)p.M * p.Cout >= ((int64_t)1 << 31))
+    return (int)hipErrorInvalidValue;  // 32-bit buffer offsets
+  p.x_bytes = (int)xb;
+  p.w_bytes = (int)wb;
   if (tile == 0 || splits == 0) mda_conv_plan(p.M, p.Cout, p.Kp, &tile, &splits);
   if (splits > 1 && p.partial == nullptr) return (int)hipErrorInvalidValue;
   const int steps = p.Kp / BK;
@@ -340,7 +485,8 @@ int dispatch(ConvParams& p, int mode, int64_t tile, int64_t splits, hipStream_t 
   }
   if (rc || splits <= 1) return rc;
   int64_t total = (int64_t)p.M * p.Cout;
-  int blocks = (int)std::min<int64_t>((total + 255) / 256, 2048);
+  int64_t work = (p.Cout % 8 == 0) ? total / 8 : total;
+  int blocks = (int)std::min<int64_t>((work + 255) / 256, 2048);
   hipLaunchKernelGGL(conv_splitk_epilogue, dim3(blocks), dim3(256), 0, st, p, (int)splits);
   return (int)hipGetLastError();
 }

@@ -32,12 +32,43 @@ constexpr int ROW = 72;      // LDS row length (bf16), 144 B
 
 enum { WG_FAST = 0, WG_VEC8 = 1, WG_SCALAR = 2 };
 
+// Division by a runtime constant as multiply-high + shift (n < 2^31):
+// q = (umulhi(n, mul) + n) >> shr with shr = ceil(log2 d),
+// mul = floor(2^32 (2^shr - d) / d) + 1.
+struct FastDiv {
+  uint32_t d, mul, shr;
+};
+inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  f.shr = l;
+  f.mul = (uint32_t)((((1ull << 32) * ((1ull << l) - d)) / d) + 1);
+  return f;
+}
+__device__ __forceinline__ int fdiv(int n, const FastDiv& f) {
+  return (int)((__umulhi((uint32_t)n, f.mul) + (uint32_t)n) >> f.shr);
+}
+
 struct WgParams {
   const bf16_t* x;   // [N, H, W, Cin]
   const bf16_t* dy;  // [N, Ho, Wo, Cout]
   float* partial;    // [splits, Cout, Kp]
   int N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, K, Kp, M, m_per_split;
+  int x_bytes, dy_bytes;
+  FastDiv div_howo, div_wo;
 };
+
+constexpr uint32_t OOB = 0x80000000u;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* ptr, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(ptr), (short)0, bytes, 0x00020000);
+}
+__device__ __forceinline__ uint4 ld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
 
 __device__ __forceinline__ bf16x8 tr_frag(const bf16_t* tile, int r0, int c0, int lane) {
   // lane 16g + 4q + p supplies &tile[r0 + 8g + q (+4)][c0 + 4p]; receives column (lane & 15)
@@ -55,7 +86,7 @@ __device__ __forceinline__ bf16x8 tr_frag(const bf16_t* tile, int r0, int c0, in
 }
 
 template <int MODE>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 conv_wgrad_kernel(const WgParams p) {
   __shared__ __attribute__((aligned(16))) bf16_t Ds[2][TM * ROW];  // dy tile [m][co]
   __shared__ __attribute__((aligned(16))) bf16_t Xs[2][TM * ROW];  // im2col tile [m][k]
@@ -66,66 +97,63 @@ conv_wgrad_kernel(const WgParams p) {
   const int m_begin = blockIdx.z * p.m_per_split;
   const int m_end = min(p.M, m_begin + p.m_per_split);
   const int chunk = tid & 7, row = tid >> 3;  // 32 rows x 8 chunks per pass, 2 passes
-  const int HoWo = p.Ho * p.Wo;
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(p.x, p.x_bytes);
+  const __amdgpu_buffer_rsrc_t dr = make_rsrc(p.dy, p.dy_bytes);
 
-  // FAST mode: the whole 64-wide k tile is one tap
-  int tap_fast = 0, c_fast = 0;
+  // this thread's im2col column (fixed for the whole block): tap and channel
+  int tap, c;
+  bool kok = true;
   if (MODE == WG_FAST) {
-    tap_fast = k0 / p.Cin;
-    c_fast = k0 - tap_fast * p.Cin;
+    tap = k0 / p.Cin;  // the whole 64-wide k tile is one tap
+    c = k0 - tap * p.Cin + chunk * 8;
+  } else {
+    const int kk = k0 + chunk * 8;
+    tap = kk / p.Cin;
+    c = kk - tap * p.Cin;
+    kok = kk < p.K;
   }
+  const int kh = tap / p.KW, kw = tap - kh * p.KW;
+  const int co = co0 + chunk * 8;
+  const bool cok = co < p.Cout;
 
-  uint4 rd[2], rx[2];
-  auto load = [&](int mb) {
+  auto load = [&](int mb, uint4 (&rd)[2], uint4 (&rx)[2]) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int r = row + 32 * j;
-      const int m = mb + r;
+      const int m = mb + row + 32 * j;
       const bool mok = m < m_end;
-      const int co = co0 + chunk * 8;
-      rd[j] = (mok && co < p.Cout) ? *(const uint4*)(p.dy + (int64_t)m * p.Cout + co)
-                                   : make_uint4(0, 0, 0, 0);
-      int n = 0, oh = 0, ow = 0;
-      if (mok) {
-        n = m / HoWo;
-        int rr = m - n * HoWo;
-        oh = rr / p.Wo;
-        ow = rr - oh * p.Wo;
-      }
+      rd[j] = ld16(dr, (mok && cok) ? (uint32_t)((m * p.Cout + co) * 2) : OOB);
+      const int n = fdiv(m, p.div_howo);
+      const int rr = m - n * p.Ho * p.Wo;
+      const int oh = fdiv(rr, p.div_wo);
+      const int ow = rr - oh * p.Wo;
       if (MODE == WG_FAST || MODE == WG_VEC8) {
-        int tap, c;
-        bool kok = true;
-        if (MODE == WG_FAST) {
-          tap = tap_fast;
-          c = c_fast + chunk * 8;
-        } else {
-          const int kk = k0 + chunk * 8;
-          tap = kk / p.Cin;
-          c = kk - tap * p.Cin;
-          kok = kk < p.K;
-        }
-        const int kh = tap / p.KW, kw = tap - kh * p.KW;
         const int ih = oh * p.stride - p.pad + kh, iw = ow * p.stride - p.pad + kw;
         const bool ok = kok && mok && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-        rx[j] = ok ? *(const uint4*)(p.x + (((int64_t)n * p.H + ih) * p.W + iw) * p.Cin + c)
-                   : make_uint4(0, 0, 0, 0);
+        rx[j] = ld16(xr, ok ? (uint32_t)((((n * p.H + ih) * p.W + iw) * p.Cin + c) * 2) : OOB);
       } else {
-        bf16_t v[8];
+        uint32_t v[4];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int kk = k0 + chunk * 8 + e;
-          const int tap = kk / p.Cin;
-          const int c = kk - tap * p.Cin;
-          const int kh = tap / p.KW, kw = tap - kh * p.KW;
-          const int ih = oh * p.stride - p.pad + kh, iw = ow * p.stride - p.pad + kw;
-          const bool ok = kk < p.K && mok && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-          v[e] = ok ? p.x[(((int64_t)n * p.H + ih) * p.W + iw) * p.Cin + c] : (bf16_t)0;
+        for (int e2 = 0; e2 < 4; ++e2) {
+          uint32_t pair = 0;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int kk = k0 + chunk * 8 + 2 * e2 + h;
+            const int tp = kk / p.Cin;
+            const int ce = kk - tp * p.Cin;
+            const int kh2 = tp / p.KW, kw2 = tp - kh2 * p.KW;
+            const int ih = oh * p.stride - p.pad + kh2, iw = ow * p.stride - p.pad + kw2;
+            const bool ok = kk < p.K && mok && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+            const uint32_t e = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(
+                xr, ok ? (int)((((n * p.H + ih) * p.W + iw) * p.Cin + ce) * 2) : (int)OOB, 0, 0);
+            pair |= e << (16 * h);
+          }
+          v[e2] = pair;
         }
-        rx[j] = *(uint4*)v;
+        rx[j] = make_uint4(v[0], v[1], v[2], v[3]);
       }
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf, const uint4 (&rd)[2], const uint4 (&rx)[2]) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int r = row + 32 * j;
@@ -140,16 +168,7 @@ conv_wgrad_kernel(const WgParams p) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  const int nst = (m_end - m_begin + TM - 1) / TM;
-  if (nst > 0) {
-    load(m_begin);
-    store(0);
-  }
-  __syncthreads();
-  for (int s = 0; s < nst; ++s) {
-    const int buf = s & 1;
-    const bool more = s + 1 < nst;
-    if (more) load(m_begin + (s + 1) * TM);
+  auto compute = [&](int buf) {
 #pragma unroll
     for (int kk = 0; kk < TM; kk += 32) {
       bf16x8 af[2], bfr[2];
@@ -163,7 +182,25 @@ conv_wgrad_kernel(const WgParams p) {
         for (int j = 0; j < 2; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (more) store(buf ^ 1);
+  };
+
+  // two register staging sets (stage s+2 in flight while s+1 is written to
+  // LDS and s computed), loop unrolled by two to keep them static
+  uint4 rd0[2], rx0[2], rd1[2], rx1[2];
+  const int n = (m_end - m_begin + TM - 1) / TM;
+  if (n > 0) load(m_begin, rd0, rx0);
+  if (n > 1) load(m_begin + TM, rd1, rx1);
+  if (n > 0) store(0, rd0, rx0);
+  __syncthreads();
+  for (int t = 0; t < n; t += 2) {
+    if (t + 2 < n) load(m_begin + (t + 2) * TM, rd0, rx0);
+    compute(0);
+    if (t + 1 < n) store(1, rd1, rx1);
+    __syncthreads();
+    if (t + 1 >= n) break;
+    if (t + 3 < n) load(m_begin + (t + 3) * TM, rd1, rx1);
+    compute(1);
+    if (t + 2 < n) store(0, rd0, rx0);
     __syncthreads();
   }
   const int ecol = lane & 15, erow = (lane >> 4) * 4;
@@ -173,10 +210,10 @@ conv_wgrad_kernel(const WgParams p) {
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int co = co0 + wm * 32 + i * 16 + erow + r;
+        const int oc = co0 + wm * 32 + i * 16 + erow + r;
         const int k = k0 + wn * 32 + j * 16 + ecol;
-        if (co < p.Cout && k < p.Kp)
-          p.partial[((int64_t)blockIdx.z * p.Cout + co) * p.Kp + k] = acc[i][j][r];
+        if (oc < p.Cout && k < p.Kp)
+          p.partial[((int64_t)blockIdx.z * p.Cout + oc) * p.Kp + k] = acc[i][j][r];
       }
 }
 
@@ -261,6 +298,12 @@ MDA_API int mda_conv_wgrad(const void* x, const void* dy, float* partial, float*
   p.x = (const bf16_t*)x; p.dy = (const bf16_t*)dy; p.partial = partial;
   p.N = N; p.H = H; p.W = W; p.Cin = Cin; p.Ho = Ho; p.Wo = Wo; p.Cout = Cout; p.KH = KH;
   p.KW = KW; p.stride = stride; p.pad = pad; p.K = KH * KW * Cin; p.Kp = Kp; p.M = N * Ho * Wo;
+  const int64_t xb = N * H * W * Cin * 2, db = N * Ho * Wo * Cout * 2;
+  if (xb >= ((int64_t)1 << 31) || db >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
+  p.x_bytes = (int)xb;
+  p.dy_bytes = (int)db;
+  p.div_howo = make_fastdiv((uint32_t)(Ho * Wo));
+  p.div_wo = make_fastdiv((uint32_t)Wo);
   if (splits <= 0) mda_wgrad_plan(p.M, Cout, Kp, &splits);
   p.m_per_split = (int)(((p.M + splits - 1) / splits + TM - 1) / TM * TM);
   dim3 grid((int)((Cout + TC - 1) / TC), (int)(Kp / TK), (int)splits);

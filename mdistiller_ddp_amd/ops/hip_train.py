@@ -32,7 +32,7 @@ class _WS:
     """Per-device scratch for the BN reductions (partials + arrival counters)."""
 
     def __init__(self, device):
-        self.partial = torch.zeros(2 * 2048 * 256, dtype=torch.float32, device=device)
+        self.partial = torch.zeros(2 * 2048 * (256 + 16), dtype=torch.float32, device=device)
         self.counter = torch.zeros(64, dtype=torch.int32, device=device)
 
 
@@ -117,9 +117,7 @@ class _ConvBNActTrain(torch.autograd.Function):
         stats = torch.empty(4, Cout, dtype=torch.float32, device=dev)  # mean, rstd, scale, shift
         _ext.call("mda_bn_stats", y, M, Cout, ws.partial, ws.counter, gamma.detach(), beta.detach(),
                   bn.running_mean, bn.running_var, stats[0], stats[1], stats[2], stats[3],
-                  float(bn.momentum), float(bn.eps))
-        if bn.num_batches_tracked is not None:
-            bn.num_batches_tracked.add_(1)
+                  float(bn.momentum), float(bn.eps), bn.num_batches_tracked)
         res = _cl_bf16(residual) if residual is not None else None
         out = torch.empty_like(y)
         pre = torch.empty_like(y) if want_preact else None

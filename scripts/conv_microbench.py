@@ -1,0 +1,83 @@
+#!/usr/bin/env python
+"""Per-shape timing of the MFMA implicit-GEMM conv kernels vs MIOpen.
+
+For every conv shape of the north-star pair (resnet32x4 teacher, resnet8x4
+student) at batch 64: forward (inference epilogue), dgrad, wgrad; reports
+us/call and TFLOP/s, and MIOpen's bf16 channels-last time for the same op.
+
+    python scripts/conv_microbench.py [--iters 50] [--json out.json]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+SHAPES = [  # N, Cin, H, Cout, k, s, p
+    (64, 3, 32, 32, 3, 1, 1),
+    (64, 32, 32, 64, 3, 1, 1),
+    (64, 64, 32, 64, 3, 1, 1),
+    (64, 64, 32, 128, 3, 2, 1),
+    (64, 128, 16, 128, 3, 1, 1),
+    (64, 128, 16, 256, 3, 2, 1),
+    (64, 256, 8, 256, 3, 1, 1),
+    (64, 64, 32, 128, 1, 2, 0),
+]
+
+
+def timeit(fn, iters):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) * 1000.0 / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--json", default=None)
+    args = ap.parse_args()
+    from mdistiller_ddp_amd.ops import hip_layers, hip_train
+    torch.backends.cudnn.benchmark = True
+    rows = []
+    for (N, Cin, H, Cout, k, s, p) in SHAPES:
+        conv = nn.Conv2d(Cin, Cout, k, s, p, bias=False).cuda()
+        bn = nn.BatchNorm2d(Cout).cuda().eval()
+        x = torch.randn(N, Cin, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        Ho = (H + 2 * p - k) // s + 1
+        flop = 2.0 * N * Ho * Ho * Cout * Cin * k * k
+        with torch.no_grad():
+            t_fwd = timeit(lambda: hip_layers.conv_bn_act(x, conv, bn, "relu", None, False), args.iters)
+            wb = conv.weight.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+            t_mio = timeit(lambda: F.conv2d(x, wb, stride=s, padding=p), args.iters)
+            dy = torch.randn(N, Cout, Ho, Ho, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+            t_wg = timeit(lambda: hip_train.conv_wgrad(x, dy, tuple(conv.weight.shape), s, p), args.iters)
+            t_dg = float("nan")
+            if Cin % 8 == 0:
+                t_dg = timeit(lambda: hip_train.conv_dgrad(dy, conv.weight, tuple(x.shape), s, p), args.iters)
+        row = dict(shape=[N, Cin, H, Cout, k, s, p], gflop=flop / 1e9, fwd_us=t_fwd,
+                   fwd_tflops=flop / t_fwd / 1e6, miopen_fwd_us=t_mio, dgrad_us=t_dg,
+                   wgrad_us=t_wg, wgrad_tflops=flop / t_wg / 1e6)
+        rows.append(row)
+        print(json.dumps({k_: (round(v, 2) if isinstance(v, float) else v) for k_, v in row.items()}),
+              flush=True)
+    if args.json:
+        with open(args.json, "w") as f:
+            json.dump(rows, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -42,3 +42,28 @@ def test_nyud_patches_to_depth():
     from tools.lineval.nyud import patches_to_depth
     x = torch.randn(2, 1 + 196, 256)
     assert patches_to_depth(x).shape == (2, 224, 224)
+
+
+def test_visualization_class_mean_logits():
+    import numpy as np
+    from tools.visualizations.correlation import class_mean_logits, discrepancy
+    logits = np.array([[1.0, 2.0], [3.0, 4.0], [5.0, 7.0]])
+    labels = np.array([0, 0, 1])
+    m = class_mean_logits(logits, labels, 3)
+    assert np.allclose(m, [[2.0, 3.0], [5.0, 7.0], [0.0, 0.0]])
+    assert np.allclose(discrepancy(logits, logits + 1.0, labels, 3)[:2], 1.0)
+
+
+def test_visualization_tools_synthetic(tmp_path):
+    import numpy as np
+    from tools.visualizations import correlation, tsne
+    out = str(tmp_path / "viz")
+    emb, labels = tsne.main(["-m", "resnet8", "--synthetic", "--max-batches", "2", "-bs", "32",
+                             "--device", "cpu", "-o", out])
+    assert emb.shape == (labels.shape[0], 2) and np.isfinite(emb).all()
+    diff = correlation.main(["-t", "resnet20", "-s", "resnet8", "--teacher-ckpt", "random",
+                             "--synthetic", "--max-batches", "2", "-bs", "32", "--device", "cpu",
+                             "-o", out])
+    assert diff.shape == (100, 100)
+    assert os.path.exists(os.path.join(out, "tsne_resnet8.png"))
+    assert os.path.exists(os.path.join(out, "corr_resnet20_resnet8.png"))

@@ -33,6 +33,7 @@
 // (Cin % 8 == 0: every 16-byte chunk lies inside one tap), SCALAR (any Cin,
 // e.g. the 3-channel stem).
 #include "common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -67,6 +68,13 @@ constexpr uint32_t OOB = 0x80000000u;
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* ptr, int bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(ptr), (short)0, bytes, 0x00020000);
+}
+// ok ? off : out-of-range, without a branch: the offset is always computed
+// and bit 31 forces it past the descriptor range (every range is < 2 GiB).
+// A select on a runtime condition made hipcc branch around each address
+// computation and load, which also broke its vmcnt bookkeeping.
+__device__ __forceinline__ uint32_t sel_off(bool ok, int off) {
+  return (uint32_t)off | ((uint32_t)(!ok) << 31);
 }
 __device__ __forceinline__ uint4 ld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
@@ -129,6 +137,72 @@ struct ConvSmem {
   static constexpr int CTILE = BM * CS * 4;
   static constexpr int BYTES = STAGE > CTILE ? STAGE : CTILE;
 };
+
+// Epilogue through LDS, shared by both conv kernels: the fp32 C tile is
+// written in MFMA layout, then each thread owns 8 consecutive channels of a
+// row -> 16-byte residual loads and output stores, scale/bias loaded once
+// per thread.  Split-K blocks write fp32 partials instead.  The caller must
+// have finished every read of `smem` (barrier) before calling.
+template <int BM, int BN>
+__device__ __forceinline__ void conv_epilogue(const ConvParams& p, const f32x4 (&acc)[BM / 32][BN / 32],
+                                              char* smem, int m0, int n0) {
+  constexpr int MI = BM / 32, NI = BN / 32;
+  constexpr int CS = ConvSmem<BM, BN>::CS;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  float* const Cs = (float*)smem;
+  {
+    const int ecol = lane & 15;
+    const int erow = (lane >> 4) * 4;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          Cs[(wm * (BM / 2) + i * 16 + erow + r) * CS + wn * (BN / 2) + j * 16 + ecol] = acc[i][j][r];
+  }
+  __syncthreads();
+  constexpr int TPR = BN / 8;    // threads per row
+  constexpr int RPP = 256 / TPR; // rows per pass
+  const int c8 = tid % TPR;
+  const int rr = tid / TPR;
+  const int co = n0 + c8 * 8;
+  const bool split = gridDim.z > 1;
+  if ((p.Cout & 7) == 0) {
+    if (co >= p.Cout) return;
+    float sc[8], bi[8];
+    if (!split) load_scale_bias8(p, co, sc, bi);
+#pragma unroll 2
+    for (int r0 = rr; r0 < BM; r0 += RPP) {
+      const int m = m0 + r0;
+      if (m >= p.M) break;
+      const float4 lo = *(const float4*)&Cs[r0 * CS + c8 * 8];
+      const float4 hi = *(const float4*)&Cs[r0 * CS + c8 * 8 + 4];
+      if (split) {
+        float* dst = p.partial + ((int64_t)blockIdx.z * p.M + m) * p.Cout + co;
+        *(float4*)dst = lo;
+        *(float4*)(dst + 4) = hi;
+      } else {
+        const float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        epilogue_store8(p, m, co, v, sc, bi);
+      }
+    }
+  } else {
+    for (int r0 = rr; r0 < BM; r0 += RPP) {
+      const int m = m0 + r0;
+      if (m >= p.M) break;
+      for (int e = 0; e < 8; ++e) {
+        if (co + e >= p.Cout) break;
+        const float a = Cs[r0 * CS + c8 * 8 + e];
+        if (split)
+          p.partial[((int64_t)blockIdx.z * p.M + m) * p.Cout + co + e] = a;
+        else
+          epilogue_store(p, m, co + e, a);
+      }
+    }
+  }
+}
 
 // Occupancy hint: without it the compiler spends up to 512 registers on a
 // 256-thread block (1 block per CU); two 4-wave blocks per CU keep the
@@ -202,10 +276,17 @@ conv_fwd_kernel(const ConvParams p) {
   const int s_end = min(total_steps, s_begin + p.steps_per_split);
   const int cin_blocks = p.Cin / BK;  // FAST modes only
 
+  // Every call issues the same number of loads, also past the end of the K
+  // range (then all offsets are OOB and the loads return zeros without
+  // touching memory): with a fixed per-iteration load count the compiler's
+  // vmcnt waits are exact.  Conditional loads made it merge the paths
+  // conservatively and wait on the just-issued prefetch every stage.
   auto load_step = [&](int s, uint4 (&ra)[AROWS], uint4 (&rb)[BLOADS]) {
+    const bool live = s < s_end;
+    s = live ? s : s_begin;
     if (MODE == LOAD_FAST || MODE == LOAD_VEC8) {
       int tap, c0;
-      bool kok = true;
+      bool kok = live;
       if (MODE == LOAD_FAST) {
         tap = s / cin_blocks;  // wave-uniform
         c0 = (s - tap * cin_blocks) * BK + chunk * 8;
@@ -220,11 +301,11 @@ conv_fwd_kernel(const ConvParams p) {
       for (int j = 0; j < AROWS; ++j) {
         const int ih = a_ih0[j] + kh, iw = a_iw0[j] + kw;
         const bool ok = kok && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-        ra[j] = ld16(xr, ok ? (uint32_t)((a_img[j] + (ih * p.W + iw) * p.Cin + c0) * 2) : OOB);
+        ra[j] = ld16(xr, sel_off(ok, (a_img[j] + (ih * p.W + iw) * p.Cin + c0) * 2));
       }
     } else if (DGRAD) {
       int tap, c0;
-      bool kok = true;
+      bool kok = live;
       if (MODE == LOAD_DGRAD_FAST) {
         tap = s / cin_blocks;
         c0 = (s - tap * cin_blocks) * BK + chunk * 8;
@@ -246,7 +327,7 @@ conv_fwd_kernel(const ConvParams p) {
           iw = nw / p.stride;
         }
         ok = ok && ih < p.H && iw < p.W;
-        ra[j] = ld16(xr, ok ? (uint32_t)((a_img[j] + (ih * p.W + iw) * p.Cin + c0) * 2) : OOB);
+        ra[j] = ld16(xr, sel_off(ok, (a_img[j] + (ih * p.W + iw) * p.Cin + c0) * 2));
       }
     } else {
 #pragma unroll
@@ -262,9 +343,9 @@ conv_fwd_kernel(const ConvParams p) {
             const int c = k - tap * p.Cin;
             const int kh = tap / p.KW, kw = tap - kh * p.KW;
             const int ih = a_ih0[j] + kh, iw = a_iw0[j] + kw;
-            const bool ok = k < p.K && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+            const bool ok = live && k < p.K && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
             const uint32_t e = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(
-                xr, ok ? (int)((a_img[j] + (ih * p.W + iw) * p.Cin + c) * 2) : (int)OOB, 0, 0);
+                xr, (int)sel_off(ok, (a_img[j] + (ih * p.W + iw) * p.Cin + c) * 2), 0, 0);
             pair |= e << (16 * h);
           }
           v[e2] = pair;
@@ -274,7 +355,7 @@ conv_fwd_kernel(const ConvParams p) {
     }
 #pragma unroll
     for (int j = 0; j < BLOADS; ++j)
-      rb[j] = ld16(wr, b_off[j] == OOB ? OOB : b_off[j] + s * BK * 2);
+      rb[j] = ld16(wr, (b_off[j] + (uint32_t)(s * BK * 2)) | ((uint32_t)(!live) << 31));
   };
 
   auto store_step = [&](int buf, const uint4 (&ra)[AROWS], const uint4 (&rb)[BLOADS]) {
@@ -316,79 +397,230 @@ conv_fwd_kernel(const ConvParams p) {
   };
 
   const int n = s_end - s_begin;
-  if (n > 0) load_step(s_begin, ra0, rb0);
-  if (n > 1) load_step(s_begin + 1, ra1, rb1);
-  if (n > 0) store_step(0, ra0, rb0);
+  load_step(s_begin, ra0, rb0);
+  load_step(s_begin + 1, ra1, rb1);
+  store_step(0, ra0, rb0);
   __syncthreads();
-  // unrolled by two so both register sets stay statically indexed
+  // unrolled by two so both register sets stay statically indexed; loads
+  // and LDS stores are unconditional (zeros past the end, see load_step)
   for (int t = 0; t < n; t += 2) {
-    if (t + 2 < n) load_step(s_begin + t + 2, ra0, rb0);
+    load_step(s_begin + t + 2, ra0, rb0);
     compute(0);
-    if (t + 1 < n) store_step(1, ra1, rb1);
+    store_step(1, ra1, rb1);
     __syncthreads();
     if (t + 1 >= n) break;
-    if (t + 3 < n) load_step(s_begin + t + 3, ra1, rb1);
+    load_step(s_begin + t + 3, ra1, rb1);
     compute(1);
-    if (t + 2 < n) store_step(0, ra0, rb0);
+    store_step(0, ra0, rb0);
     __syncthreads();
   }
 
-  // Epilogue through LDS: the fp32 C tile is written in MFMA layout, then
-  // each thread owns 8 consecutive channels of a row -> 16-byte residual
-  // loads and output stores, scale/bias loaded once per thread.
-  constexpr int CS = ConvSmem<BM, BN>::CS;
-  float* const Cs = (float*)smem;
-  {
-    const int ecol = lane & 15;
-    const int erow = (lane >> 4) * 4;
+  __syncthreads();  // (loop ended with a barrier; keeps the C tile write safe either way)
+  conv_epilogue<BM, BN>(p, acc, smem, m0, n0);
+}
+
+// ---------------------------------------------------------------------------
+// LDS-DMA variant (all modes except SCALAR).  Tiles go global -> LDS with
+// global_load_lds_dwordx4 (no VGPR staging), three LDS buffers, two stages in
+// flight, ONE barrier per stage: at iteration t the wave waits until its own
+// stage-t copies landed (vmcnt = loads of the one newer stage), the barrier
+// makes every wave's copies visible AND retires every wave's reads of the
+// buffer the next copy overwrites, then stage t+2 is issued and stage t
+// computed.  The copies are inline asm, so hipcc neither counts them nor
+// inserts vmcnt(0) drains of its own (CDNA HIP guide §5 "Pipelining across
+// barriers", §5.7).  LDS rows are 128 B, lane-linear per wave (the DMA
+// writes base + lane*16); bank conflicts of the fragment reads are removed
+// by an XOR swizzle applied on the SOURCE side: LDS slot c of row r holds
+// k-chunk c ^ ((r >> 1) & 7), so the 16 rows of a fragment read hit 16
+// distinct 16-byte bank groups.  Padding taps, tail rows and dead stages
+// read a 16-byte zero page instead of branching.
+__device__ __attribute__((aligned(16))) uint32_t g_zero16[4] = {0u, 0u, 0u, 0u};
+
+constexpr int GLDS_NBUF = 3;
+
+template <int BM, int BN>
+struct GldsSmem {
+  static constexpr int STAGE = (BM + BN) * 128;  // bytes per stage: A rows then B rows
+  static constexpr int PIPE = GLDS_NBUF * STAGE;
+  static constexpr int CTILE = ConvSmem<BM, BN>::CTILE;
+  static constexpr int BYTES = PIPE > CTILE ? PIPE : CTILE;
+};
+
+__device__ __forceinline__ void glds16(const void* src, uint32_t lds_wave_base) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds_wave_base)
+      : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(N) : "memory");
+}
+
+template <int BM, int BN>
+struct GldsOcc { static constexpr int W = (BM * BN >= 16384) ? 1 : 2; };
+
+template <int BM, int BN, int MODE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GldsOcc<BM, BN>::W)))
+conv_glds_kernel(const ConvParams p) {
+  constexpr int MI = BM / 32, NI = BN / 32;
+  constexpr int AROWS = BM / 32;
+  constexpr int BLOADS = (BN * 8 + 255) / 256;
+  constexpr int NL = AROWS + BLOADS;  // DMA instructions per stage per wave
+  constexpr int STAGE = GldsSmem<BM, BN>::STAGE;
+  constexpr bool DGRAD = (MODE == LOAD_DGRAD_FAST || MODE == LOAD_DGRAD_VEC8);
+  constexpr bool FASTK = (MODE == LOAD_FAST || MODE == LOAD_DGRAD_FAST);
+  static_assert(MODE != LOAD_SCALAR, "SCALAR gathers use conv_fwd_kernel");
+
+  __shared__ __attribute__((aligned(16))) char smem[GldsSmem<BM, BN>::BYTES];
+  typedef __attribute__((address_space(3))) char lds_char;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_char*)smem;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int m0 = blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int trow = tid >> 3;                              // row within each 32-row slab
+  const int chunk = (tid & 7) ^ ((trow >> 1) & 7);        // swizzled k-chunk this lane copies
+  const uint32_t wave_off = (uint32_t)__builtin_amdgcn_readfirstlane(wid) * 1024u;
+  const int HoWo = p.Ho * p.Wo;
+  const bf16_t* const zero = (const bf16_t*)g_zero16;
+
+  int a_img[AROWS], a_ih0[AROWS], a_iw0[AROWS];
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
+  for (int j = 0; j < AROWS; ++j) {
+    const int m = m0 + trow + 32 * j;
+    const bool ok = m < p.M;
+    const int mm = ok ? m : 0;
+    const int n = mm / HoWo;
+    const int r = mm - n * HoWo;
+    const int oh = r / p.Wo;
+    const int ow = r - oh * p.Wo;
+    a_img[j] = n * p.H * p.W * p.Cin;
+    if (DGRAD) {
+      a_ih0[j] = oh + p.pad;
+      a_iw0[j] = ow + p.pad;
+    } else {
+      a_ih0[j] = oh * p.stride - p.pad;
+      a_iw0[j] = ow * p.stride - p.pad;
+    }
+    if (!ok) a_ih0[j] = -(1 << 28);
+  }
+  const bf16_t* b_row[BLOADS];
+  bool b_ok[BLOADS];
+#pragma unroll
+  for (int j = 0; j < BLOADS; ++j) {
+    const int co = n0 + trow + 32 * j;
+    b_ok[j] = (trow + 32 * j < BN) && co < p.Cout;
+    b_row[j] = p.w + (int64_t)(b_ok[j] ? co : 0) * p.Kp + chunk * 8;
+  }
+
+  const int total_steps = p.Kp / BK;
+  const int s_begin = blockIdx.z * p.steps_per_split;
+  const int s_end = min(total_steps, s_begin + p.steps_per_split);
+  const int cin_blocks = p.Cin / BK;
+
+  // issue every copy of stage s into LDS buffer buf (always NL per wave)
+  auto issue = [&](int s, int buf) {
+    const bool live = s < s_end;
+    s = live ? s : s_begin;
+    int tap, c0;
+    bool kok = live;
+    if (FASTK) {
+      tap = s / cin_blocks;
+      c0 = (s - tap * cin_blocks) * BK + chunk * 8;
+    } else {
+      const int k0 = s * BK + chunk * 8;
+      tap = k0 / p.Cin;
+      c0 = k0 - tap * p.Cin;
+      kok = kok && k0 < p.K;
+    }
+    const int kh = tap / p.KW, kw = tap - kh * p.KW;
+    const uint32_t abase = lds0 + (uint32_t)(buf * STAGE) + wave_off;
+#pragma unroll
+    for (int j = 0; j < AROWS; ++j) {
+      int ih, iw;
+      bool ok = kok;
+      if (DGRAD) {
+        const int nh = a_ih0[j] - kh, nw = a_iw0[j] - kw;
+        ok = ok && nh >= 0 && nw >= 0;
+        ih = nh; iw = nw;
+        if (p.stride != 1) {
+          ok = ok && (nh % p.stride == 0) && (nw % p.stride == 0);
+          ih = nh / p.stride;
+          iw = nw / p.stride;
+        }
+        ok = ok && ih < p.H && iw < p.W;
+      } else {
+        ih = a_ih0[j] + kh;
+        iw = a_iw0[j] + kw;
+        ok = ok && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+      }
+      const bf16_t* src = ok ? p.x + (a_img[j] + (ih * p.W + iw) * p.Cin + c0) : zero;
+      glds16(src, abase + (uint32_t)(j * 32 * 128));
+    }
+    const uint32_t bbase = abase + (uint32_t)(BM * 128);
+#pragma unroll
+    for (int j = 0; j < BLOADS; ++j) {
+      const bf16_t* src = (live && b_ok[j]) ? b_row[j] + s * BK : zero;
+      glds16(src, bbase + (uint32_t)(j * 32 * 128));
+    }
+  };
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // fragment read offsets: row R, logical chunk q -> R*128 + ((q ^ ((R>>1)&7)) * 16);
+  // every fragment row R = (multiple of 16) + (lane & 15), so the swizzle is per-lane
+  const int frow = lane & 15;
+  const int swz = (frow >> 1) & 7;
+  const int g4 = lane >> 4;
+  auto compute = [&](int buf) {
+    const char* As = smem + buf * STAGE;
+    const char* Bs = As + BM * 128;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int coff = ((kk * 4 + g4) ^ swz) * 16;
+      bf16x8 af[MI], bfr[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+        af[i] = *(const bf16x8*)(As + (wm * (BM / 2) + i * 16 + frow) * 128 + coff);
 #pragma unroll
       for (int j = 0; j < NI; ++j)
+        bfr[j] = *(const bf16x8*)(Bs + (wn * (BN / 2) + j * 16 + frow) * 128 + coff);
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          Cs[(wm * (BM / 2) + i * 16 + erow + r) * CS + wn * (BN / 2) + j * 16 + ecol] = acc[i][j][r];
-  }
-  __syncthreads();
-  constexpr int TPR = BN / 8;    // threads per row
-  constexpr int RPP = 256 / TPR; // rows per pass
-  const int c8 = tid % TPR;
-  const int rr = tid / TPR;
-  const int co = n0 + c8 * 8;
-  const bool split = gridDim.z > 1;
-  if ((p.Cout & 7) == 0) {
-    if (co >= p.Cout) return;
-    float sc[8], bi[8];
-    if (!split) load_scale_bias8(p, co, sc, bi);
-#pragma unroll 2
-    for (int r0 = rr; r0 < BM; r0 += RPP) {
-      const int m = m0 + r0;
-      if (m >= p.M) break;
-      const float4 lo = *(const float4*)&Cs[r0 * CS + c8 * 8];
-      const float4 hi = *(const float4*)&Cs[r0 * CS + c8 * 8 + 4];
-      if (split) {
-        float* dst = p.partial + ((int64_t)blockIdx.z * p.M + m) * p.Cout + co;
-        *(float4*)dst = lo;
-        *(float4*)(dst + 4) = hi;
-      } else {
-        const float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-        epilogue_store8(p, m, co, v, sc, bi);
-      }
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-  } else {
-    for (int r0 = rr; r0 < BM; r0 += RPP) {
-      const int m = m0 + r0;
-      if (m >= p.M) break;
-      for (int e = 0; e < 8; ++e) {
-        if (co + e >= p.Cout) break;
-        const float a = Cs[r0 * CS + c8 * 8 + e];
-        if (split)
-          p.partial[((int64_t)blockIdx.z * p.M + m) * p.Cout + co + e] = a;
-        else
-          epilogue_store(p, m, co + e, a);
-      }
-    }
+  };
+
+  const int n = s_end - s_begin;
+  issue(s_begin, 0);
+  issue(s_begin + 1, 1);
+  int cbuf = 0;
+  for (int t = 0; t < n; ++t) {
+    vm_wait_barrier<NL>();  // stage t landed everywhere; stage t-1 reads retired everywhere
+    const int ibuf = cbuf == 0 ? 2 : cbuf - 1;  // (t + 2) % 3
+    issue(s_begin + t + 2, ibuf);
+    compute(cbuf);
+    cbuf = cbuf == 2 ? 0 : cbuf + 1;
   }
+  vm_wait_barrier<0>();  // drain the zero-page prefetches; all reads done before the C tile
+  conv_epilogue<BM, BN>(p, acc, smem, m0, n0);
 }
 
 // Split-K combine: y = epilogue(sum_z partial[z]) in fixed z order.
@@ -424,9 +656,28 @@ __global__ void __launch_bounds__(256) conv_splitk_epilogue(const ConvParams p, 
   }
 }
 
+bool use_glds() {
+  static const bool on = [] {
+    const char* e = getenv("MDA_CONV_GLDS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 template <int BM, int BN>
 int launch_tile(const ConvParams& p, int mode, int splits, hipStream_t st) {
   dim3 grid((p.M + BM - 1) / BM, (p.Cout + BN - 1) / BN, splits);
+  if (mode != LOAD_SCALAR && use_glds()) {
+    if (mode == LOAD_FAST)
+      hipLaunchKernelGGL((conv_glds_kernel<BM, BN, LOAD_FAST>), grid, dim3(256), 0, st, p);
+    else if (mode == LOAD_VEC8)
+      hipLaunchKernelGGL((conv_glds_kernel<BM, BN, LOAD_VEC8>), grid, dim3(256), 0, st, p);
+    else if (mode == LOAD_DGRAD_FAST)
+      hipLaunchKernelGGL((conv_glds_kernel<BM, BN, LOAD_DGRAD_FAST>), grid, dim3(256), 0, st, p);
+    else
+      hipLaunchKernelGGL((conv_glds_kernel<BM, BN, LOAD_DGRAD_VEC8>), grid, dim3(256), 0, st, p);
+    return (int)hipGetLastError();
+  }
   if (mode == LOAD_FAST)
     hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, LOAD_FAST>), grid, dim3(256), 0, st, p);
   else if (mode == LOAD_VEC8)

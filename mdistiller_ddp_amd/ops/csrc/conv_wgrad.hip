@@ -65,6 +65,13 @@ constexpr uint32_t OOB = 0x80000000u;
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* ptr, int bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(ptr), (short)0, bytes, 0x00020000);
 }
+// ok ? off : out-of-range, without a branch: the offset is always computed
+// and bit 31 forces it past the descriptor range (every range is < 2 GiB).
+// A select on a runtime condition made hipcc branch around each address
+// computation and load, which also broke its vmcnt bookkeeping.
+__device__ __forceinline__ uint32_t sel_off(bool ok, int off) {
+  return (uint32_t)off | ((uint32_t)(!ok) << 31);
+}
 __device__ __forceinline__ uint4 ld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
   return make_uint4(v[0], v[1], v[2], v[3]);
@@ -121,7 +128,7 @@ conv_wgrad_kernel(const WgParams p) {
     for (int j = 0; j < 2; ++j) {
       const int m = mb + row + 32 * j;
       const bool mok = m < m_end;
-      rd[j] = ld16(dr, (mok && cok) ? (uint32_t)((m * p.Cout + co) * 2) : OOB);
+      rd[j] = ld16(dr, sel_off(mok && cok, (m * p.Cout + co) * 2));
       const int n = fdiv(m, p.div_howo);
       const int rr = m - n * p.Ho * p.Wo;
       const int oh = fdiv(rr, p.div_wo);
@@ -129,7 +136,7 @@ conv_wgrad_kernel(const WgParams p) {
       if (MODE == WG_FAST || MODE == WG_VEC8) {
         const int ih = oh * p.stride - p.pad + kh, iw = ow * p.stride - p.pad + kw;
         const bool ok = kok && mok && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-        rx[j] = ld16(xr, ok ? (uint32_t)((((n * p.H + ih) * p.W + iw) * p.Cin + c) * 2) : OOB);
+        rx[j] = ld16(xr, sel_off(ok, (((n * p.H + ih) * p.W + iw) * p.Cin + c) * 2));
       } else {
         uint32_t v[4];
 #pragma unroll
@@ -144,7 +151,7 @@ conv_wgrad_kernel(const WgParams p) {
             const int ih = oh * p.stride - p.pad + kh2, iw = ow * p.stride - p.pad + kw2;
             const bool ok = kk < p.K && mok && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
             const uint32_t e = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(
-                xr, ok ? (int)((((n * p.H + ih) * p.W + iw) * p.Cin + ce) * 2) : (int)OOB, 0, 0);
+                xr, (int)sel_off(ok, (((n * p.H + ih) * p.W + iw) * p.Cin + ce) * 2), 0, 0);
             pair |= e << (16 * h);
           }
           v[e2] = pair;
@@ -187,20 +194,23 @@ conv_wgrad_kernel(const WgParams p) {
   // two register staging sets (stage s+2 in flight while s+1 is written to
   // LDS and s computed), loop unrolled by two to keep them static
   uint4 rd0[2], rx0[2], rd1[2], rx1[2];
+  // loads are unconditional: past m_end every row is OOB and reads zeros,
+  // so each iteration issues a fixed number of loads and the vmcnt waits
+  // stay exact (conditional prefetches made the compiler wait on them)
   const int n = (m_end - m_begin + TM - 1) / TM;
-  if (n > 0) load(m_begin, rd0, rx0);
-  if (n > 1) load(m_begin + TM, rd1, rx1);
-  if (n > 0) store(0, rd0, rx0);
+  load(m_begin, rd0, rx0);
+  load(m_begin + TM, rd1, rx1);
+  store(0, rd0, rx0);
   __syncthreads();
   for (int t = 0; t < n; t += 2) {
-    if (t + 2 < n) load(m_begin + (t + 2) * TM, rd0, rx0);
+    load(m_begin + (t + 2) * TM, rd0, rx0);
     compute(0);
-    if (t + 1 < n) store(1, rd1, rx1);
+    store(1, rd1, rx1);
     __syncthreads();
     if (t + 1 >= n) break;
-    if (t + 3 < n) load(m_begin + (t + 3) * TM, rd1, rx1);
+    load(m_begin + (t + 3) * TM, rd1, rx1);
     compute(1);
-    if (t + 2 < n) store(0, rd0, rx0);
+    store(0, rd0, rx0);
     __syncthreads();
   }
   const int ecol = lane & 15, erow = (lane >> 4) * 4;

@@ -18,6 +18,7 @@ SHAPES = [
     (64, 128, 16, 256, 3, 2, 1),
     (64, 256, 8, 256, 3, 1, 1),
     (64, 64, 32, 128, 1, 2, 0),   # 1x1 shortcut
+    (64, 64, 32, 128, 3, 1, 1),   # 128x128 tile
     (8, 16, 32, 16, 3, 1, 1),     # resnet20 (vec8 loader)
     (5, 24, 15, 40, 3, 2, 1),     # odd everything
     (3, 96, 7, 100, 1, 1, 0),

@@ -623,6 +623,191 @@ conv_glds_kernel(const ConvParams p) {
   conv_epilogue<BM, BN>(p, acc, smem, m0, n0);
 }
 
+// ---------------------------------------------------------------------------
+// Halo-tiled 3x3 / stride-1 / pad-1 convolution (the CIFAR ResNet body).
+// The implicit-GEMM kernels above gather im2col rows, so every input pixel
+// crosses L2 -> LDS nine times: ~113 MB of L2 traffic for one 64->64 32x32
+// conv at batch 64, which at ~70 GB/s per CU of L2-served gathers is the
+// kernel's whole runtime.  Here a block owns BM = 128 output pixels made of
+// whole output rows (R = 128 / W rows of one image, or 128 / (H*W) whole
+// images), stages the (rows + 2) x (W + 2) input patch of one 64-channel
+// chunk into LDS ONCE, and forms all nine taps from it: A traffic drops ~5x.
+// K loop = channel chunks (runtime) x 9 taps (unrolled).  Per step the
+// weight tile of (chunk, tap) arrives by LDS-DMA into a 3-deep ring; the next
+// chunk's patch (7 DMA pieces of 32 rows) is spread over taps 0..6, so every
+// step's DMA count -- and hence every counted vmcnt -- is a compile-time
+// constant.  FLIP mirrors the taps (dgrad: dx = conv(dy, w^T flipped)).
+constexpr int HALO_BM = 128;
+constexpr int HALO_PIECES = 7;                        // patch DMA pieces (32 rows each)
+constexpr int HALO_PROWS = HALO_PIECES * 32;          // 224 patch rows max
+
+template <int BN>
+struct HaloSmem {
+  static constexpr int PATCH = HALO_PROWS * 128;      // bytes per patch buffer
+  static constexpr int BT = BN * 128;                 // bytes per weight tile
+  static constexpr int PIPE = 2 * PATCH + 3 * BT;
+  static constexpr int CTILE = ConvSmem<HALO_BM, BN>::CTILE;
+  static constexpr int BYTES = PIPE > CTILE ? PIPE : CTILE;
+};
+
+template <int BN, bool FLIP>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BN >= 128 ? 1 : 2)))
+conv_halo_kernel(const ConvParams p) {
+  constexpr int BM = HALO_BM;
+  constexpr int MI = BM / 32, NI = BN / 32;
+  constexpr int BLOADS = (BN * 8 + 255) / 256;
+  constexpr int PATCH = HaloSmem<BN>::PATCH;
+  constexpr int BT = HaloSmem<BN>::BT;
+
+  __shared__ __attribute__((aligned(16))) char smem[HaloSmem<BN>::BYTES];
+  typedef __attribute__((address_space(3))) char lds_char;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_char*)smem;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int m0 = blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const uint32_t wave_off = (uint32_t)__builtin_amdgcn_readfirstlane(wid) * 1024u;
+  const bf16_t* const zero = (const bf16_t*)g_zero16;
+
+  // block geometry: R output rows per block; IMGS images of RH rows each
+  const int W = p.W, H = p.H;
+  const int R = BM / W;
+  const int IMGS = R > H ? R / H : 1;
+  const int RH = R > H ? H : R;
+  const int PW = W + 2;                       // patch row length (pixels)
+  const int PH = RH + 2;                      // patch rows per image
+  const int grow0 = m0 / W;                   // first global output row (n*H + oh)
+  const int img0 = grow0 / H;
+  const int oh0 = grow0 - img0 * H;
+
+  // patch DMA: piece j covers patch rows 32j..32j+31; this thread's row/chunk
+  const int trow = tid >> 3;
+  const int chunk = (tid & 7) ^ ((trow >> 1) & 7);  // (32j + trow) >> 1 & 7 == trow >> 1 & 7
+  int p_src[HALO_PIECES];                     // element offset of the patch pixel, or -1
+  {
+    const int P = IMGS * PH * PW;
+#pragma unroll
+    for (int j = 0; j < HALO_PIECES; ++j) {
+      const int pr = 32 * j + trow;
+      int off = -1;
+      if (pr < P) {
+        const int img = pr / (PH * PW);
+        const int rem = pr - img * PH * PW;
+        const int ir = rem / PW, ic = rem - (rem / PW) * PW;
+        const int n = img0 + img;
+        const int ih = oh0 + ir - 1, iw = ic - 1;
+        if (n < p.N && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
+          off = ((n * H + ih) * W + iw) * p.Cin;
+      }
+      p_src[j] = off;
+    }
+  }
+  // weight rows
+  const bf16_t* b_row[BLOADS];
+  bool b_ok[BLOADS];
+#pragma unroll
+  for (int j = 0; j < BLOADS; ++j) {
+    const int co = n0 + trow + 32 * j;
+    b_ok[j] = (trow + 32 * j < BN) && co < p.Cout;
+    b_row[j] = p.w + (int64_t)(b_ok[j] ? co : 0) * p.Kp + chunk * 8;
+  }
+
+  const int nchunks = p.Cin / BK;
+  const int c_begin = blockIdx.z * p.steps_per_split;
+  const int c_end = min(nchunks, c_begin + p.steps_per_split);
+  const int nsteps = (c_end - c_begin) * 9;
+
+  auto issue_b = [&](int step, int bbuf) {   // weight tile of step (chunk, tap)
+    const bool live = step < nsteps;
+    const int st = live ? step : 0;
+    const int cc = c_begin + st / 9, tap = st - (st / 9) * 9;
+    const int wtap = FLIP ? 8 - tap : tap;
+    const uint32_t base = lds0 + 2 * PATCH + (uint32_t)(bbuf * BT) + wave_off;
+#pragma unroll
+    for (int j = 0; j < BLOADS; ++j) {
+      const bf16_t* src = (live && b_ok[j]) ? b_row[j] + wtap * p.Cin + cc * BK : zero;
+      glds16(src, base + (uint32_t)(j * 32 * 128));
+    }
+  };
+  auto issue_piece = [&](int cc, int pbuf, int j) {  // patch piece j of chunk cc
+    const bool live = cc < c_end;
+    const int off = p_src[j];
+    const bf16_t* src = (live && off >= 0) ? p.x + off + cc * BK + chunk * 8 : zero;
+    glds16(src, lds0 + (uint32_t)(pbuf * PATCH) + wave_off + (uint32_t)(j * 32 * 128));
+  };
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // per A fragment: patch row of (pixel, tap 0,0)
+  const int frow = lane & 15;
+  const int g4 = lane >> 4;
+  int a_prow[MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int ml = wm * (BM / 2) + i * 16 + frow;   // local output pixel
+    const int lr = ml / W, c = ml - (ml / W) * W;   // local output row, column
+    const int img = lr / RH, r = lr - img * RH;
+    a_prow[i] = (img * PH + r) * PW + c;
+  }
+  const int bswz = (frow >> 1) & 7;
+
+  auto compute = [&](int pbuf, int bbuf, int tap) {
+    const char* Ps = smem + pbuf * PATCH;
+    const char* Bs = smem + 2 * PATCH + bbuf * BT;
+    const int kh = tap / 3, kw = tap - (tap / 3) * 3;
+    const int toff = kh * PW + kw;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int q = kk * 4 + g4;
+      bf16x8 af[MI], bfr[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int pr = a_prow[i] + toff;
+        af[i] = *(const bf16x8*)(Ps + pr * 128 + ((q ^ ((pr >> 1) & 7)) * 16));
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+        bfr[j] = *(const bf16x8*)(Bs + (wn * (BN / 2) + j * 16 + frow) * 128 + ((q ^ bswz) * 16));
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  // prologue: patch of the first chunk, weight tiles of steps 0 and 1
+#pragma unroll
+  for (int j = 0; j < HALO_PIECES; ++j) issue_piece(c_begin, 0, j);
+  issue_b(0, 0);
+  issue_b(1, 1);
+  int pbuf = 0, bbuf = 0, step = 0;
+  for (int cc = c_begin; cc < c_end; ++cc) {
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      // DMAs issued after B(step): [piece(tap-2) if 0<=tap-2<7] B(step+1) [piece(tap-1) if 0<=tap-1<7]
+      if (tap == 0) vm_wait_barrier<BLOADS>();
+      else if (tap == 1) vm_wait_barrier<BLOADS + 1>();
+      else if (tap <= 7) vm_wait_barrier<BLOADS + 2>();
+      else vm_wait_barrier<BLOADS + 1>();
+      const int nb = bbuf == 0 ? 2 : bbuf - 1;   // (step + 2) % 3
+      issue_b(step + 2, nb);
+      if (tap < HALO_PIECES) issue_piece(cc + 1, pbuf ^ 1, tap);
+      compute(pbuf, bbuf, tap);
+      bbuf = bbuf == 2 ? 0 : bbuf + 1;
+      ++step;
+    }
+    pbuf ^= 1;
+  }
+  vm_wait_barrier<0>();
+  conv_epilogue<BM, BN>(p, acc, smem, m0, n0);
+}
+
 // Split-K combine: y = epilogue(sum_z partial[z]) in fixed z order.
 // Cout % 8 == 0: one thread per 8 channels (16-byte traffic).
 __global__ void __launch_bounds__(256) conv_splitk_epilogue(const ConvParams p, int splits) {
@@ -654,6 +839,23 @@ __global__ void __launch_bounds__(256) conv_splitk_epilogue(const ConvParams p, 
     const int co = (int)(i - (int64_t)m * p.Cout);
     epilogue_store(p, m, co, a);
   }
+}
+
+// 3x3 / stride 1 / pad 1 "same" conv whose rows tile BM = 128 exactly and
+// whose input patch fits HALO_PROWS rows (CIFAR 32x32, 16x16, 8x8 maps).
+bool halo_eligible(const ConvParams& p) {
+  static const bool on = [] {
+    const char* e = getenv("MDA_CONV_HALO");
+    return !(e && e[0] == '0');
+  }();
+  if (!on) return false;
+  if (p.KH != 3 || p.KW != 3 || p.stride != 1 || p.pad != 1) return false;
+  if (p.Ho != p.H || p.Wo != p.W || p.Cin % BK || p.Kp != 9 * p.Cin) return false;
+  if (p.W > HALO_BM || HALO_BM % p.W) return false;
+  const int R = HALO_BM / p.W;
+  if (R <= p.H ? (p.H % R) : (R % p.H)) return false;
+  const int imgs = R > p.H ? R / p.H : 1, rh = R > p.H ? p.H : R;
+  return imgs * (rh + 2) * (p.W + 2) <= HALO_PROWS;
 }
 
 bool use_glds() {
@@ -713,7 +915,7 @@ MDA_API int mda_conv_plan(int64_t M, int64_t Cout, int64_t Kp, int64_t* tile, in
 
 namespace {
 
-int dispatch(ConvParams& p, int mode, int64_t tile, int64_t splits, hipStream_t st) {
+int dispatch(ConvParams& p, int mode, int64_t tile, int64_t splits, hipStream_t st, int halo = 0) {
   if (p.Kp % BK || p.Kp < p.K) return (int)hipErrorInvalidValue;
   const int64_t xb = (int64_t)p.N * p.H * p.W * p.Cin * 2, wb = (int64_t)p.Cout * p.Kp * 2;
   if (xb >= ((int64_t)1 << 31) || wb >= ((int64_t)1 << 31) || (int64_t)p.M * p.Cout >= ((int64_t)1 << 31))
@@ -722,9 +924,23 @@ int dispatch(ConvParams& p, int mode, int64_t tile, int64_t splits, hipStream_t 
   p.w_bytes = (int)wb;
   if (tile == 0 || splits == 0) mda_conv_plan(p.M, p.Cout, p.Kp, &tile, &splits);
   if (splits > 1 && p.partial == nullptr) return (int)hipErrorInvalidValue;
+  int rc;
+  if (halo) {  // halo kernel: split over 64-channel chunks, BM = 128
+    const int nchunks = p.Cin / BK;
+    p.steps_per_split = (int)((nchunks + splits - 1) / splits);
+    const int bn = p.Cout <= 32 ? 32 : 64;
+    dim3 grid((p.M + HALO_BM - 1) / HALO_BM, (p.Cout + bn - 1) / bn, (int)splits);
+    if (bn == 32) {
+      if (halo == 2) hipLaunchKernelGGL((conv_halo_kernel<32, true>), grid, dim3(256), 0, st, p);
+      else hipLaunchKernelGGL((conv_halo_kernel<32, false>), grid, dim3(256), 0, st, p);
+    } else {
+      if (halo == 2) hipLaunchKernelGGL((conv_halo_kernel<64, true>), grid, dim3(256), 0, st, p);
+      else hipLaunchKernelGGL((conv_halo_kernel<64, false>), grid, dim3(256), 0, st, p);
+    }
+    rc = (int)hipGetLastError();
+  } else {
   const int steps = p.Kp / BK;
   p.steps_per_split = (int)((steps + splits - 1) / splits);
-  int rc;
   switch (tile) {
     case 128128: rc = launch_tile<128, 128>(p, mode, splits, st); break;
     case 128064: rc = launch_tile<128, 64>(p, mode, splits, st); break;
@@ -733,6 +949,7 @@ int dispatch(ConvParams& p, int mode, int64_t tile, int64_t splits, hipStream_t 
     case 64064: rc = launch_tile<64, 64>(p, mode, splits, st); break;
     case 64032: rc = launch_tile<64, 32>(p, mode, splits, st); break;
     default: return (int)hipErrorInvalidValue;
+  }
   }
   if (rc || splits <= 1) return rc;
   int64_t total = (int64_t)p.M * p.Cout;
@@ -758,7 +975,7 @@ MDA_API int mda_conv_fwd(const void* x, const void* w, const float* scale, const
   p.KW = KW; p.stride = stride; p.pad = pad; p.K = KH * KW * Cin; p.Kp = Kp; p.M = N * Ho * Wo;
   p.act = act;
   int mode = (Cin % BK == 0) ? LOAD_FAST : (Cin % 8 == 0 ? LOAD_VEC8 : LOAD_SCALAR);
-  return dispatch(p, mode, tile, splits, st);
+  return dispatch(p, mode, tile, splits, st, halo_eligible(p) ? 1 : 0);
 }
 
 // Input gradient of a convolution (any stride): dx[N, H, W, Cin] =
@@ -778,5 +995,6 @@ MDA_API int mda_conv_dgrad(const void* dy, const void* wt, void* dx, float* part
   p.KW = KW; p.stride = stride; p.pad = pad; p.K = KH * KW * Cout; p.Kp = Kp; p.M = N * H * W;
   p.act = 0;
   int mode = (Cout % BK == 0) ? LOAD_DGRAD_FAST : LOAD_DGRAD_VEC8;
-  return dispatch(p, mode, tile, splits, st);
+  // stride-1 3x3 pad-1 dgrad is a "same" conv of dy with the mirrored taps
+  return dispatch(p, mode, tile, splits, st, halo_eligible(p) ? 2 : 0);
 }

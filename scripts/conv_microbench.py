@@ -49,24 +49,29 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--shape", type=int, default=-1, help="index into SHAPES (-1 = all)")
+    ap.add_argument("--ops", default="fwd,mio,wgrad,dgrad")
     args = ap.parse_args()
+    ops = set(args.ops.split(","))
     from mdistiller_ddp_amd.ops import hip_layers, hip_train
     torch.backends.cudnn.benchmark = True
     rows = []
-    for (N, Cin, H, Cout, k, s, p) in SHAPES:
+    shapes = SHAPES if args.shape < 0 else [SHAPES[args.shape]]
+    nan = float("nan")
+    for (N, Cin, H, Cout, k, s, p) in shapes:
         conv = nn.Conv2d(Cin, Cout, k, s, p, bias=False).cuda()
         bn = nn.BatchNorm2d(Cout).cuda().eval()
         x = torch.randn(N, Cin, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         Ho = (H + 2 * p - k) // s + 1
         flop = 2.0 * N * Ho * Ho * Cout * Cin * k * k
         with torch.no_grad():
-            t_fwd = timeit(lambda: hip_layers.conv_bn_act(x, conv, bn, "relu", None, False), args.iters)
+            t_fwd = timeit(lambda: hip_layers.conv_bn_act(x, conv, bn, "relu", None, False), args.iters) if "fwd" in ops else nan
             wb = conv.weight.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-            t_mio = timeit(lambda: F.conv2d(x, wb, stride=s, padding=p), args.iters)
+            t_mio = timeit(lambda: F.conv2d(x, wb, stride=s, padding=p), args.iters) if "mio" in ops else nan
             dy = torch.randn(N, Cout, Ho, Ho, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-            t_wg = timeit(lambda: hip_train.conv_wgrad(x, dy, tuple(conv.weight.shape), s, p), args.iters)
-            t_dg = float("nan")
-            if Cin % 8 == 0:
+            t_wg = timeit(lambda: hip_train.conv_wgrad(x, dy, tuple(conv.weight.shape), s, p), args.iters) if "wgrad" in ops else nan
+            t_dg = nan
+            if Cin % 8 == 0 and "dgrad" in ops:
                 t_dg = timeit(lambda: hip_train.conv_dgrad(dy, conv.weight, tuple(x.shape), s, p), args.iters)
         row = dict(shape=[N, Cin, H, Cout, k, s, p], gflop=flop / 1e9, fwd_us=t_fwd,
                    fwd_tflops=flop / t_fwd / 1e6, miopen_fwd_us=t_mio, dgrad_us=t_dg,

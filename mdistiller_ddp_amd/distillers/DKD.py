@@ -9,7 +9,7 @@ fragile in bf16), computing everything in fp32.
 """
 from __future__ import annotations
 
-from ._base import Distiller, warmup_factor
+from ._base import Distiller
 from ..ops import losses as L
 
 
@@ -28,6 +28,6 @@ class DKD(Distiller):
         logits_student, _ = self.student(image)
         logits_teacher, _ = t_out.get()
         loss_ce, loss_dkd = L.ce_dkd(logits_student, logits_teacher, target, self.ce_loss_weight,
-                                     self.alpha, self.beta, self.temperature)
-        loss_dkd = warmup_factor(kwargs["epoch"], self.warmup) * loss_dkd
+                                     self.alpha, self.beta, self.temperature,
+                                     epoch=kwargs.get("epoch"), warmup=self.warmup)
         return logits_student, {"loss_ce": loss_ce, "loss_kd": loss_dkd}

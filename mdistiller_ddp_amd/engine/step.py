@@ -51,6 +51,17 @@ class DeviceMeters:
         self.buf = torch.zeros(len(self.loss_keys) + 5, dtype=torch.float64, device=device)
 
     def update(self, preds, target, losses: dict):
+        if self._native(preds, losses):
+            from ..ops import _ext
+            ls = [losses[k].detach().reshape(()) for k in self.loss_keys]
+            ls = [v if v.dtype == torch.float32 else v.float() for v in ls]
+            ptrs = ls + [None] * (4 - len(ls))
+            p = preds.detach()
+            if p.dtype not in (torch.float32, torch.bfloat16):
+                p = p.float()
+            _ext.call("mda_meters_update", 0 if p.dtype == torch.float32 else 1, p.contiguous(),
+                      target.contiguous(), p.shape[0], p.shape[1], *ptrs, len(ls), self.buf)
+            return
         b = self.buf
         total = None
         for i, k in enumerate(self.loss_keys):
@@ -64,6 +75,11 @@ class DeviceMeters:
         b[n + 2] += (rank < 5).sum().double()
         b[n + 3] += float(target.shape[0])
         b[n + 4] += 1.0
+
+    def _native(self, preds, losses) -> bool:
+        from ..ops.backend import hip_enabled_for
+        return (len(self.loss_keys) <= 4 and preds.dim() == 2 and hip_enabled_for(preds)
+                and all(losses[k].numel() == 1 for k in self.loss_keys))
 
     def reset(self):
         self.buf.zero_()
@@ -146,6 +162,7 @@ class TrainStep:
         self._graphs = None
         self._static = None
         self._dot_ready = not self.is_dot
+        self._units = {}
 
     # ------------------------------------------------------------------
     def set_epoch(self, epoch: float) -> None:
@@ -176,6 +193,13 @@ class TrainStep:
             self.meters = DeviceMeters(self.device, sorted(losses.keys()))
         return preds, losses
 
+    def _unit(self, v):
+        key = (v.dtype, v.device, tuple(v.shape))
+        u = self._units.get(key)
+        if u is None:
+            u = self._units[key] = torch.ones_like(v)
+        return u
+
     def _dot_reachability(self, losses):
         """Which params receive task / KD gradients (DOT's momentum branches)."""
         ps = self.flat.params
@@ -195,10 +219,13 @@ class TrainStep:
             self.flat.bind_grads(0)
             losses["loss_ce"].backward()
         else:
-            loss = sum(losses.values())
             if overlap_comm:
                 self.reducer.arm()
-            loss.backward()
+            # backward of the loss terms with unit seeds straight into each term
+            # (no sum node, no per-step fill kernels)
+            terms = [v for v in losses.values() if v.requires_grad]
+            if terms:
+                torch.autograd.backward(terms, [self._unit(v) for v in terms])
         post = getattr(self.distiller, "post_backward", None)
         if post is not None:
             post()

@@ -12,7 +12,7 @@ from __future__ import annotations
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ...ops.nn import conv_bn_act
+from ...ops.nn import conv_bn_act, pool_linear
 from .._base import ModelBase, PreactStage
 
 
@@ -152,8 +152,7 @@ class ResNet(nn.Module, ModelBase):
         f2 = x
         x, f3_pre = self.layer3(x)
         f3 = x
-        avg = F.avg_pool2d(x, 8).reshape(x.size(0), -1)
-        out = self.fc(avg)
+        avg, out = pool_linear(x, self.fc, 8)
         return out, {
             "feats": [f0, f1, f2, f3],
             "preact_feats": [f0_pre, f1_pre, f2_pre, f3_pre],

@@ -12,7 +12,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ...ops.nn import conv_bn_act, channel_shuffle
+from ...ops.nn import conv_bn_act, channel_shuffle, pool_linear
 from .._base import ModelBase, PreactStage
 from .resnet import Stage
 
@@ -105,8 +105,8 @@ class ShuffleNet(nn.Module, ModelBase):
         f2 = out
         out, f3_pre = self.layer3(out)
         f3 = out
-        avg = F.adaptive_avg_pool2d(out, 1).reshape(out.size(0), -1)
-        return self.linear(avg), {"feats": [f0, f1, f2, f3],
+        avg, logits = pool_linear(out, self.linear)
+        return logits, {"feats": [f0, f1, f2, f3],
                                   "preact_feats": [f0_pre, f1_pre, f2_pre, f3_pre],
                                   "pooled_feat": avg}
 

@@ -11,7 +11,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ...ops.nn import bn_act, conv_bn_act
+from ...ops.nn import bn_act, conv_bn_act, pool_linear
 from .._base import ModelBase
 
 
@@ -98,8 +98,7 @@ class WideResNet(nn.Module, ModelBase):
         f2 = self.block2(F.relu(f1))
         f3 = self.block3(F.relu(f2))
         out, _ = bn_act(f3, self.bn1, "relu")
-        avg = F.avg_pool2d(out, 8).reshape(-1, self.nChannels)
-        logits = self.fc(avg)
+        avg, logits = pool_linear(out, self.fc, 8)
         return logits, {
             "feats": [f0, F.relu(f1), F.relu(f2), F.relu(f3)],
             "preact_feats": [f0_pre, f1, f2, f3],

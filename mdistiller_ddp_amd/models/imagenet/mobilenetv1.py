@@ -10,6 +10,8 @@ from __future__ import annotations
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ...ops.nn import pool_linear
+
 from .._base import ModelBase
 from .._seq import run_seq
 
@@ -76,8 +78,8 @@ class MobileNetV1(nn.Module, ModelBase):
             pres.append(h)
             h = F.relu(h)
             feats.append(h)
-        avg = F.adaptive_avg_pool2d(h, 1).reshape(h.size(0), -1)
-        return self.fc(avg), {"pooled_feat": avg, "feats": feats, "preact_feats": pres}
+        avg, logits = pool_linear(h, self.fc)
+        return logits, {"pooled_feat": avg, "feats": feats, "preact_feats": pres}
 
     def get_bn_before_relu(self):
         return [self.model[2][4], self.model[4][4], self.model[10][4], self.model[13][4]]

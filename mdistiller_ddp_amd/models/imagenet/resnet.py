@@ -16,7 +16,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ...ops.nn import conv_bn_act
+from ...ops.nn import conv_bn_act, pool_linear
 from .._base import ModelBase, PreactStage
 from ..cifar.resnet import Stage
 
@@ -147,8 +147,7 @@ class ResNet(nn.Module, ModelBase):
         f3 = x
         x, p4 = self.layer4(x)
         f4 = x
-        avg = F.adaptive_avg_pool2d(x, 1).view(x.size(0), -1)
-        out = self.fc(avg)
+        avg, out = pool_linear(x, self.fc)
         return out, {"pooled_feat": avg, "feats": [f0, f1, f2, f3, f4],
                      "preact_feats": [f0_pre, p1, p2, p3, p4]}
 

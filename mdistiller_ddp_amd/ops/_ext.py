@@ -29,7 +29,7 @@ _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int64, "f": ctypes.c_float, "s": ctyp
 # name -> argument codes (stream last).  Kept in sync with csrc/*.hip `extern "C"` launchers.
 SIGNATURES = {
     # losses (csrc/losses.hip)
-    "mda_logit_loss": "iiippppppppiifffffs",
+    "mda_logit_loss": "iiippppppppiifffffpfs",
     "mda_axpby": "ipppppis",
     # feature losses (csrc/feat.hip)
     "mda_at_loss": "iipppppp" + "iiii" + "fs",
@@ -49,6 +49,10 @@ SIGNATURES = {
     "mda_crd_scores": "ppppiiifs",
     "mda_crd_grad": "ppppppiiifs",
     "mda_crd_update": "pppiifs",
+    # classifier head + metrics (csrc/head.hip)
+    "mda_pool_fc_fwd": "ipppppiiiis",
+    "mda_pool_fc_bwd": "ippppppp" + "iiiii" + "s",
+    "mda_meters_update": "ippii" + "pppp" + "ips",
     # data augmentation (csrc/aug.hip)
     "mda_crop_flip_norm": "ppppppp" + "iiiiii" + "s",
     # optimizers (csrc/optim.hip)

@@ -10,7 +10,8 @@
 //
 // Outputs
 //   losses[0] = ce_w * mean_b CE(s_b, y_b)
-//   losses[1] = kd_w * (KD | DKD) as defined by the reference
+//   losses[1] = kd_w * w(epoch) * (KD | DKD) as defined by the reference,
+//               w = min(epoch / warmup, 1) when an epoch pointer is given (else 1)
 //   g_ce[b,c] = d losses[0] / d s[b,c]     (same dtype as s)
 //   g_kd[b,c] = d losses[1] / d s[b,c]
 // The autograd backward combines them as go_ce*g_ce + go_kd*g_kd
@@ -31,7 +32,10 @@ logit_loss_kernel(const TS* __restrict__ s, const TT* __restrict__ t,
                   TG* __restrict__ g_kd, float* __restrict__ partial,
                   unsigned* __restrict__ counter, float* __restrict__ losses,
                   int B, int C, float inv_T, float ce_w, float kd_w, float alpha,
-                  float beta) {
+                  float beta, const float* __restrict__ epoch, float warmup) {
+  // DKD/ReviewKD-style linear warm-up of the KD term, min(epoch / warmup, 1),
+  // read from device memory so a replayed hipGraph sees the current epoch
+  if (epoch != nullptr && warmup > 0.f) kd_w *= fminf(*epoch / warmup, 1.f);
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int row = blockIdx.x * ROWS_PER_BLOCK + wid;
@@ -194,23 +198,23 @@ logit_loss_kernel(const TS* __restrict__ s, const TT* __restrict__ t,
 template <typename TS, typename TT, int MODE, int NPL>
 int launch_t(const void* s, const void* t, const int64_t* y, void* gce, void* gkd, float* part,
              unsigned* cnt, float* losses, int B, int C, float invT, float cew, float kdw, float a,
-             float b, hipStream_t st) {
+             float b, const float* ep, float wu, hipStream_t st) {
   dim3 grid((B + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK);
   hipLaunchKernelGGL((logit_loss_kernel<TS, TT, TS, NPL, MODE>), grid, dim3(256), 0, st,
                      (const TS*)s, (const TT*)t, y, (TS*)gce, (TS*)gkd, part, cnt, losses, B, C,
-                     invT, cew, kdw, a, b);
+                     invT, cew, kdw, a, b, ep, wu);
   MDA_CHECK_LAUNCH();
 }
 
 template <typename TS, typename TT, int MODE>
 int launch_npl(const void* s, const void* t, const int64_t* y, void* gce, void* gkd, float* part,
                unsigned* cnt, float* losses, int B, int C, float invT, float cew, float kdw,
-               float a, float b, hipStream_t st) {
+               float a, float b, const float* ep, float wu, hipStream_t st) {
   int npl = (C + 63) / 64;
 #define NPL_CASE(N)                                                                          \
   if (npl <= N)                                                                              \
     return launch_t<TS, TT, MODE, N>(s, t, y, gce, gkd, part, cnt, losses, B, C, invT, cew, \
-                                     kdw, a, b, st);
+                                     kdw, a, b, ep, wu, st);
   NPL_CASE(2) NPL_CASE(4) NPL_CASE(8) NPL_CASE(16) NPL_CASE(32)
 #undef NPL_CASE
   return (int)hipErrorInvalidValue;
@@ -219,14 +223,14 @@ int launch_npl(const void* s, const void* t, const int64_t* y, void* gce, void* 
 template <int MODE>
 int launch_mode(int dts, int dtt, const void* s, const void* t, const int64_t* y, void* gce,
                 void* gkd, float* part, unsigned* cnt, float* losses, int B, int C, float invT,
-                float cew, float kdw, float a, float b, hipStream_t st) {
+                float cew, float kdw, float a, float b, const float* ep, float wu, hipStream_t st) {
   if (dts == DT_F32 && dtt == DT_F32)
-    return launch_npl<float, float, MODE>(s, t, y, gce, gkd, part, cnt, losses, B, C, invT, cew, kdw, a, b, st);
+    return launch_npl<float, float, MODE>(s, t, y, gce, gkd, part, cnt, losses, B, C, invT, cew, kdw, a, b, ep, wu, st);
   if (dts == DT_BF16 && dtt == DT_BF16)
-    return launch_npl<bf16_t, bf16_t, MODE>(s, t, y, gce, gkd, part, cnt, losses, B, C, invT, cew, kdw, a, b, st);
+    return launch_npl<bf16_t, bf16_t, MODE>(s, t, y, gce, gkd, part, cnt, losses, B, C, invT, cew, kdw, a, b, ep, wu, st);
   if (dts == DT_BF16 && dtt == DT_F32)
-    return launch_npl<bf16_t, float, MODE>(s, t, y, gce, gkd, part, cnt, losses, B, C, invT, cew, kdw, a, b, st);
-  return launch_npl<float, bf16_t, MODE>(s, t, y, gce, gkd, part, cnt, losses, B, C, invT, cew, kdw, a, b, st);
+    return launch_npl<bf16_t, float, MODE>(s, t, y, gce, gkd, part, cnt, losses, B, C, invT, cew, kdw, a, b, ep, wu, st);
+  return launch_npl<float, bf16_t, MODE>(s, t, y, gce, gkd, part, cnt, losses, B, C, invT, cew, kdw, a, b, ep, wu, st);
 }
 
 // out = (*a) * x + (*b) * y ; a/b are device scalars (graph-replay safe).
@@ -250,13 +254,14 @@ __global__ void axpby_kernel(const float* __restrict__ a, const T* __restrict__ 
 MDA_API int mda_logit_loss(int64_t mode, int64_t dts, int64_t dtt, const void* s, const void* t,
                            const int64_t* y, void* g_ce, void* g_kd, float* partial,
                            unsigned* counter, float* losses, int64_t B, int64_t C, float inv_T,
-                           float ce_w, float kd_w, float alpha, float beta, hipStream_t st) {
+                           float ce_w, float kd_w, float alpha, float beta, const float* epoch,
+                           float warmup, hipStream_t st) {
   if (C > 64 * MAXNPL || B <= 0) return (int)hipErrorInvalidValue;
   if (mode == MODE_CE)
-    return launch_mode<MODE_CE>(dts, dtt, s, t, y, g_ce, g_kd, partial, counter, losses, B, C, inv_T, ce_w, kd_w, alpha, beta, st);
+    return launch_mode<MODE_CE>(dts, dtt, s, t, y, g_ce, g_kd, partial, counter, losses, B, C, inv_T, ce_w, kd_w, alpha, beta, epoch, warmup, st);
   if (mode == MODE_KD)
-    return launch_mode<MODE_KD>(dts, dtt, s, t, y, g_ce, g_kd, partial, counter, losses, B, C, inv_T, ce_w, kd_w, alpha, beta, st);
-  return launch_mode<MODE_DKD>(dts, dtt, s, t, y, g_ce, g_kd, partial, counter, losses, B, C, inv_T, ce_w, kd_w, alpha, beta, st);
+    return launch_mode<MODE_KD>(dts, dtt, s, t, y, g_ce, g_kd, partial, counter, losses, B, C, inv_T, ce_w, kd_w, alpha, beta, epoch, warmup, st);
+  return launch_mode<MODE_DKD>(dts, dtt, s, t, y, g_ce, g_kd, partial, counter, losses, B, C, inv_T, ce_w, kd_w, alpha, beta, epoch, warmup, st);
 }
 
 MDA_API int mda_axpby(int64_t dt, const float* a, const void* x, const float* b, const void* y,

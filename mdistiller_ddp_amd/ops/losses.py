@@ -85,7 +85,7 @@ def _supported(s, t, C):
 
 class _LogitLoss(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, s, t, target, mode, inv_T, ce_w, kd_w, alpha, beta):
+    def forward(ctx, s, t, target, mode, inv_T, ce_w, kd_w, alpha, beta, epoch=None, warmup=0.0):
         s = s.contiguous()
         t = s if t is None else t.contiguous()
         target = target.contiguous().to(torch.int64)
@@ -95,7 +95,8 @@ class _LogitLoss(torch.autograd.Function):
         losses = torch.empty(2, dtype=torch.float32, device=s.device)
         ws = workspace(s.device)
         _ext.call("mda_logit_loss", mode, _DT[s.dtype], _DT[t.dtype], s, t, target, g_ce, g_kd,
-                  ws.partial, ws.counter, losses, B, C, inv_T, ce_w, kd_w, alpha, beta)
+                  ws.partial, ws.counter, losses, B, C, inv_T, ce_w, kd_w, alpha, beta,
+                  _epoch_ptr(epoch, warmup), float(warmup or 0.0))
         ctx.save_for_backward(g_ce, g_kd)
         ctx.mode = mode
         return losses[0], losses[1]
@@ -107,7 +108,16 @@ class _LogitLoss(torch.autograd.Function):
         a = None if go_ce is None else go_ce.float().reshape(1).contiguous()
         b = None if (go_kd is None or ctx.mode == 0) else go_kd.float().reshape(1).contiguous()
         _ext.call("mda_axpby", _DT[out.dtype], a, g_ce, b, g_kd, out, out.numel())
-        return out, None, None, None, None, None, None, None, None
+        return out, None, None, None, None, None, None, None, None, None, None
+
+
+def _epoch_ptr(epoch, warmup):
+    """Device fp32 epoch scalar for the in-kernel warm-up factor, or None."""
+    if epoch is None or not warmup or warmup <= 0:
+        return None
+    if not isinstance(epoch, torch.Tensor) or epoch.dtype != torch.float32 or not epoch.is_cuda:
+        raise TypeError("warm-up epoch must be a float32 device tensor on the HIP path")
+    return epoch
 
 
 def ce_kd(logits_s, logits_t, target, temperature, ce_weight, kd_weight):
@@ -120,14 +130,32 @@ def ce_kd(logits_s, logits_t, target, temperature, ce_weight, kd_weight):
             kd_weight * kd_loss_ref(logits_s, logits_t.detach(), temperature))
 
 
-def ce_dkd(logits_s, logits_t, target, ce_weight, alpha, beta, temperature):
-    """``(ce_weight * CE(s, y), DKD(s, t))`` (the warm-up factor is applied by the caller)."""
+def _warmup(epoch, warmup):
+    if epoch is None or not warmup or warmup <= 0:
+        return 1.0
+    if isinstance(epoch, torch.Tensor):
+        return torch.clamp(epoch.float() / float(warmup), max=1.0)
+    return min(float(epoch) / float(warmup), 1.0)
+
+
+def ce_dkd(logits_s, logits_t, target, ce_weight, alpha, beta, temperature, epoch=None, warmup=0):
+    """``(ce_weight * CE(s, y), min(epoch / warmup, 1) * DKD(s, t))``.
+
+    The warm-up factor (``DKD.WARMUP``, reference ``DKD.py:78``) is applied
+    inside the fused kernel from the device epoch tensor when one is given.
+    """
     C = logits_s.shape[1]
-    if hip_enabled_for(logits_s) and _supported(logits_s, logits_t, C):
+    if (hip_enabled_for(logits_s) and _supported(logits_s, logits_t, C)
+            and (epoch is None or isinstance(epoch, torch.Tensor) or not warmup)):
+        ep = epoch if isinstance(epoch, torch.Tensor) else None
+        if ep is not None and (ep.dtype != torch.float32 or ep.device != logits_s.device):
+            ep = ep.to(device=logits_s.device, dtype=torch.float32)
         return _LogitLoss.apply(logits_s, logits_t.detach(), target, 2, 1.0 / float(temperature),
-                                float(ce_weight), 1.0, float(alpha), float(beta))
+                                float(ce_weight), 1.0, float(alpha), float(beta), ep,
+                                float(warmup or 0.0) if ep is not None else 0.0)
     return (ce_weight * cross_entropy(logits_s, target),
-            dkd_loss_ref(logits_s, logits_t.detach(), target, alpha, beta, temperature))
+            _warmup(epoch, warmup) * dkd_loss_ref(logits_s, logits_t.detach(), target, alpha, beta,
+                                                  temperature))
 
 
 def ce(logits_s, target, ce_weight=1.0):

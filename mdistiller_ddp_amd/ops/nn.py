@@ -88,6 +88,77 @@ def linear(x: torch.Tensor, fc: nn.Linear) -> torch.Tensor:
     return fc(x)
 
 
+class _PoolFC(torch.autograd.Function):
+    """Global average pool + Linear on the fused HIP head kernels (csrc/head.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        from . import _ext
+        N, C, H, W = x.shape
+        J = weight.shape[0]
+        dt = 0 if x.dtype == torch.float32 else 1
+        xc = x.contiguous(memory_format=torch.channels_last)
+        pooled = torch.empty(N, C, dtype=x.dtype, device=x.device)
+        logits = torch.empty(N, J, dtype=x.dtype, device=x.device)
+        w = weight.detach()
+        b = bias.detach() if bias is not None else None
+        _ext.call("mda_pool_fc_fwd", dt, xc, w, b, pooled, logits, N, H * W, C, J)
+        ctx.save_for_backward(pooled, weight, bias)
+        ctx.meta = (N, C, H, W, J, dt, bias is not None)
+        return pooled, logits
+
+    @staticmethod
+    def backward(ctx, dpooled, dlogits):
+        from . import _ext
+        pooled, weight, bias = ctx.saved_tensors
+        N, C, H, W, J, dt, has_b = ctx.meta
+        dev = pooled.device
+        dtype = pooled.dtype
+        if dlogits is None:
+            dlogits = torch.zeros(N, J, dtype=dtype, device=dev)
+        dlogits = dlogits.to(dtype).contiguous()
+        dpooled = dpooled.to(dtype).contiguous() if dpooled is not None else None
+        need_w = ctx.needs_input_grad[1]
+        need_b = has_b and ctx.needs_input_grad[2]
+        # accumulate straight into the flat fp32 gradient views when bound
+        direct_w = need_w and weight.grad is not None and weight.grad.is_contiguous()
+        direct_b = need_b and bias.grad is not None
+        dw = weight.grad if direct_w else (torch.zeros_like(weight) if need_w else None)
+        db = bias.grad if direct_b else (torch.zeros_like(bias) if need_b else None)
+        dx = torch.empty((N, C, H, W), dtype=dtype, device=dev, memory_format=torch.channels_last)
+        _ext.call("mda_pool_fc_bwd", dt, dlogits, dpooled, pooled, weight.detach(), dw, db, dx, N,
+                  H * W, C, J, 1)
+        return (dx, None if direct_w else dw, None if direct_b else db)
+
+
+def _pool_fc_native(x: torch.Tensor, fc: nn.Linear, kernel) -> bool:
+    if not (x.dim() == 4 and hip_enabled_for(x)):
+        return False
+    N, C, H, W = x.shape
+    if kernel not in (None, H) or H != W or fc.in_features != C or fc.weight.dtype != torch.float32:
+        return False
+    if C > 8192 or fc.out_features * C > (1 << 20) or N > 16384:
+        return False
+    if x.dtype == torch.bfloat16:
+        return True
+    return x.dtype == torch.float32 and not torch.is_autocast_enabled("cuda")
+
+
+def pool_linear(x: torch.Tensor, fc: nn.Linear, kernel: int | None = None):
+    """``avg = avg_pool2d(x, kernel).flatten(1); (avg, fc(avg))`` -- the CNN head.
+
+    With a global pool (``kernel`` == spatial size, or None) on the GPU this is
+    one fused HIP launch forward and one backward (:class:`_PoolFC`).
+    """
+    if _pool_fc_native(x, fc, kernel):
+        return _PoolFC.apply(x, fc.weight, fc.bias)
+    if kernel is None:
+        avg = F.adaptive_avg_pool2d(x, 1).reshape(x.size(0), -1)
+    else:
+        avg = F.avg_pool2d(x, kernel).reshape(x.size(0), -1)
+    return avg, fc(avg)
+
+
 def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
     """(N, C, H, W) -> (N, C), fp32-accumulated."""
     return x.float().mean(dim=(2, 3)).to(x.dtype)

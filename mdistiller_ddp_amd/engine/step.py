@@ -163,6 +163,7 @@ class TrainStep:
         self._static = None
         self._dot_ready = not self.is_dot
         self._units = {}
+        self._packs = None
 
     # ------------------------------------------------------------------
     def set_epoch(self, epoch: float) -> None:
@@ -210,7 +211,22 @@ class TrainStep:
 
     def _fwd_bwd(self, b: dict, overlap_comm: bool):
         self.flat.zero_grad()
-        preds, losses = self._forward(b)
+        packs = None
+        if self.device.type == "cuda":
+            from ..ops.backend import hip_enabled_for
+            if hip_enabled_for(self.flat.data):
+                from ..ops import hip_train
+                packs = self._packs
+                if packs is None:
+                    packs = self._packs = hip_train.PackCache()
+                packs.pack_all(self.device)
+                hip_train.set_active_packs(packs)
+        try:
+            preds, losses = self._forward(b)
+        finally:
+            if packs is not None:
+                packs.disarm()
+                hip_train.set_active_packs(None)
         if self.is_dot:
             if not self._dot_ready:
                 self._dot_reachability(losses)

@@ -40,11 +40,15 @@ SIGNATURES = {
     "mda_conv_wgrad": "pppp" + "i" * 13 + "fis",
     "mda_wgrad_plan": "iiip",
     "mda_pack_conv_weights": "ppp" + "i" * 6 + "s",
+    "mda_pack_conv_weights_multi": "piis",
     # training-mode BatchNorm (csrc/bn.hip)
     "mda_bn_stats": "pii" + "pp" + "pppp" + "pppp" + "ffps",
     "mda_bn_apply": "pppppp" + "iii" + "s",
     "mda_bn_bwd_reduce": "pppppppp" + "iii" + "ppppp" + "s",
     "mda_bn_bwd_apply": "p" * 11 + "iii" + "s",
+    "mda_bn_tune": "ii",
+    "mda_bn_stats2": "piip" + "pppp" + "pppp" + "ffps",
+    "mda_bn_bwd_reduce2": "pppppppp" + "iii" + "pppp" + "s",
     # CRD memory (csrc/crd.hip)
     "mda_crd_scores": "ppppiiifs",
     "mda_crd_grad": "ppppppiiifs",

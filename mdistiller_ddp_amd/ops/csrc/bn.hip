@@ -150,6 +150,7 @@ _Pragma("unroll")
     })
   }
   block_channel_partials(s, ss, C, rpi, partial);
+  if (counter == nullptr) return;  // partials only; bn_finalize_kernel combines
   __shared__ double tot[2 * 2048];
   if (combine_partials(partial, 2 * C, counter, tot)) {
     if (threadIdx.x == 0 && nbt) nbt[0] += 1;
@@ -259,6 +260,7 @@ _Pragma("unroll")
     })
   }
   block_channel_partials(sdz, sdzx, C, rpi, partial);
+  if (counter == nullptr) return;  // partials only; bn_finalize_kernel combines
   __shared__ double tot[2 * 2048];
   if (combine_partials(partial, 2 * C, counter, tot)) {
     for (int t = threadIdx.x; t < 2 * C; t += blockDim.x) {
@@ -331,14 +333,92 @@ bn_bwd_apply_kernel(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ 
   }
 }
 
-inline int reduce_blocks(int64_t M, int64_t C) {
-  // ~8 sixteen-byte vectors per thread (issued 4 at a time), up to one block
-  // per CU; the two-level combine keeps the tail short at any block count
-  int64_t b = (M * (C / 8) + 256 * 8 - 1) / (256 * 8);
+// Channel-parallel combine of the per-block partials partial[nblk][2C]:
+// block b owns channels [8b, 8b+8); thread (v = tid % 16, g = tid / 16)
+// sums rows g, g+16, ... of value v in fp64, then the 16 row groups are
+// added in fixed order -- deterministic, no atomics, no cross-block hand-off.
+// MODE 0: forward statistics (mean, rstd, scale, shift, running stats);
+// MODE 1: backward sums (dbeta = sum dz, dgamma = sum dz*xhat).
+template <int MODE>
+__global__ void __launch_bounds__(256)
+bn_finalize_kernel(const float* __restrict__ partial, int nblk, int M, int C,
+                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                   float* __restrict__ running_mean, float* __restrict__ running_var,
+                   float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                   float* __restrict__ scale_out, float* __restrict__ shift_out, float momentum,
+                   float eps, int64_t* __restrict__ nbt, float* __restrict__ sums,
+                   float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  __shared__ double red[16][17];
+  const int v = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int q = v >> 3, k = v & 7;
+  const int c = blockIdx.x * 8 + k;
+  double acc = 0.0;
+  if (c < C) {
+    const float* src = partial + q * C + c;
+    float x[4];
+    int r = g;
+    for (; r + 48 < nblk; r += 64) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) x[u] = src[(int64_t)(r + 16 * u) * 2 * C];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc += (double)x[u];
+    }
+    for (; r < nblk; r += 16) acc += (double)src[(int64_t)r * 2 * C];
+  }
+  red[g][v] = acc;
+  __syncthreads();
+  if (threadIdx.x >= 8) return;
+  const int ch = blockIdx.x * 8 + threadIdx.x;
+  if (ch >= C) return;
+  double t0 = 0.0, t1 = 0.0;
+  for (int i = 0; i < 16; ++i) {
+    t0 += red[i][threadIdx.x];
+    t1 += red[i][8 + threadIdx.x];
+  }
+  if (MODE == 0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) nbt[0] += 1;
+    const double mean = t0 / M;
+    double var = t1 / M - mean * mean;
+    if (var < 0) var = 0;
+    const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+    const float gm = gamma ? gamma[ch] : 1.f;
+    const float bb = beta ? beta[ch] : 0.f;
+    mean_out[ch] = (float)mean;
+    rstd_out[ch] = rstd;
+    scale_out[ch] = gm * rstd;
+    shift_out[ch] = bb - (float)mean * gm * rstd;
+    if (running_mean) {
+      const double unbiased = M > 1 ? var * M / (M - 1) : var;
+      running_mean[ch] = (1.f - momentum) * running_mean[ch] + momentum * (float)mean;
+      running_var[ch] = (1.f - momentum) * running_var[ch] + momentum * (float)unbiased;
+    }
+  } else {
+    sums[ch] = (float)t0;
+    sums[C + ch] = (float)t1;
+    if (dbeta) dbeta[ch] += (float)t0;
+    if (dgamma) dgamma[ch] += (float)t1;
+  }
+}
+
+int g_red_vpt = 8;       // sixteen-byte vectors per thread in the reduction kernels
+int g_red_max = RED_MAX_BLOCKS;
+
+inline int reduce_blocks(int64_t M, int64_t C, int vpt = 0, int max_blocks = 0) {
+  // ~vpt sixteen-byte vectors per thread (issued 4 at a time)
+  if (vpt <= 0) vpt = g_red_vpt;
+  if (max_blocks <= 0) max_blocks = g_red_max;
+  int64_t b = (M * (C / 8) + 256 * vpt - 1) / (256 * vpt);
   if (b < 1) b = 1;
-  if (b > RED_MAX_BLOCKS) b = RED_MAX_BLOCKS;
+  if (b > max_blocks) b = max_blocks;
   return (int)b;
 }
+
+// Measured on MI355X (scripts/bn_microbench.py, student shapes): the stats
+// pass is load-bound and best at 8 vectors/thread; the backward reduce does
+// ~3x the math per vector and is best at 4 vectors/thread (up to 512 blocks).
+constexpr int STATS2_VPT = 8, STATS2_MAXB = 256;
+constexpr int BWD2_VPT = 4, BWD2_MAXB = 512;
+constexpr int RED2_MAX_BLOCKS = 512;  // workspace sizing: partial >= 2*C*512 floats
 
 inline int ew_blocks(int64_t n8) {
   // power of two, so the grid stride is a multiple of C/8 (hoisted per-channel params)
@@ -397,5 +477,55 @@ MDA_API int mda_bn_bwd_apply(const void* dout, const void* dpre, const void* y, 
                      (const bf16_t*)dout, (const bf16_t*)dpre, (const bf16_t*)y,
                      (const bf16_t*)res, scale, shift, mean, rstd, sums, (bf16_t*)dy,
                      (bf16_t*)dres, M, (int)C, (int)act);
+  MDA_CHECK_LAUNCH();
+}
+
+// Tuning hook (microbenchmarks): vectors per thread and max blocks of the
+// reduction kernels.  The in-kernel hand-off variants require max <= 256.
+MDA_API int mda_bn_tune(int64_t vpt, int64_t max_blocks) {
+  if (vpt < 1 || max_blocks < 1 || max_blocks > 4096) return (int)hipErrorInvalidValue;
+  g_red_vpt = (int)vpt;
+  g_red_max = (int)max_blocks;
+  return 0;
+}
+
+// Two-launch variants (the training path): partials kernel (no in-kernel
+// hand-off) + channel-parallel finalize.  2-3x faster than the single-launch
+// last-arriver combine at batch 64 (the agent-scope release/acquire hand-off
+// serialises two L2 round trips into every call).  Workspace: partial >=
+// 2*C*512 floats; no counters.
+MDA_API int mda_bn_stats2(const void* y, int64_t M, int64_t C, float* partial,
+                          const float* gamma, const float* beta, float* running_mean,
+                          float* running_var, float* mean, float* rstd, float* scale,
+                          float* shift, float momentum, float eps, int64_t* nbt,
+                          hipStream_t st) {
+  if (C % 8 || C / 8 > 256 || C > 2048) return (int)hipErrorInvalidValue;
+  const int nblk = reduce_blocks(M, C, STATS2_VPT, STATS2_MAXB);
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(nblk), dim3(256), 0, st, (const bf16_t*)y, (int)M,
+                     (int)C, partial, (unsigned*)nullptr, gamma, beta, running_mean, running_var,
+                     mean, rstd, scale, shift, momentum, eps, nbt);
+  hipLaunchKernelGGL(bn_finalize_kernel<0>, dim3((unsigned)((C + 7) / 8)), dim3(256), 0, st,
+                     partial, nblk, (int)M, (int)C, gamma, beta, running_mean, running_var, mean,
+                     rstd, scale, shift, momentum, eps, nbt, (float*)nullptr, (float*)nullptr,
+                     (float*)nullptr);
+  MDA_CHECK_LAUNCH();
+}
+
+MDA_API int mda_bn_bwd_reduce2(const void* dout, const void* dpre, const void* y, const void* res,
+                               const float* scale, const float* shift, const float* mean,
+                               const float* rstd, int64_t M, int64_t C, int64_t act,
+                               float* partial, float* sums, float* dgamma, float* dbeta,
+                               hipStream_t st) {
+  if (C % 8 || C / 8 > 256 || C > 2048) return (int)hipErrorInvalidValue;
+  const int nblk = reduce_blocks(M, C, BWD2_VPT, BWD2_MAXB);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nblk), dim3(256), 0, st, (const bf16_t*)dout,
+                     (const bf16_t*)dpre, (const bf16_t*)y, (const bf16_t*)res, scale, shift,
+                     mean, rstd, (int)M, (int)C, (int)act, partial, (unsigned*)nullptr, sums,
+                     dgamma, dbeta);
+  hipLaunchKernelGGL(bn_finalize_kernel<1>, dim3((unsigned)((C + 7) / 8)), dim3(256), 0, st,
+                     partial, nblk, (int)M, (int)C, (const float*)nullptr, (const float*)nullptr,
+                     (float*)nullptr, (float*)nullptr, (float*)nullptr, (float*)nullptr,
+                     (float*)nullptr, (float*)nullptr, 0.f, 0.f, (int64_t*)nullptr, sums, dgamma,
+                     dbeta);
   MDA_CHECK_LAUNCH();
 }

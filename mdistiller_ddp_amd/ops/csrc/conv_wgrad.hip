@@ -287,7 +287,60 @@ pack_kernel(const float* __restrict__ w, bf16_t* __restrict__ wf, bf16_t* __rest
   }
 }
 
+// All layers of a network in one launch.  table[l] = {w, wf, wt (0 = none),
+// Cout, Cin, KH, KW, Kp, KpT, start} (int64), start = first global element
+// of layer l; layer l covers Cout*Kp forward elements then, with wt, the
+// Cin*(KpT - KH*KW*Cout) dgrad padding zeros.
+constexpr int PACK_MAX_LAYERS = 128;
+constexpr int PACK_FIELDS = 10;
+
+__global__ void __launch_bounds__(256)
+pack_multi_kernel(const int64_t* __restrict__ table, int L, int64_t total) {
+  __shared__ int64_t tb[PACK_MAX_LAYERS * PACK_FIELDS];
+  for (int i = threadIdx.x; i < L * PACK_FIELDS; i += blockDim.x) tb[i] = table[i];
+  __syncthreads();
+  int l = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    while (l + 1 < L && i >= tb[(l + 1) * PACK_FIELDS + 9]) ++l;  // i only grows per thread
+    const int64_t* e = tb + l * PACK_FIELDS;
+    const float* w = (const float*)e[0];
+    bf16_t* wf = (bf16_t*)e[1];
+    bf16_t* wt = (bf16_t*)e[2];
+    const int Cout = (int)e[3], Cin = (int)e[4], KH = (int)e[5], KW = (int)e[6];
+    const int Kp = (int)e[7], KpT = (int)e[8];
+    const int64_t li = i - e[9];
+    const int64_t nf = (int64_t)Cout * Kp;
+    if (li < nf) {
+      const int co = (int)(li / Kp);
+      const int k = (int)(li - (int64_t)co * Kp);
+      float v = 0.f;
+      if (k < KH * KW * Cin) {
+        const int tap = k / Cin, ci = k - (k / Cin) * Cin;
+        const int kh = tap / KW, kw = tap - kh * KW;
+        v = w[(((int64_t)co * Cin + ci) * KH + kh) * KW + kw];
+        if (wt) wt[(int64_t)ci * KpT + tap * Cout + co] = f2bf(v);
+      }
+      wf[li] = f2bf(v);
+    } else if (wt) {
+      const int64_t pi = li - nf;
+      const int w_ = KpT - KH * KW * Cout;
+      const int ci = (int)(pi / w_);
+      const int j = (int)(pi - (int64_t)ci * w_);
+      wt[(int64_t)ci * KpT + KH * KW * Cout + j] = 0;
+    }
+  }
+}
+
 }  // namespace
+
+MDA_API int mda_pack_conv_weights_multi(const int64_t* table, int64_t L, int64_t total,
+                                        hipStream_t st) {
+  if (L <= 0 || L > PACK_MAX_LAYERS || total <= 0) return (int)hipErrorInvalidValue;
+  int blocks = (int)std::min<int64_t>((total + 255) / 256, 2048);
+  hipLaunchKernelGGL(pack_multi_kernel, dim3(blocks), dim3(256), 0, st, table, (int)L, total);
+  MDA_CHECK_LAUNCH();
+}
 
 MDA_API int mda_wgrad_plan(int64_t M, int64_t Cout, int64_t Kp, int64_t* splits) {
   int64_t tiles = ((Cout + TC - 1) / TC) * ((Kp + TK - 1) / TK);

@@ -4,7 +4,8 @@ One autograd node per layer:
 
 forward   pack weights (fp32 OIHW -> bf16 GEMM operands, 1 launch)
           conv          (MFMA implicit GEMM, raw output y)
-          bn_stats      (batch mean / rstd, scale/shift, running-stat update)
+          bn_stats      (per-block partials + channel-parallel finalize: batch mean /
+                         rstd, scale/shift, running-stat update)
           bn_apply      (z = y*scale + shift + res, out = act(z), optional preact)
 backward  bn_bwd_reduce (dgamma / dbeta accumulated straight into the flat grad buffer)
           bn_bwd_apply  (dy, and dz for the residual branch)
@@ -32,7 +33,7 @@ class _WS:
     """Per-device scratch for the BN reductions (partials + arrival counters)."""
 
     def __init__(self, device):
-        self.partial = torch.zeros(2 * 2048 * (256 + 16), dtype=torch.float32, device=device)
+        self.partial = torch.zeros(2 * 2048 * 512, dtype=torch.float32, device=device)
         self.counter = torch.zeros(64, dtype=torch.int32, device=device)
 
 
@@ -58,6 +59,78 @@ def _wgrad_splits(M, Cout, Kp):
         _ext.call("mda_wgrad_plan", M, Cout, Kp, s)
         v = _WG_PLANS[key] = s.value
     return v
+
+
+class PackCache:
+    """Packed bf16 GEMM operands of every student conv, refreshed by ONE launch per step.
+
+    The first (eager) forward of a layer packs it on its own and registers
+    persistent ``wf``/``wt`` buffers; from then on :meth:`pack_all` (called by
+    the training step before the forward, and captured into its hipGraph)
+    repacks every registered layer in a single ``mda_pack_conv_weights_multi``
+    launch and *arms* the cache, so the layers' forwards reuse the buffers
+    instead of launching one pack kernel each.  :meth:`disarm` after the
+    forward keeps any later, out-of-step call from seeing stale weights.
+    """
+
+    def __init__(self):
+        self.entries: dict = {}
+        self.armed = False
+        self._table = None
+        self._dirty = False
+        self._total = 0
+
+    def lookup(self, weight, need_dx):
+        if not self.armed:
+            return None
+        e = self.entries.get(id(weight))
+        if e is None or e["weight"] is not weight or (need_dx and e["wt"] is None):
+            return None
+        return e
+
+    def register(self, weight, wf, wt, Cout, Cin, KH, KW, Kp, KpT):
+        if torch.cuda.is_current_stream_capturing():
+            return
+        self.entries[id(weight)] = dict(weight=weight, wf=wf, wt=wt, meta=(Cout, Cin, KH, KW, Kp, KpT))
+        self._dirty = True
+
+    def _build(self, device):
+        rows, start = [], 0
+        for e in self.entries.values():
+            Cout, Cin, KH, KW, Kp, KpT = e["meta"]
+            n = Cout * Kp + (Cin * (KpT - KH * KW * Cout) if e["wt"] is not None else 0)
+            w = e["weight"]
+            rows.append([w.data_ptr(), e["wf"].data_ptr(), e["wt"].data_ptr() if e["wt"] is not None else 0,
+                         Cout, Cin, KH, KW, Kp, KpT, start])
+            start += n
+        self._table = torch.tensor(rows, dtype=torch.int64).to(device)
+        self._total = start
+        self._ptrs = [e["weight"].data_ptr() for e in self.entries.values()]
+        self._dirty = False
+
+    def pack_all(self, device) -> bool:
+        if not self.entries or len(self.entries) > 128:
+            return False
+        capturing = torch.cuda.is_current_stream_capturing()
+        stale = self._table is None or self._dirty or any(
+            e["weight"].data_ptr() != p for e, p in zip(self.entries.values(), self._ptrs))
+        if stale:
+            if capturing:
+                return False
+            self._build(device)
+        _ext.call("mda_pack_conv_weights_multi", self._table, self._table.shape[0], self._total)
+        self.armed = True
+        return True
+
+    def disarm(self):
+        self.armed = False
+
+
+_ACTIVE = [None]  # the PackCache of the training step currently running its forward
+
+
+def set_active_packs(cache) -> None:
+    _ACTIVE[0] = cache
 
 
 def _cl_bf16(t):
@@ -102,10 +175,17 @@ class _ConvBNActTrain(torch.autograd.Function):
         need_dx = ctx.needs_input_grad[0]
         KpT = (KH * KW * Cout + 63) // 64 * 64
         dev = x.device
-        wf = torch.empty(Cout, Kp, dtype=torch.bfloat16, device=dev)
-        wt = torch.empty(Cin, KpT, dtype=torch.bfloat16, device=dev) if need_dx else None
-        _ext.call("mda_pack_conv_weights", weight.detach().contiguous(), wf, wt, Cout, Cin, KH, KW,
-                  Kp, KpT)
+        packs = _ACTIVE[0]
+        ent = packs.lookup(weight, need_dx) if packs is not None else None
+        if ent is not None:  # packed for this step by PackCache.pack_all
+            wf, wt = ent["wf"], ent["wt"]
+        else:
+            wf = torch.empty(Cout, Kp, dtype=torch.bfloat16, device=dev)
+            wt = torch.empty(Cin, KpT, dtype=torch.bfloat16, device=dev) if need_dx else None
+            wc = weight.detach()
+            if packs is not None and wc.is_contiguous() and wc.dtype == torch.float32:
+                packs.register(weight, wf, wt, Cout, Cin, KH, KW, Kp, KpT)
+            _ext.call("mda_pack_conv_weights", wc.contiguous(), wf, wt, Cout, Cin, KH, KW, Kp, KpT)
         from .hip_layers import conv_plan
         tile, splits = conv_plan(M, Cout, Kp)
         part = torch.empty(splits * M * Cout, dtype=torch.float32, device=dev) if splits > 1 else None
@@ -115,7 +195,7 @@ class _ConvBNActTrain(torch.autograd.Function):
                   Cout, KH, KW, stride, pad, Kp, 0, tile, splits)
         ws = _ws(dev)
         stats = torch.empty(4, Cout, dtype=torch.float32, device=dev)  # mean, rstd, scale, shift
-        _ext.call("mda_bn_stats", y, M, Cout, ws.partial, ws.counter, gamma.detach(), beta.detach(),
+        _ext.call("mda_bn_stats2", y, M, Cout, ws.partial, gamma.detach(), beta.detach(),
                   bn.running_mean, bn.running_var, stats[0], stats[1], stats[2], stats[3],
                   float(bn.momentum), float(bn.eps), bn.num_batches_tracked)
         res = _cl_bf16(residual) if residual is not None else None
@@ -143,8 +223,8 @@ class _ConvBNActTrain(torch.autograd.Function):
         direct_gb = gamma.grad is not None and beta.grad is not None
         dg = gamma.grad if direct_gb else None
         db = beta.grad if direct_gb else None
-        _ext.call("mda_bn_bwd_reduce", dout, dpre, y, res, stats[2], stats[3], stats[0], stats[1],
-                  M, Cout, act, ws.partial, ws.counter, sums, dg, db)
+        _ext.call("mda_bn_bwd_reduce2", dout, dpre, y, res, stats[2], stats[3], stats[0], stats[1],
+                  M, Cout, act, ws.partial, sums, dg, db)
         need_res = ctx.has_res and ctx.needs_input_grad[4]
         dy = torch.empty_like(y)
         dres = torch.empty_like(y) if need_res else None

@@ -122,3 +122,35 @@ def test_student_train_step_uses_native_path():
     e_native = ((grads[0] - ref).norm() / ref.norm()).item()
     e_miopen = ((grads[1] - ref).norm() / ref.norm()).item()
     assert e_native < max(2.0 * e_miopen, 0.05), (e_native, e_miopen)
+
+
+def test_pack_cache_matches_per_layer_packing():
+    """TrainStep with the one-launch PackCache == per-layer packing, over a few
+    steps (the packed weights must track every optimizer update)."""
+    from mdistiller_ddp_amd.config import get_cfg
+    from mdistiller_ddp_amd.engine.build import build_distiller
+    from mdistiller_ddp_amd.engine.step import TrainStep
+    from mdistiller_ddp_amd.data.synthetic import SyntheticLoader
+    cfg = get_cfg()
+    cfg.DISTILLER.TYPE = "KD"
+    cfg.DISTILLER.TEACHER = "resnet32x4"
+    cfg.DISTILLER.STUDENT = "resnet8x4"
+    cfg.DISTILLER.RANDOM_TEACHER = True
+    torch.manual_seed(0)
+    d1 = build_distiller(cfg, 100, "cuda")
+    d2 = copy.deepcopy(d1)
+    out = []
+    for d, use_cache in ((d1, True), (d2, False)):
+        d.train()
+        st = TrainStep(d, cfg, "cuda", use_graph=False, dtype=torch.bfloat16)
+        st.set_epoch(1.0)
+        if not use_cache:
+            st._packs = hip_train.PackCache()
+            st._packs.pack_all = lambda device: False
+        for b in SyntheticLoader("cifar100", 16, "cuda", steps_per_epoch=4, channels_last=True):
+            st.step(b)
+        torch.cuda.synchronize()
+        if use_cache:
+            assert st._packs.entries and st._packs._table is not None
+        out.append(st.flat.data.clone())
+    torch.testing.assert_close(out[0], out[1], rtol=0, atol=0)

@@ -26,9 +26,31 @@ CONFIGS = {
     "kd_cifar_res32x4_res8x4": ("configs/cifar100/kd.yaml", 64, [], None),
     "crd_cifar_res32x4_res8x4": ("configs/cifar100/crd.yaml", 64, [], None),
     "reviewkd_cifar_res32x4_res8x4": ("configs/cifar100/reviewkd.yaml", 64, [], None),
+    "fitnet_cifar_res32x4_res8x4": ("configs/cifar100/fitnet.yaml", 64, [], None),
+    "ofd_cifar_res32x4_res8x4": ("configs/cifar100/ofd.yaml", 64, [], None),
+    "rkd_cifar_res32x4_res8x4": ("configs/cifar100/rkd.yaml", 64, [], None),
+    "at_cifar_res32x4_res8x4": ("configs/cifar100/at.yaml", 64, [], None),
+    "nst_cifar_res32x4_res8x4": ("configs/cifar100/nst.yaml", 64, [], None),
+    "pkt_cifar_res32x4_res8x4": ("configs/cifar100/pkt.yaml", 64, [], None),
+    "sp_cifar_res32x4_res8x4": ("configs/cifar100/sp.yaml", 64, [], None),
+    "vid_cifar_res32x4_res8x4": ("configs/cifar100/vid.yaml", 64, [], None),
+    "vanilla_cifar_res8x4": ("configs/cifar100/vanilla.yaml", 64,
+                             ["DISTILLER.STUDENT", "resnet8x4"], None),
+    "dkd_cifar_vgg13_vgg8": ("configs/cifar100/dkd/vgg13_vgg8.yaml", 64, [], None),
+    "dkd_cifar_wrn40_2_wrn16_2": ("configs/cifar100/dkd/wrn40_2_wrn_16_2.yaml", 64, [], None),
+    "dkd_cifar_res32x4_shuv1": ("configs/cifar100/dkd/res32x4_shuv1.yaml", 64, [], None),
+    "dkd_cifar_vgg13_mv2": ("configs/cifar100/dkd/vgg13_mv2.yaml", 64, [], None),
     "reviewkd_imagenet_r34_r18": ("configs/imagenet/r34_r18/reviewkd.yaml", 32, [], None),
     "dkd_imagenet_r50_mv1": ("configs/imagenet/r50_mv1/dkd.yaml", 64, [], None),
 }
+
+
+# reference "training time (ms)" per iteration at batch 64, `.github/dkd.png`
+# inset, CIFAR-100 ResNet32x4 -> ResNet8x4, unstated GPU
+BASELINE_MS = {"kd_cifar_res32x4_res8x4": 11.0, "dkd_cifar_res32x4_res8x4": 11.0,
+               "fitnet_cifar_res32x4_res8x4": 14.0, "ofd_cifar_res32x4_res8x4": 19.0,
+               "rkd_cifar_res32x4_res8x4": 25.0, "reviewkd_cifar_res32x4_res8x4": 26.0,
+               "crd_cifar_res32x4_res8x4": 41.0}
 
 
 def main():
@@ -43,13 +65,20 @@ def main():
     names = list(CONFIGS) if args.configs == "all" else args.configs.split(",")
     for name in names:
         yaml, bs, opts, ds = CONFIGS[name]
-        r = benchmark.run(os.path.join(ROOT, yaml), bs, args.steps, args.warmup, opts=opts,
-                          use_graph=not args.no_graph, dataset=ds)
+        try:
+            r = benchmark.run(os.path.join(ROOT, yaml), bs, args.steps, args.warmup, opts=opts,
+                              use_graph=not args.no_graph, dataset=ds)
+        except Exception as e:  # report and continue with the other configs
+            print(json.dumps({"config": name, "error": f"{type(e).__name__}: {e}"[:300]}), flush=True)
+            continue
         if r["rank"] == 0:
             row = {"config": name, "images_per_s": round(r["images_per_s"], 1),
                    "ms_per_step": round(r["ms_per_step"], 3), "per_gpu_batch": bs,
                    "n_gpus": r["n_gpus"], "graph": r["graph"], "dtype": r["dtype"],
                    "final_loss": round(r["final_loss"], 4)}
+            if name in BASELINE_MS and r["n_gpus"] == 1 and bs == 64:
+                row["baseline_ms"] = BASELINE_MS[name]
+                row["speedup_vs_baseline"] = round(BASELINE_MS[name] / r["ms_per_step"], 2)
             print(json.dumps(row), flush=True)
             if args.out:
                 with open(args.out, "a") as f:

@@ -41,6 +41,12 @@ SIGNATURES = {
     "mda_wgrad_plan": "iiip",
     "mda_pack_conv_weights": "ppp" + "i" * 6 + "s",
     "mda_pack_conv_weights_multi": "piis",
+    # depthwise 3x3 conv (csrc/dwconv.hip)
+    "mda_dw_pack": "pppiis",
+    "mda_dw_fwd": "ppppppp" + "i" * 11 + "s",
+    "mda_dw_dgrad": "ppp" + "i" * 10 + "s",
+    "mda_dw_wgrad_blocks": "iiiip",
+    "mda_dw_wgrad": "pppp" + "i" * 12 + "s",
     # training-mode BatchNorm (csrc/bn.hip)
     "mda_bn_stats": "pii" + "pp" + "pppp" + "pppp" + "ffps",
     "mda_bn_apply": "pppppp" + "iii" + "s",

@@ -1,0 +1,384 @@
+// Depthwise KxK convolution on NHWC bf16 activations (survey K3: MobileNetV1
+// `mobilenetv1.py:19-29`, MobileNetV2 `cifar/mobilenetv2.py:42-50`,
+// ShuffleNetV1/V2 depthwise 3x3).  There is no reduction over input channels,
+// so MFMA does not apply: this is a memory-bound stencil on the vector ALUs.
+//
+//  * forward   -- one thread owns V consecutive channels (V = 8/4/2/1 bf16, one
+//    16/8/4/2-byte load) of OWT = 4 consecutive output columns; per filter row
+//    the (OWT-1)*stride + K input columns it needs are loaded once into
+//    registers and reused by all four outputs.  Fused epilogue (inference /
+//    folded-BN teacher path): y = act(acc*scale + bias (+ res)), optional
+//    pre-activation; training path: raw y (BN runs in bn.hip).
+//  * dgrad     -- dx[h, w] = sum over taps whose (h + p - kh, w + p - kw) lands
+//    on the stride grid of dy; same V x OWT thread tile.
+//  * wgrad     -- per-block partial sums of dy * x for every (tap, channel),
+//    reduced over pixel lanes through LDS one tap at a time, then a
+//    channel-parallel finalize kernel combines the blocks in fixed order and
+//    writes/accumulates the fp32 [C, K, K] gradient (deterministic).
+// Weights arrive as fp32 packed tap-major [KH*KW, C] (coalesced per-channel
+// loads); folded teacher weights are packed once on the host.  3x3 kernels,
+// stride 1 or 2 (every depthwise layer of the model zoo); others use PyTorch.
+#include "common.h"
+
+namespace {
+
+constexpr int OWT = 4;       // output (or input, for dgrad) columns per thread
+constexpr int KS = 3;        // kernel size (every depthwise conv of the zoo is 3x3)
+
+template <int V> struct vec;
+template <> struct vec<8> { typedef uint4 t; };
+template <> struct vec<4> { typedef uint2 t; };
+template <> struct vec<2> { typedef uint32_t t; };
+template <> struct vec<1> { typedef uint16_t t; };
+
+template <int V>
+__device__ __forceinline__ void ld_vec(const bf16_t* p, float (&o)[V]) {
+  const typename vec<V>::t r = *reinterpret_cast<const typename vec<V>::t*>(p);
+  const bf16_t* e = reinterpret_cast<const bf16_t*>(&r);
+#pragma unroll
+  for (int i = 0; i < V; ++i) o[i] = bf2f(e[i]);
+}
+
+template <int V>
+__device__ __forceinline__ void st_vec(bf16_t* p, const float (&v)[V]) {
+  typename vec<V>::t r;
+  bf16_t* e = reinterpret_cast<bf16_t*>(&r);
+#pragma unroll
+  for (int i = 0; i < V; ++i) e[i] = f2bf(v[i]);
+  *reinterpret_cast<typename vec<V>::t*>(p) = r;
+}
+
+__device__ __forceinline__ float act_fn(float v, int act) {
+  if (act == 1) return fmaxf(v, 0.f);
+  if (act == 2) return fminf(fmaxf(v, 0.f), 6.f);
+  return v;
+}
+
+struct DwParams {
+  const bf16_t* x;      // [N, H, W, C]   (dgrad: dy [N, Ho, Wo, C])
+  const float* w;       // [KH*KW, C] fp32
+  const float* scale;   // [C] or null
+  const float* bias;    // [C] or null
+  const bf16_t* res;    // [N, Ho, Wo, C] or null
+  bf16_t* y;            // output
+  bf16_t* preact;       // or null
+  int N, H, W, C, Ho, Wo, KH, KW, stride, pad, act;
+};
+
+template <int V, int S>
+__global__ void __launch_bounds__(256) dw_fwd_kernel(const DwParams p) {
+  constexpr int NCOLS = (OWT - 1) * S + KS;
+  const int CG = p.C / V;
+  const int WT = (p.Wo + OWT - 1) / OWT;
+  const int64_t total = (int64_t)p.N * p.Ho * WT * CG;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int cg = (int)(i % CG);
+    int64_t r = i / CG;
+    const int wt = (int)(r % WT);
+    r /= WT;
+    const int ho = (int)(r % p.Ho);
+    const int n = (int)(r / p.Ho);
+    const int c0 = cg * V;
+    const int wo0 = wt * OWT;
+    const int iw0 = wo0 * S - p.pad;
+    float acc[OWT][V];
+#pragma unroll
+    for (int j = 0; j < OWT; ++j)
+#pragma unroll
+      for (int v = 0; v < V; ++v) acc[j][v] = 0.f;
+#pragma unroll
+    for (int kh = 0; kh < KS; ++kh) {
+      const int ih = ho * S - p.pad + kh;
+      if ((unsigned)ih >= (unsigned)p.H) continue;
+      const bf16_t* row = p.x + (((int64_t)n * p.H + ih) * p.W) * p.C + c0;
+      float xin[NCOLS][V];
+#pragma unroll
+      for (int q = 0; q < NCOLS; ++q) {
+        const int iw = iw0 + q;
+        if ((unsigned)iw < (unsigned)p.W) {
+          ld_vec<V>(row + (int64_t)iw * p.C, xin[q]);
+        } else {
+#pragma unroll
+          for (int v = 0; v < V; ++v) xin[q][v] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int kw = 0; kw < KS; ++kw) {
+        float wv[V];
+        const float* wp = p.w + (kh * KS + kw) * p.C + c0;
+#pragma unroll
+        for (int v = 0; v < V; ++v) wv[v] = wp[v];
+#pragma unroll
+        for (int j = 0; j < OWT; ++j)
+#pragma unroll
+          for (int v = 0; v < V; ++v) acc[j][v] += xin[j * S + kw][v] * wv[v];
+      }
+    }
+    float sc[V], bi[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      sc[v] = p.scale ? p.scale[c0 + v] : 1.f;
+      bi[v] = p.bias ? p.bias[c0 + v] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < OWT; ++j) {
+      const int wo = wo0 + j;
+      if (wo >= p.Wo) break;
+      const int64_t o = (((int64_t)n * p.Ho + ho) * p.Wo + wo) * p.C + c0;
+      float t[V];
+#pragma unroll
+      for (int v = 0; v < V; ++v) t[v] = acc[j][v] * sc[v] + bi[v];
+      if (p.res) {
+        float rr[V];
+        ld_vec<V>(p.res + o, rr);
+#pragma unroll
+        for (int v = 0; v < V; ++v) t[v] += rr[v];
+      }
+      if (p.preact) st_vec<V>(p.preact + o, t);
+#pragma unroll
+      for (int v = 0; v < V; ++v) t[v] = act_fn(t[v], p.act);
+      st_vec<V>(p.y + o, t);
+    }
+  }
+}
+
+// dx[n, h, w, c] = sum_{kh, kw} dy[n, (h + p - kh)/s, (w + p - kw)/s, c] * w[kh, kw, c]
+// over taps landing on the stride grid.  p.x = dy, p.y = dx; H/W = input dims.
+template <int V>
+__global__ void __launch_bounds__(256) dw_dgrad_kernel(const DwParams p) {
+  const int CG = p.C / V;
+  const int WT = (p.W + OWT - 1) / OWT;
+  const int64_t total = (int64_t)p.N * p.H * WT * CG;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int cg = (int)(i % CG);
+    int64_t r = i / CG;
+    const int wt = (int)(r % WT);
+    r /= WT;
+    const int h = (int)(r % p.H);
+    const int n = (int)(r / p.H);
+    const int c0 = cg * V;
+    const int w0 = wt * OWT;
+    float acc[OWT][V];
+#pragma unroll
+    for (int j = 0; j < OWT; ++j)
+#pragma unroll
+      for (int v = 0; v < V; ++v) acc[j][v] = 0.f;
+#pragma unroll
+    for (int kh = 0; kh < KS; ++kh) {
+      const int t = h + p.pad - kh;
+      if (t < 0 || t % p.stride) continue;
+      const int oh = t / p.stride;
+      if (oh >= p.Ho) continue;
+      const bf16_t* row = p.x + (((int64_t)n * p.Ho + oh) * p.Wo) * p.C + c0;
+#pragma unroll
+      for (int kw = 0; kw < KS; ++kw) {
+        float wv[V];
+        const float* wp = p.w + (kh * KS + kw) * p.C + c0;
+#pragma unroll
+        for (int v = 0; v < V; ++v) wv[v] = wp[v];
+#pragma unroll
+        for (int j = 0; j < OWT; ++j) {
+          const int u = w0 + j + p.pad - kw;
+          if (w0 + j >= p.W || u < 0 || u % p.stride) continue;
+          const int ow = u / p.stride;
+          if (ow >= p.Wo) continue;
+          float d[V];
+          ld_vec<V>(row + (int64_t)ow * p.C, d);
+#pragma unroll
+          for (int v = 0; v < V; ++v) acc[j][v] += d[v] * wv[v];
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < OWT; ++j) {
+      const int w = w0 + j;
+      if (w >= p.W) break;
+      st_vec<V>(p.y + (((int64_t)n * p.H + h) * p.W + w) * p.C + c0, acc[j]);
+    }
+  }
+}
+
+// Per-block partials of dW[tap, c] = sum_m dy[m, c] * x[src(m, tap), c].
+// Thread = (channel group cg, pixel lane pl); partial[blk][KH*KW][C].
+template <int V>
+__global__ void __launch_bounds__(256)
+dw_wgrad_partial_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
+                        float* __restrict__ partial, int N, int H, int W, int C, int Ho, int Wo,
+                        int KH, int KW, int stride, int pad) {
+  __shared__ float red[256 * 8];
+  const int CG = C / V;
+  const int PL = max(1, 256 / CG);  // pixel lanes per block
+  const int tid = threadIdx.x;
+  const int cg = tid % CG, pl = tid / CG;
+  const bool active = tid < CG * PL && cg < CG;
+  const int c0 = cg * V;
+  const int64_t M = (int64_t)N * Ho * Wo;
+  constexpr int KK = KS * KS;
+  float acc[KK][V];
+#pragma unroll
+  for (int t = 0; t < KK; ++t)
+#pragma unroll
+    for (int v = 0; v < V; ++v) acc[t][v] = 0.f;
+  if (active) {
+    for (int64_t m = (int64_t)blockIdx.x * PL + pl; m < M; m += (int64_t)gridDim.x * PL) {
+      const int wo = (int)(m % Wo);
+      const int64_t r = m / Wo;
+      const int ho = (int)(r % Ho);
+      const int n = (int)(r / Ho);
+      float d[V];
+      ld_vec<V>(dy + m * C + c0, d);
+#pragma unroll
+      for (int kh = 0; kh < KS; ++kh) {
+        const int ih = ho * stride - pad + kh;
+        if ((unsigned)ih >= (unsigned)H) continue;
+#pragma unroll
+        for (int kw = 0; kw < KS; ++kw) {
+          const int iw = wo * stride - pad + kw;
+          if ((unsigned)iw >= (unsigned)W) continue;
+          float xv[V];
+          ld_vec<V>(x + (((int64_t)n * H + ih) * W + iw) * C + c0, xv);
+          const int t = kh * KS + kw;
+#pragma unroll
+          for (int v = 0; v < V; ++v) acc[t][v] += d[v] * xv[v];
+        }
+      }
+    }
+  }
+  // reduce over pixel lanes, one tap at a time: LDS [PL][C]
+#pragma unroll
+  for (int t = 0; t < KK; ++t) {
+    if (active) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) red[pl * C + c0 + v] = acc[t][v];
+    }
+    __syncthreads();
+    for (int c = tid; c < C; c += blockDim.x) {
+      float s = 0.f;
+      for (int q = 0; q < PL; ++q) s += red[q * C + c];
+      partial[((int64_t)blockIdx.x * KK + t) * C + c] = s;
+    }
+    __syncthreads();
+  }
+}
+
+// grad[c, tap] (+)= sum_blk partial[blk][tap][c]   (fixed order, fp64)
+__global__ void __launch_bounds__(256)
+dw_wgrad_finalize_kernel(const float* __restrict__ partial, int nblk, int KK, int C,
+                         float* __restrict__ grad, int accumulate) {
+  const int64_t V = (int64_t)KK * C;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < V;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    double s = 0.0;
+    for (int b = 0; b < nblk; ++b) s += (double)partial[(int64_t)b * V + i];
+    const int t = (int)(i / C), c = (int)(i - (int64_t)t * C);
+    float* o = grad + (int64_t)c * KK + t;
+    *o = accumulate ? *o + (float)s : (float)s;
+  }
+}
+
+// fp32 [C, KH, KW] -> fp32 [KH*KW, C] (optionally scaled per channel)
+__global__ void dw_pack_kernel(const float* __restrict__ w, const float* __restrict__ scale,
+                               float* __restrict__ out, int C, int KK) {
+  const int total = C * KK;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int t = i / C, c = i - t * C;
+    out[i] = w[c * KK + t] * (scale ? scale[c] : 1.f);
+  }
+}
+
+inline int vwidth(int C) { return (C % 8 == 0) ? 8 : (C % 4 == 0) ? 4 : (C % 2 == 0) ? 2 : 1; }
+
+inline int grid_for(int64_t work) {
+  int64_t b = (work + 255) / 256;
+  if (b > 8192) b = 8192;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+int launch_fwd(const DwParams& p, hipStream_t st) {
+  const int V = vwidth(p.C);
+  const int64_t work = (int64_t)p.N * p.Ho * ((p.Wo + OWT - 1) / OWT) * (p.C / V);
+  const dim3 g(grid_for(work));
+#define DW_FWD(VV, SS) hipLaunchKernelGGL((dw_fwd_kernel<VV, SS>), g, dim3(256), 0, st, p)
+  if (p.stride == 1) {
+    if (V == 8) DW_FWD(8, 1); else if (V == 4) DW_FWD(4, 1); else if (V == 2) DW_FWD(2, 1); else DW_FWD(1, 1);
+  } else {
+    if (V == 8) DW_FWD(8, 2); else if (V == 4) DW_FWD(4, 2); else if (V == 2) DW_FWD(2, 2); else DW_FWD(1, 2);
+  }
+#undef DW_FWD
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+MDA_API int mda_dw_pack(const float* w, const float* scale, float* out, int64_t C, int64_t KK,
+                        hipStream_t st) {
+  hipLaunchKernelGGL(dw_pack_kernel, dim3(grid_for(C * KK)), dim3(256), 0, st, w, scale, out,
+                     (int)C, (int)KK);
+  MDA_CHECK_LAUNCH();
+}
+
+// x [N,H,W,C] bf16; w packed [KH*KW, C] fp32; scale/bias [C] or null; res/preact or null.
+MDA_API int mda_dw_fwd(const void* x, const float* w, const float* scale, const float* bias,
+                       const void* res, void* y, void* preact, int64_t N, int64_t H, int64_t W,
+                       int64_t C, int64_t Ho, int64_t Wo, int64_t KH, int64_t KW, int64_t stride,
+                       int64_t pad, int64_t act, hipStream_t st) {
+  if (KH != KS || KW != KS || stride < 1 || stride > 2) return (int)hipErrorInvalidValue;
+  DwParams p{(const bf16_t*)x, w, scale, bias, (const bf16_t*)res, (bf16_t*)y, (bf16_t*)preact,
+             (int)N, (int)H, (int)W, (int)C, (int)Ho, (int)Wo, (int)KH, (int)KW, (int)stride,
+             (int)pad, (int)act};
+  return launch_fwd(p, st);
+}
+
+// dy [N,Ho,Wo,C] bf16 -> dx [N,H,W,C] bf16.
+MDA_API int mda_dw_dgrad(const void* dy, const float* w, void* dx, int64_t N, int64_t H, int64_t W,
+                         int64_t C, int64_t Ho, int64_t Wo, int64_t KH, int64_t KW, int64_t stride,
+                         int64_t pad, hipStream_t st) {
+  if (KH != KS || KW != KS || stride < 1 || stride > 2) return (int)hipErrorInvalidValue;
+  DwParams p{(const bf16_t*)dy, w, nullptr, nullptr, nullptr, (bf16_t*)dx, nullptr, (int)N,
+             (int)H, (int)W, (int)C, (int)Ho, (int)Wo, (int)KH, (int)KW, (int)stride, (int)pad, 0};
+  const int V = vwidth((int)C);
+  const int64_t work = N * H * ((W + OWT - 1) / OWT) * (C / V);
+  const dim3 g(grid_for(work));
+#define DW_DG(VV) hipLaunchKernelGGL(dw_dgrad_kernel<VV>, g, dim3(256), 0, st, p)
+  if (V == 8) DW_DG(8); else if (V == 4) DW_DG(4); else if (V == 2) DW_DG(2); else DW_DG(1);
+#undef DW_DG
+  MDA_CHECK_LAUNCH();
+}
+
+MDA_API int mda_dw_wgrad_blocks(int64_t N, int64_t Ho, int64_t Wo, int64_t C, int64_t* nblk) {
+  const int V = vwidth((int)C);
+  const int64_t CG = C / V;
+  const int64_t PL = CG >= 256 ? 1 : 256 / CG;
+  const int64_t M = N * Ho * Wo;
+  int64_t b = (M + PL * 16 - 1) / (PL * 16);  // ~16 pixels per lane
+  if (b > 512) b = 512;
+  if (b < 1) b = 1;
+  *nblk = b;
+  return 0;
+}
+
+// x [N,H,W,C], dy [N,Ho,Wo,C] bf16; partial >= nblk*KH*KW*C floats;
+// grad fp32 [C, KH, KW] (accumulated when accumulate != 0).
+MDA_API int mda_dw_wgrad(const void* x, const void* dy, float* partial, float* grad, int64_t N,
+                         int64_t H, int64_t W, int64_t C, int64_t Ho, int64_t Wo, int64_t KH,
+                         int64_t KW, int64_t stride, int64_t pad, int64_t nblk,
+                         int64_t accumulate, hipStream_t st) {
+  if (KH != KS || KW != KS || stride < 1 || stride > 2 || nblk < 1) return (int)hipErrorInvalidValue;
+  const int V = vwidth((int)C);
+  if (C / V > 256) return (int)hipErrorInvalidValue;
+#define DW_WG(VV)                                                                             \
+  hipLaunchKernelGGL(dw_wgrad_partial_kernel<VV>, dim3(nblk), dim3(256), 0, st,              \
+                     (const bf16_t*)x, (const bf16_t*)dy, partial, (int)N, (int)H, (int)W,    \
+                     (int)C, (int)Ho, (int)Wo, (int)KH, (int)KW, (int)stride, (int)pad)
+  if (V == 8) DW_WG(8);
+  else if (V == 4) DW_WG(4);
+  else if (V == 2) DW_WG(2);
+  else DW_WG(1);
+#undef DW_WG
+  hipLaunchKernelGGL(dw_wgrad_finalize_kernel, dim3(grid_for(KH * KW * C)), dim3(256), 0, st,
+                     partial, (int)nblk, (int)(KH * KW), (int)C, grad, (int)accumulate);
+  MDA_CHECK_LAUNCH();
+}

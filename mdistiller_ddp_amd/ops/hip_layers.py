@@ -35,7 +35,11 @@ def _needs_grad(x, conv, bn) -> bool:
 def conv_supported(x, conv, bn) -> bool:
     if not (x.is_cuda and x.dim() == 4 and isinstance(conv, nn.Conv2d)):
         return False
-    if conv.groups != 1 or conv.dilation != (1, 1) or conv.padding_mode != "zeros":
+    if conv.groups != 1:
+        from .hip_train import dw_supported_geometry
+        if not dw_supported_geometry(conv):
+            return False
+    if conv.dilation != (1, 1) or conv.padding_mode != "zeros":
         return False
     if conv.stride[0] != conv.stride[1] or not isinstance(conv.padding, tuple):
         return False
@@ -95,7 +99,48 @@ def _nhwc_bf16(t):
     return t.contiguous(memory_format=torch.channels_last)
 
 
+@torch.no_grad()
+def _dw_packed(conv, bn):
+    """Depthwise: BN folded into fp32 tap-major [9, C] weights + bias (cached)."""
+    key = _version_key(conv, bn)
+    cache = getattr(conv, "_mda_dwpack", None)
+    if cache is not None and cache[0] == key and cache[1] is bn:
+        return cache[2], cache[3]
+    from .hip_train import dw_pack
+    C = conv.out_channels
+    dev = conv.weight.device
+    b = conv.bias.detach().float() if conv.bias is not None else torch.zeros(C, device=dev)
+    s = None
+    if bn is not None:
+        g = bn.weight.detach().float() if bn.weight is not None else torch.ones(C, device=dev)
+        beta = bn.bias.detach().float() if bn.bias is not None else torch.zeros(C, device=dev)
+        s = (g / torch.sqrt(bn.running_var.float() + bn.eps)).contiguous()
+        b = beta + (b - bn.running_mean.float()) * s
+    wp = dw_pack(conv.weight, s)
+    b = b.contiguous()
+    conv._mda_dwpack = (key, bn, wp, b)
+    return wp, b
+
+
+def _dw_conv_bn_act(x, conv, bn, act, residual, want_preact):
+    wp, bias = _dw_packed(conv, bn)
+    x = _nhwc_bf16(x)
+    N, C, H, W = x.shape
+    s, p = conv.stride[0], conv.padding[0]
+    Ho = (H + 2 * p - 3) // s + 1
+    Wo = (W + 2 * p - 3) // s + 1
+    y = torch.empty((N, C, Ho, Wo), dtype=torch.bfloat16, device=x.device,
+                    memory_format=torch.channels_last)
+    pre = torch.empty_like(y) if want_preact else None
+    res = _nhwc_bf16(residual) if residual is not None else None
+    _ext.call("mda_dw_fwd", x, wp, None, bias, res, y, pre, N, H, W, C, Ho, Wo, 3, 3, s, p,
+              _ACT[act])
+    return y, pre
+
+
 def conv_bn_act(x, conv, bn, act, residual, want_preact):
+    if conv.groups != 1:
+        return _dw_conv_bn_act(x, conv, bn, act, residual, want_preact)
     wp, bias = _packed(conv, bn)
     x = _nhwc_bf16(x)
     N, Cin, H, W = x.shape

@@ -144,8 +144,10 @@ def train_supported(x, conv, bn) -> bool:
         return False
     if bn is None or not bn.training or not bn.track_running_stats or bn.momentum is None:
         return False
-    if conv.groups != 1 or conv.dilation != (1, 1) or conv.padding_mode != "zeros" or conv.bias is not None:
+    if conv.dilation != (1, 1) or conv.padding_mode != "zeros" or conv.bias is not None:
         return False
+    if conv.groups != 1:
+        return dw_train_supported(x, conv, bn)
     if conv.stride[0] != conv.stride[1] or not isinstance(conv.padding, tuple) or conv.padding[0] != conv.padding[1]:
         return False
     if conv.kernel_size[0] != conv.kernel_size[1]:
@@ -160,10 +162,55 @@ def train_supported(x, conv, bn) -> bool:
     return torch.is_grad_enabled()
 
 
+def is_depthwise(conv) -> bool:
+    return (conv.groups > 1 and conv.groups == conv.in_channels == conv.out_channels)
+
+
+def dw_supported_geometry(conv) -> bool:
+    """3x3 depthwise, stride 1/2, square padding (csrc/dwconv.hip)."""
+    return (is_depthwise(conv) and conv.kernel_size == (3, 3) and conv.stride[0] == conv.stride[1]
+            and conv.stride[0] in (1, 2) and isinstance(conv.padding, tuple)
+            and conv.padding[0] == conv.padding[1] and conv.dilation == (1, 1)
+            and conv.padding_mode == "zeros" and conv.out_channels <= 2048)
+
+
+def dw_train_supported(x, conv, bn) -> bool:
+    if not dw_supported_geometry(conv) or bn is None or bn.weight is None or bn.bias is None:
+        return False
+    if conv.out_channels % 8:  # BN kernels are 8-channel vectorised
+        return False
+    if x.dtype != torch.bfloat16 and not (torch.is_autocast_enabled("cuda")
+                                          and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+        return False
+    return torch.is_grad_enabled()
+
+
+def dw_pack(weight, scale=None):
+    """fp32 [C, 1, 3, 3] -> fp32 tap-major [9, C] (optionally scaled per channel)."""
+    C = weight.shape[0]
+    out = torch.empty(9, C, dtype=torch.float32, device=weight.device)
+    _ext.call("mda_dw_pack", weight.detach().float().contiguous(), scale, out, C, 9)
+    return out
+
+
+def _dw_wgrad_blocks(N, Ho, Wo, C):
+    key = ("dw", N, Ho, Wo, C)
+    v = _WG_PLANS.get(key)
+    if v is None:
+        b = ctypes.c_int64(0)
+        _ext.call("mda_dw_wgrad_blocks", N, Ho, Wo, C, b)
+        v = _WG_PLANS[key] = b.value
+    return v
+
+
 class _ConvBNActTrain(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, gamma, beta, residual, meta, bn, want_preact):
-        stride, pad, act = meta
+        stride, pad, act = meta[:3]
+        if len(meta) > 3 and meta[3] == "dw":
+            return _dw_forward(ctx, x, weight, gamma, beta, residual, stride, pad, act, bn,
+                               want_preact)
+        ctx.kind = "dense"
         x = _cl_bf16(x)
         N, Cin, H, W = x.shape
         Cout, _, KH, KW = weight.shape
@@ -211,6 +258,8 @@ class _ConvBNActTrain(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout, dpre):
+        if ctx.kind == "dw":
+            return _dw_backward(ctx, dout, dpre)
         x, wt, weight, gamma, beta, y, res, stats = ctx.saved_tensors
         N, Cin, H, W, Cout, Ho, Wo, KH, KW, stride, pad, Kp, KpT, act = ctx.meta
         M = N * Ho * Wo
@@ -251,6 +300,86 @@ class _ConvBNActTrain(torch.autograd.Function):
         dgamma = None if direct_gb else sums[1].clone()
         dbeta = None if direct_gb else sums[0].clone()
         return dx, dw, dgamma, dbeta, dres, None, None, None
+
+
+def _bn_train_forward(y, M, C, gamma, beta, bn, residual, act, want_preact):
+    dev = y.device
+    ws = _ws(dev)
+    stats = torch.empty(4, C, dtype=torch.float32, device=dev)  # mean, rstd, scale, shift
+    _ext.call("mda_bn_stats2", y, M, C, ws.partial, gamma.detach(), beta.detach(),
+              bn.running_mean, bn.running_var, stats[0], stats[1], stats[2], stats[3],
+              float(bn.momentum), float(bn.eps), bn.num_batches_tracked)
+    res = _cl_bf16(residual) if residual is not None else None
+    out = torch.empty_like(y)
+    pre = torch.empty_like(y) if want_preact else None
+    _ext.call("mda_bn_apply", y, stats[2], stats[3], res, out, pre, M, C, act)
+    return out, pre, res, stats
+
+
+def _bn_train_backward(ctx, dout, dpre, y, res, stats, gamma, beta, M, C, act):
+    """-> (dy, dres, dgamma or None, dbeta or None); dgamma/dbeta go straight
+    into bound flat-gradient views when present."""
+    dev = y.device
+    dout = _cl_bf16(dout) if dout is not None else None
+    dpre = _cl_bf16(dpre) if dpre is not None else None
+    ws = _ws(dev)
+    sums = torch.empty(2, C, dtype=torch.float32, device=dev)
+    direct_gb = gamma.grad is not None and beta.grad is not None
+    dg = gamma.grad if direct_gb else None
+    db = beta.grad if direct_gb else None
+    _ext.call("mda_bn_bwd_reduce2", dout, dpre, y, res, stats[2], stats[3], stats[0], stats[1],
+              M, C, act, ws.partial, sums, dg, db)
+    dy = torch.empty_like(y)
+    dres = torch.empty_like(y) if res is not None else None
+    _ext.call("mda_bn_bwd_apply", dout, dpre, y, res, stats[2], stats[3], stats[0], stats[1],
+              sums, dy, dres, M, C, act)
+    if direct_gb:
+        return dy, dres, None, None
+    return dy, dres, sums[1].clone(), sums[0].clone()
+
+
+def _dw_forward(ctx, x, weight, gamma, beta, residual, stride, pad, act, bn, want_preact):
+    ctx.kind = "dw"
+    x = _cl_bf16(x)
+    N, C, H, W = x.shape
+    Ho = (H + 2 * pad - 3) // stride + 1
+    Wo = (W + 2 * pad - 3) // stride + 1
+    wp = dw_pack(weight)
+    y = torch.empty((N, C, Ho, Wo), dtype=torch.bfloat16, device=x.device,
+                    memory_format=torch.channels_last)
+    _ext.call("mda_dw_fwd", x, wp, None, None, None, y, None, N, H, W, C, Ho, Wo, 3, 3, stride,
+              pad, 0)
+    M = N * Ho * Wo
+    out, pre, res, stats = _bn_train_forward(y, M, C, gamma, beta, bn, residual, act, want_preact)
+    ctx.save_for_backward(x, wp, weight, gamma, beta, y, res, stats)
+    ctx.meta = (N, C, H, W, Ho, Wo, stride, pad, act)
+    ctx.has_res = residual is not None
+    return out, pre
+
+
+def _dw_backward(ctx, dout, dpre):
+    x, wp, weight, gamma, beta, y, res, stats = ctx.saved_tensors
+    N, C, H, W, Ho, Wo, stride, pad, act = ctx.meta
+    M = N * Ho * Wo
+    dy, dres, dgamma, dbeta = _bn_train_backward(ctx, dout, dpre, y, res, stats, gamma, beta, M,
+                                                 C, act)
+    if not (ctx.has_res and ctx.needs_input_grad[4]):
+        dres = None
+    dx = None
+    if ctx.needs_input_grad[0]:
+        dx = torch.empty((N, C, H, W), dtype=torch.bfloat16, device=y.device,
+                         memory_format=torch.channels_last)
+        _ext.call("mda_dw_dgrad", dy, wp, dx, N, H, W, C, Ho, Wo, 3, 3, stride, pad)
+    dw = None
+    if ctx.needs_input_grad[1]:
+        nblk = _dw_wgrad_blocks(N, Ho, Wo, C)
+        part = torch.empty(nblk * 9 * C, dtype=torch.float32, device=y.device)
+        direct_w = weight.grad is not None and weight.grad.is_contiguous()
+        target = weight.grad if direct_w else torch.empty_like(weight, memory_format=torch.contiguous_format)
+        _ext.call("mda_dw_wgrad", x, dy, part, target, N, H, W, C, Ho, Wo, 3, 3, stride, pad,
+                  nblk, 1 if direct_w else 0)
+        dw = None if direct_w else target
+    return dx, dw, dgamma, dbeta, dres, None, None, None
 
 
 def pack_weights(weight, dgrad=True):
@@ -301,6 +430,8 @@ def conv_wgrad(x, dy, weight_shape, stride, pad):
 
 def conv_bn_act_train(x, conv, bn, act, residual, want_preact):
     meta = (conv.stride[0], conv.padding[0], _ACT[act])
+    if conv.groups != 1:
+        meta = meta + ("dw",)
     out, pre = _ConvBNActTrain.apply(x, conv.weight, bn.weight, bn.bias, residual, meta, bn,
                                      bool(want_preact))
     return out, pre

@@ -17,10 +17,68 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ._base import Distiller, warmup_factor
+from ._base import Distiller
 from ..ops import losses as L
 from ..ops import feat_losses as FL
 from ..ops.nn import conv_bn_act
+
+
+class _ABFFuse(torch.autograd.Function):
+    """``x * s0 + up(y) * s1``, ``(s0, s1) = sigmoid(att_conv([x; up(y)]))`` on the
+    fused HIP kernels (``ops/csrc/reviewkd.hip``): no upsampled copy of ``y``,
+    no concat, no separate 1x1 conv / sigmoid / blend launches."""
+
+    @staticmethod
+    def forward(ctx, x, y, weight, bias):
+        from ..ops import _ext
+        N, C, h, w = x.shape
+        hy, wy = y.shape[2], y.shape[3]
+        x = x.contiguous(memory_format=torch.channels_last)
+        y = y.to(x.dtype).contiguous(memory_format=torch.channels_last)
+        out = torch.empty_like(x, memory_format=torch.channels_last)
+        att = torch.empty(N * h * w * 2, dtype=torch.float32, device=x.device)
+        wt = weight.detach().reshape(2, 2 * C).contiguous()
+        _ext.call("mda_abf_fwd", x, y, wt, bias.detach() if bias is not None else None, out, att,
+                  N, h, w, hy, wy, C)
+        ctx.save_for_backward(x, y, att, weight, bias)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        import ctypes
+        from ..ops import _ext
+        x, y, att, weight, bias = ctx.saved_tensors
+        N, C, h, w = x.shape
+        hy, wy = y.shape[2], y.shape[3]
+        dout = dout.to(x.dtype).contiguous(memory_format=torch.channels_last)
+        dx = torch.empty_like(x, memory_format=torch.channels_last)
+        dy = torch.empty_like(y, memory_format=torch.channels_last) if ctx.needs_input_grad[1] else None
+        dyup = torch.empty(N * h * w * C, dtype=torch.float32, device=x.device)
+        nb = ctypes.c_int64(0)
+        _ext.call("mda_abf_bwd_blocks", N, h, w, C, nb)
+        part = torch.empty(nb.value * (4 * C + 2), dtype=torch.float32, device=x.device)
+        need_w, need_b = ctx.needs_input_grad[2], bias is not None and ctx.needs_input_grad[3]
+        direct = (need_w and weight.grad is not None and weight.grad.is_contiguous()
+                  and (not need_b or bias.grad is not None))
+        dW = weight.grad if direct else (torch.zeros_like(weight) if need_w else None)
+        db = (bias.grad if direct else torch.zeros_like(bias)) if need_b else None
+        _ext.call("mda_abf_bwd", dout, x, y, att, weight.detach().reshape(2, 2 * C).contiguous(),
+                  dx, dy, dyup, part, dW, db, N, h, w, hy, wy, C, nb.value, 1)
+        if direct:
+            return dx, dy, None, None
+        return dx, dy, dW, db
+
+
+def _abf_native_ok(x, y, att_conv) -> bool:
+    from ..ops.backend import hip_enabled_for
+    if not (hip_enabled_for(x) and x.dtype == torch.bfloat16 and x.dim() == 4 and y.dim() == 4):
+        return False
+    C = x.shape[1]
+    G = C // 8
+    conv = att_conv[0]
+    return (C % 8 == 0 and 0 < G <= 64 and (G & (G - 1)) == 0 and y.shape[1] == C
+            and conv.weight.shape == (2, 2 * C, 1, 1) and conv.weight.dtype == torch.float32
+            and x.shape[0] == y.shape[0])
 
 
 class ABF(nn.Module):
@@ -42,9 +100,12 @@ class ABF(nn.Module):
         n, _, h, w = x.shape
         x = conv_bn_act(x, self.conv1[0], self.conv1[1], "none")[0]
         if self.att_conv is not None:
-            y = F.interpolate(y, (shape, shape), mode="nearest")
-            z = self.att_conv(torch.cat([x, y.to(x.dtype)], dim=1))
-            x = x * z[:, 0].view(n, 1, h, w) + y * z[:, 1].view(n, 1, h, w)
+            if x.shape[-2:] == (shape, shape) and _abf_native_ok(x, y, self.att_conv):
+                x = _ABFFuse.apply(x, y, self.att_conv[0].weight, self.att_conv[0].bias)
+            else:
+                y = F.interpolate(y, (shape, shape), mode="nearest")
+                z = self.att_conv(torch.cat([x, y.to(x.dtype)], dim=1))
+                x = x * z[:, 0].view(n, 1, h, w) + y * z[:, 1].view(n, 1, h, w)
         if x.shape[-1] != out_shape:
             x = F.interpolate(x, (out_shape, out_shape), mode="nearest")
         y = conv_bn_act(x, self.conv2[0], self.conv2[1], "none")[0]
@@ -90,6 +151,6 @@ class ReviewKD(Distiller):
         pooled_t = ft["pooled_feat"].reshape(ft["pooled_feat"].shape[0], -1, 1, 1)
         t_feats = list(ft["preact_feats"][1:]) + [pooled_t]
         loss_ce = L.ce(logits_student, target, self.ce_loss_weight)
-        loss_kd = (self.reviewkd_loss_weight * warmup_factor(kwargs["epoch"], self.warmup_epochs)
-                   * FL.hcl_loss(results, t_feats))
+        loss_kd = FL.hcl_loss_weighted(results, t_feats, self.reviewkd_loss_weight,
+                                       kwargs.get("epoch"), self.warmup_epochs)
         return logits_student, {"loss_ce": loss_ce, "loss_kd": loss_kd}

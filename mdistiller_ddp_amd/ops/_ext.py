@@ -63,6 +63,11 @@ SIGNATURES = {
     "mda_pool_fc_fwd": "ipppppiiiis",
     "mda_pool_fc_bwd": "ippppppp" + "iiiii" + "s",
     "mda_meters_update": "ippii" + "pppp" + "ips",
+    # ReviewKD HCL + ABF (csrc/reviewkd.hip)
+    "mda_hcl_loss": "piiipfpfps",
+    "mda_abf_fwd": "pppppp" + "iiiiii" + "s",
+    "mda_abf_bwd_blocks": "iiiip",
+    "mda_abf_bwd": "ppppppppppp" + "iiiiii" + "ii" + "s",
     # data augmentation (csrc/aug.hip)
     "mda_crop_flip_norm": "ppppppp" + "iiiiii" + "s",
     # optimizers (csrc/optim.hip)

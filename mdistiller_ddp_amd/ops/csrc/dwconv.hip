@@ -201,52 +201,75 @@ __global__ void __launch_bounds__(256) dw_dgrad_kernel(const DwParams p) {
 }
 
 // Per-block partials of dW[tap, c] = sum_m dy[m, c] * x[src(m, tap), c].
-// Thread = (channel group cg, pixel lane pl); partial[blk][KH*KW][C].
-template <int V>
+// Thread = (channel group cg, lane); a lane's work item is OWT consecutive
+// output pixels of one output row: it loads the 3 x ((OWT-1)*S + 3) input
+// columns and OWT dy vectors once (~5.5 loads per pixel instead of 10, all
+// independent), accumulating acc[9][V].  partial[blk][9][C].
+template <int V, int S>
 __global__ void __launch_bounds__(256)
 dw_wgrad_partial_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
                         float* __restrict__ partial, int N, int H, int W, int C, int Ho, int Wo,
-                        int KH, int KW, int stride, int pad) {
+                        int pad) {
+  constexpr int NCOLS = (OWT - 1) * S + KS;
+  constexpr int KK = KS * KS;
   __shared__ float red[256 * 8];
   const int CG = C / V;
-  const int PL = max(1, 256 / CG);  // pixel lanes per block
+  const int PL = max(1, 256 / CG);  // lanes per block
   const int tid = threadIdx.x;
   const int cg = tid % CG, pl = tid / CG;
-  const bool active = tid < CG * PL && cg < CG;
+  const bool active = tid < CG * PL;
   const int c0 = cg * V;
-  const int64_t M = (int64_t)N * Ho * Wo;
-  constexpr int KK = KS * KS;
+  const int WT = (Wo + OWT - 1) / OWT;
+  const int64_t items = (int64_t)N * Ho * WT;
   float acc[KK][V];
 #pragma unroll
   for (int t = 0; t < KK; ++t)
 #pragma unroll
     for (int v = 0; v < V; ++v) acc[t][v] = 0.f;
   if (active) {
-    for (int64_t m = (int64_t)blockIdx.x * PL + pl; m < M; m += (int64_t)gridDim.x * PL) {
-      const int wo = (int)(m % Wo);
-      const int64_t r = m / Wo;
+    for (int64_t it = (int64_t)blockIdx.x * PL + pl; it < items; it += (int64_t)gridDim.x * PL) {
+      const int wt = (int)(it % WT);
+      const int64_t r = it / WT;
       const int ho = (int)(r % Ho);
       const int n = (int)(r / Ho);
-      float d[V];
-      ld_vec<V>(dy + m * C + c0, d);
+      const int wo0 = wt * OWT;
+      float d[OWT][V];
+#pragma unroll
+      for (int j = 0; j < OWT; ++j) {
+        if (wo0 + j < Wo) {
+          ld_vec<V>(dy + (((int64_t)n * Ho + ho) * Wo + wo0 + j) * C + c0, d[j]);
+        } else {
+#pragma unroll
+          for (int v = 0; v < V; ++v) d[j][v] = 0.f;
+        }
+      }
+      const int iw0 = wo0 * S - pad;
 #pragma unroll
       for (int kh = 0; kh < KS; ++kh) {
-        const int ih = ho * stride - pad + kh;
+        const int ih = ho * S - pad + kh;
         if ((unsigned)ih >= (unsigned)H) continue;
+        const bf16_t* row = x + (((int64_t)n * H + ih) * W) * C + c0;
+        float xin[NCOLS][V];
 #pragma unroll
-        for (int kw = 0; kw < KS; ++kw) {
-          const int iw = wo * stride - pad + kw;
-          if ((unsigned)iw >= (unsigned)W) continue;
-          float xv[V];
-          ld_vec<V>(x + (((int64_t)n * H + ih) * W + iw) * C + c0, xv);
-          const int t = kh * KS + kw;
+        for (int q = 0; q < NCOLS; ++q) {
+          const int iw = iw0 + q;
+          if ((unsigned)iw < (unsigned)W) {
+            ld_vec<V>(row + (int64_t)iw * C, xin[q]);
+          } else {
 #pragma unroll
-          for (int v = 0; v < V; ++v) acc[t][v] += d[v] * xv[v];
+            for (int v = 0; v < V; ++v) xin[q][v] = 0.f;
+          }
         }
+#pragma unroll
+        for (int kw = 0; kw < KS; ++kw)
+#pragma unroll
+          for (int j = 0; j < OWT; ++j)
+#pragma unroll
+            for (int v = 0; v < V; ++v) acc[kh * KS + kw][v] += d[j][v] * xin[j * S + kw][v];
       }
     }
   }
-  // reduce over pixel lanes, one tap at a time: LDS [PL][C]
+  // reduce over lanes, one tap at a time: LDS [PL][C]
 #pragma unroll
   for (int t = 0; t < KK; ++t) {
     if (active) {
@@ -270,8 +293,16 @@ dw_wgrad_finalize_kernel(const float* __restrict__ partial, int nblk, int KK, in
   const int64_t V = (int64_t)KK * C;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < V;
        i += (int64_t)gridDim.x * blockDim.x) {
-    double s = 0.0;
-    for (int b = 0; b < nblk; ++b) s += (double)partial[(int64_t)b * V + i];
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    int b = 0;
+    for (; b + 4 <= nblk; b += 4) {  // four independent loads in flight, fixed order
+      s0 += (double)partial[(int64_t)(b + 0) * V + i];
+      s1 += (double)partial[(int64_t)(b + 1) * V + i];
+      s2 += (double)partial[(int64_t)(b + 2) * V + i];
+      s3 += (double)partial[(int64_t)(b + 3) * V + i];
+    }
+    for (; b < nblk; ++b) s0 += (double)partial[(int64_t)b * V + i];
+    const double s = (s0 + s1) + (s2 + s3);
     const int t = (int)(i / C), c = (int)(i - (int64_t)t * C);
     float* o = grad + (int64_t)c * KK + t;
     *o = accumulate ? *o + (float)s : (float)s;
@@ -352,8 +383,8 @@ MDA_API int mda_dw_wgrad_blocks(int64_t N, int64_t Ho, int64_t Wo, int64_t C, in
   const int V = vwidth((int)C);
   const int64_t CG = C / V;
   const int64_t PL = CG >= 256 ? 1 : 256 / CG;
-  const int64_t M = N * Ho * Wo;
-  int64_t b = (M + PL * 16 - 1) / (PL * 16);  // ~16 pixels per lane
+  const int64_t items = N * Ho * ((Wo + OWT - 1) / OWT);
+  int64_t b = (items + PL * 4 - 1) / (PL * 4);  // ~4 items (16 pixels) per lane
   if (b > 512) b = 512;
   if (b < 1) b = 1;
   *nblk = b;
@@ -369,14 +400,15 @@ MDA_API int mda_dw_wgrad(const void* x, const void* dy, float* partial, float* g
   if (KH != KS || KW != KS || stride < 1 || stride > 2 || nblk < 1) return (int)hipErrorInvalidValue;
   const int V = vwidth((int)C);
   if (C / V > 256) return (int)hipErrorInvalidValue;
-#define DW_WG(VV)                                                                             \
-  hipLaunchKernelGGL(dw_wgrad_partial_kernel<VV>, dim3(nblk), dim3(256), 0, st,              \
+#define DW_WG(VV, SS)                                                                         \
+  hipLaunchKernelGGL((dw_wgrad_partial_kernel<VV, SS>), dim3(nblk), dim3(256), 0, st,        \
                      (const bf16_t*)x, (const bf16_t*)dy, partial, (int)N, (int)H, (int)W,    \
-                     (int)C, (int)Ho, (int)Wo, (int)KH, (int)KW, (int)stride, (int)pad)
-  if (V == 8) DW_WG(8);
-  else if (V == 4) DW_WG(4);
-  else if (V == 2) DW_WG(2);
-  else DW_WG(1);
+                     (int)C, (int)Ho, (int)Wo, (int)pad)
+  if (stride == 1) {
+    if (V == 8) DW_WG(8, 1); else if (V == 4) DW_WG(4, 1); else if (V == 2) DW_WG(2, 1); else DW_WG(1, 1);
+  } else {
+    if (V == 8) DW_WG(8, 2); else if (V == 4) DW_WG(4, 2); else if (V == 2) DW_WG(2, 2); else DW_WG(1, 2);
+  }
 #undef DW_WG
   hipLaunchKernelGGL(dw_wgrad_finalize_kernel, dim3(grid_for(KH * KW * C)), dim3(256), 0, st,
                      partial, (int)nblk, (int)(KH * KW), (int)C, grad, (int)accumulate);

@@ -254,3 +254,89 @@ def hcl_loss(fstudent, fteacher):
         loss = loss / tot
         loss_all = loss_all + loss
     return loss_all
+
+
+# --------------------------------------------------------------------------
+# fused HIP path of HCL (csrc/reviewkd.hip::mda_hcl_loss)
+
+def _hcl_cpb(C, HW):
+    for cpb in (8, 4, 2, 1):
+        if C % cpb == 0 and HW * cpb <= 16384:
+            return cpb
+    return 0
+
+
+def hcl_native_ok(fstudent, fteacher) -> bool:
+    from .backend import hip_enabled_for
+    if not fstudent or len(fstudent) != len(fteacher) or len(fstudent) > 8:
+        return False
+    for a, b in zip(fstudent, fteacher):
+        if not (hip_enabled_for(a) and a.dim() == 4 and a.shape == b.shape
+                and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16):
+            return False
+        if _hcl_cpb(a.shape[1], a.shape[2] * a.shape[3]) == 0:
+            return False
+    return True
+
+
+class _HCL(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, weight, warmup, epoch, n, *tensors):
+        import numpy as np
+        from . import _ext
+        fs, ft = tensors[:n], tensors[n:]
+        rows, grads, nblk, lds = [], [], 0, 0
+        keep = []
+        for a, b in zip(fs, ft):
+            a = a.contiguous(memory_format=torch.channels_last)
+            b = b.contiguous(memory_format=torch.channels_last)
+            keep += [a, b]
+            N, C, H, W = a.shape
+            cpb = _hcl_cpb(C, H * W)
+            g = torch.empty_like(a, memory_format=torch.channels_last)
+            grads.append(g)
+            nb = N * (C // cpb)
+            rows.append([a.data_ptr(), b.data_ptr(), g.data_ptr(), N, H, W, C, cpb, nblk, nb])
+            nblk += nb
+            lds = max(lds, H * W * cpb)
+        table = np.asarray(rows, dtype=np.int64)
+        dev = fs[0].device
+        partial = torch.empty(nblk, dtype=torch.float32, device=dev)
+        loss = torch.empty(1, dtype=torch.float32, device=dev)
+        ep = epoch if (epoch is not None and warmup and warmup > 0) else None
+        _ext.call("mda_hcl_loss", table.ctypes.data, len(rows), nblk, lds, partial, float(weight),
+                  ep, float(warmup or 0.0), loss)
+        ctx.save_for_backward(*grads)
+        ctx.n = n
+        return loss.reshape(())
+
+    @staticmethod
+    def backward(ctx, go):
+        from . import _ext
+        grads = ctx.saved_tensors
+        a = go.float().reshape(1).contiguous()
+        outs = []
+        for g in grads:
+            o = torch.empty_like(g)
+            _ext.call("mda_axpby", 1, a, g, None, None, o, g.numel())
+            outs.append(o)
+        return (None, None, None, None, *outs, *([None] * ctx.n))
+
+
+def hcl_loss_weighted(fstudent, fteacher, weight, epoch=None, warmup=0.0):
+    """``weight * min(epoch / warmup, 1) * hcl_loss(fstudent, fteacher)`` (teacher detached).
+
+    On the GPU with bf16 features this is ONE fused launch (+ a tiny
+    finalize) for all levels, forward value and gradient together.
+    """
+    ft = [t.detach() for t in fteacher]
+    if hcl_native_ok(fstudent, ft) and (epoch is None or isinstance(epoch, torch.Tensor)):
+        ep = epoch
+        if ep is not None and (ep.dtype != torch.float32 or ep.device != fstudent[0].device):
+            ep = ep.to(device=fstudent[0].device, dtype=torch.float32)
+        return _HCL.apply(float(weight), float(warmup or 0.0), ep, len(fstudent), *fstudent, *ft)
+    f = float(weight)
+    if epoch is not None and warmup and warmup > 0:
+        f = f * (torch.clamp(epoch.float() / float(warmup), max=1.0)
+                 if isinstance(epoch, torch.Tensor) else min(float(epoch) / float(warmup), 1.0))
+    return f * hcl_loss(fstudent, ft)

@@ -808,6 +808,169 @@ conv_halo_kernel(const ConvParams p) {
   conv_epilogue<BM, BN>(p, acc, smem, m0, n0);
 }
 
+// Single-chunk (Cin == 64) halo variant: the block's one patch is staged
+// once (no second patch buffer, no dummy prefetch of a next chunk) and the
+// freed LDS holds a RING-deep weight-tile ring, so weight tiles are fetched
+// RING-1 taps ahead instead of 2 -- the 3-deep ring of the generic kernel
+// leaves every tap waiting on an L2 round trip at these tiny per-tap MFMA
+// workloads.  Still two blocks per CU.
+template <int BN>
+struct Halo1Smem {
+  static constexpr int PATCH = HALO_PROWS * 128;
+  static constexpr int BT = BN * 128;
+  static constexpr int RING = (81920 - PATCH) / BT > 9 ? 9 : (81920 - PATCH) / BT;
+  static constexpr int PIPE = PATCH + RING * BT;
+  static constexpr int CTILE = ConvSmem<HALO_BM, BN>::CTILE;
+  static constexpr int BYTES = PIPE > CTILE ? PIPE : CTILE;
+};
+
+template <int BN, bool FLIP>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+conv_halo1_kernel(const ConvParams p) {
+  constexpr int BM = HALO_BM;
+  constexpr int MI = BM / 32, NI = BN / 32;
+  constexpr int BLOADS = (BN * 8 + 255) / 256;
+  constexpr int PATCH = Halo1Smem<BN>::PATCH;
+  constexpr int BT = Halo1Smem<BN>::BT;
+  constexpr int RING = Halo1Smem<BN>::RING;
+
+  __shared__ __attribute__((aligned(16))) char smem[Halo1Smem<BN>::BYTES];
+  typedef __attribute__((address_space(3))) char lds_char;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_char*)smem;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int m0 = blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const uint32_t wave_off = (uint32_t)__builtin_amdgcn_readfirstlane(wid) * 1024u;
+  const bf16_t* const zero = (const bf16_t*)g_zero16;
+
+  // block geometry: R output rows per block; IMGS images of RH rows each
+  const int W = p.W, H = p.H;
+  const int R = BM / W;
+  const int IMGS = R > H ? R / H : 1;
+  const int RH = R > H ? H : R;
+  const int PW = W + 2;                       // patch row length (pixels)
+  const int PH = RH + 2;                      // patch rows per image
+  const int grow0 = m0 / W;                   // first global output row (n*H + oh)
+  const int img0 = grow0 / H;
+  const int oh0 = grow0 - img0 * H;
+
+  // patch DMA: piece j covers patch rows 32j..32j+31; this thread's row/chunk
+  const int trow = tid >> 3;
+  const int chunk = (tid & 7) ^ ((trow >> 1) & 7);  // (32j + trow) >> 1 & 7 == trow >> 1 & 7
+  int p_src[HALO_PIECES];                     // element offset of the patch pixel, or -1
+  {
+    const int P = IMGS * PH * PW;
+#pragma unroll
+    for (int j = 0; j < HALO_PIECES; ++j) {
+      const int pr = 32 * j + trow;
+      int off = -1;
+      if (pr < P) {
+        const int img = pr / (PH * PW);
+        const int rem = pr - img * PH * PW;
+        const int ir = rem / PW, ic = rem - (rem / PW) * PW;
+        const int n = img0 + img;
+        const int ih = oh0 + ir - 1, iw = ic - 1;
+        if (n < p.N && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
+          off = ((n * H + ih) * W + iw) * p.Cin;
+      }
+      p_src[j] = off;
+    }
+  }
+  // weight rows
+  const bf16_t* b_row[BLOADS];
+  bool b_ok[BLOADS];
+#pragma unroll
+  for (int j = 0; j < BLOADS; ++j) {
+    const int co = n0 + trow + 32 * j;
+    b_ok[j] = (trow + 32 * j < BN) && co < p.Cout;
+    b_row[j] = p.w + (int64_t)(b_ok[j] ? co : 0) * p.Kp + chunk * 8;
+  }
+
+  const int c_begin = 0, c_end = 1;  // Cin == 64: one channel chunk, 9 taps
+  const int nsteps = 9;
+
+  auto issue_b = [&](int step, int bbuf) {   // weight tile of step (chunk, tap)
+    const bool live = step < nsteps;
+    const int st = live ? step : 0;
+    const int cc = c_begin + st / 9, tap = st - (st / 9) * 9;
+    const int wtap = FLIP ? 8 - tap : tap;
+    const uint32_t base = lds0 + PATCH + (uint32_t)(bbuf * BT) + wave_off;
+#pragma unroll
+    for (int j = 0; j < BLOADS; ++j) {
+      const bf16_t* src = (live && b_ok[j]) ? b_row[j] + wtap * p.Cin + cc * BK : zero;
+      glds16(src, base + (uint32_t)(j * 32 * 128));
+    }
+  };
+  auto issue_piece = [&](int cc, int pbuf, int j) {  // patch piece j of chunk cc
+    const bool live = cc < c_end;
+    const int off = p_src[j];
+    const bf16_t* src = (live && off >= 0) ? p.x + off + cc * BK + chunk * 8 : zero;
+    glds16(src, lds0 + (uint32_t)(pbuf * PATCH) + wave_off + (uint32_t)(j * 32 * 128));
+  };
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // per A fragment: patch row of (pixel, tap 0,0)
+  const int frow = lane & 15;
+  const int g4 = lane >> 4;
+  int a_prow[MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int ml = wm * (BM / 2) + i * 16 + frow;   // local output pixel
+    const int lr = ml / W, c = ml - (ml / W) * W;   // local output row, column
+    const int img = lr / RH, r = lr - img * RH;
+    a_prow[i] = (img * PH + r) * PW + c;
+  }
+  const int bswz = (frow >> 1) & 7;
+
+  auto compute = [&](int pbuf, int bbuf, int tap) {
+    const char* Ps = smem + pbuf * PATCH;
+    const char* Bs = smem + PATCH + bbuf * BT;
+    const int kh = tap / 3, kw = tap - (tap / 3) * 3;
+    const int toff = kh * PW + kw;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int q = kk * 4 + g4;
+      bf16x8 af[MI], bfr[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int pr = a_prow[i] + toff;
+        af[i] = *(const bf16x8*)(Ps + pr * 128 + ((q ^ ((pr >> 1) & 7)) * 16));
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+        bfr[j] = *(const bf16x8*)(Bs + (wn * (BN / 2) + j * 16 + frow) * 128 + ((q ^ bswz) * 16));
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  // prologue: the (only) patch, then weight tiles of steps 0 .. RING-2
+#pragma unroll
+  for (int j = 0; j < HALO_PIECES; ++j) issue_piece(c_begin, 0, j);
+#pragma unroll
+  for (int s0 = 0; s0 < RING - 1; ++s0) issue_b(s0, s0);
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    // DMAs issued after B(tap): B(tap+1) .. B(tap+RING-2), always RING-2 tiles
+    // (tiles past the last step are zero-page dummies, so counts stay constant)
+    vm_wait_barrier<(RING - 2) * BLOADS>();
+    issue_b(tap + RING - 1, (tap + RING - 1) % RING);
+    compute(0, tap % RING, tap);
+  }
+  vm_wait_barrier<0>();
+  conv_epilogue<BM, BN>(p, acc, smem, m0, n0);
+}
+
 // Split-K combine: y = epilogue(sum_z partial[z]) in fixed z order.
 // Cout % 8 == 0: one thread per 8 channels (16-byte traffic).
 __global__ void __launch_bounds__(256) conv_splitk_epilogue(const ConvParams p, int splits) {
@@ -856,6 +1019,14 @@ bool halo_eligible(const ConvParams& p) {
   if (R <= p.H ? (p.H % R) : (R % p.H)) return false;
   const int imgs = R > p.H ? R / p.H : 1, rh = R > p.H ? p.H : R;
   return imgs * (rh + 2) * (p.W + 2) <= HALO_PROWS;
+}
+
+bool use_halo1() {
+  static const bool on = [] {
+    const char* e = getenv("MDA_CONV_HALO1");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 
 bool use_glds() {
@@ -930,7 +1101,15 @@ int dispatch(ConvParams& p, int mode, int64_t tile, int64_t splits, hipStream_t 
     p.steps_per_split = (int)((nchunks + splits - 1) / splits);
     const int bn = p.Cout <= 32 ? 32 : 64;
     dim3 grid((p.M + HALO_BM - 1) / HALO_BM, (p.Cout + bn - 1) / bn, (int)splits);
-    if (bn == 32) {
+    if (nchunks == 1 && splits == 1 && use_halo1()) {
+      if (bn == 32) {
+        if (halo == 2) hipLaunchKernelGGL((conv_halo1_kernel<32, true>), grid, dim3(256), 0, st, p);
+        else hipLaunchKernelGGL((conv_halo1_kernel<32, false>), grid, dim3(256), 0, st, p);
+      } else {
+        if (halo == 2) hipLaunchKernelGGL((conv_halo1_kernel<64, true>), grid, dim3(256), 0, st, p);
+        else hipLaunchKernelGGL((conv_halo1_kernel<64, false>), grid, dim3(256), 0, st, p);
+      }
+    } else if (bn == 32) {
       if (halo == 2) hipLaunchKernelGGL((conv_halo_kernel<32, true>), grid, dim3(256), 0, st, p);
       else hipLaunchKernelGGL((conv_halo_kernel<32, false>), grid, dim3(256), 0, st, p);
     } else {

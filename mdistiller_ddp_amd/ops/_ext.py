@@ -68,6 +68,10 @@ SIGNATURES = {
     "mda_abf_fwd": "pppppp" + "iiiiii" + "s",
     "mda_abf_bwd_blocks": "iiiip",
     "mda_abf_bwd": "ppppppppppp" + "iiiiii" + "ii" + "s",
+    # detection: multi-level ROIAlign + NMS (csrc/det.hip)
+    "mda_roi_align_fwd": "ii" + "pppppp" + "iiiiii" + "s",
+    "mda_roi_align_bwd": "ii" + "pppppp" + "iiiiii" + "s",
+    "mda_nms": "pifpipps",
     # data augmentation (csrc/aug.hip)
     "mda_crop_flip_norm": "ppppppp" + "iiiiii" + "s",
     # optimizers (csrc/optim.hip)

@@ -52,7 +52,10 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d | None = No
         from . import hip_train
         if _TRAIN_KERNELS["on"] and hip_train.train_supported(x, conv, bn):
             return hip_train.conv_bn_act_train(x, conv, bn, act, residual, want_preact)
-    y = conv(x)
+    # the raw convolution (not ``conv(x)``): modules that route their own
+    # forward through this op -- e.g. the detection Conv2d with a norm child --
+    # must not recurse
+    y = nn.Conv2d._conv_forward(conv, x, conv.weight, conv.bias) if isinstance(conv, nn.Conv2d) else conv(x)
     if bn is not None:
         y = _bn(y, bn)
     if residual is not None:

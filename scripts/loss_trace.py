@@ -1,8 +1,11 @@
 """Per-step losses of a config on the GPU (eager vs graph, bf16 vs fp32):
 debugging aid for divergence/NaN reports from benchmarks/throughput.py."""
+import os
 import sys
 
-import torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
 
 from mdistiller_ddp_amd.config import get_cfg
 from mdistiller_ddp_amd.engine.build import build_distiller

@@ -96,8 +96,11 @@ class Distiller(nn.Module):
         after issuing the student forward so the two overlap on the GPU.
         """
         if self._teacher_train_bn:  # OFD (SURVEY D17): BN stats update, same stream
-            with torch.no_grad():
-                return streams.TeacherOutput(self.teacher(image))
+            # fp32 even inside a bf16 step: bf16 MIOpen train-mode BN replayed
+            # from a hipGraph drifted from eager and went non-finite
+            # (scripts/gpu_ab_ofd.sh); fp32 graph == fp32 eager exactly.
+            with torch.no_grad(), torch.autocast("cuda", enabled=False):
+                return streams.TeacherOutput(self.teacher(image.float()))
         return streams.run_teacher_async(self.teacher, image)
 
     def forward_train(self, **kwargs):

@@ -17,7 +17,8 @@ import torch
 
 
 def run(cfg_file: str, per_gpu_batch: int, steps: int, warmup: int, opts=(), use_graph=True,
-        backend="auto", dtype="bf16", teacher_stream=True, dataset=None, crd_k=None):
+        backend="auto", dtype="bf16", teacher_stream=True, dataset=None, crd_k=None,
+        check_replicas=False):
     from .ops.backend import set_backend
     from .parallel import dist as D
     from .config import get_cfg
@@ -41,6 +42,8 @@ def run(cfg_file: str, per_gpu_batch: int, steps: int, warmup: int, opts=(), use
     cfg.freeze()
     ds = dataset or cfg.DATASET.TYPE
     _, ncls, ntrain, _ = dataset_shape(ds)
+    # same seed on every rank is NOT relied upon: TrainStep broadcasts rank 0's
+    # full state (C2) -- rank-dependent seeding here proves it
     torch.manual_seed(1234 + info.rank)
     distiller = build_distiller(cfg, num_classes=ncls, device=dev, num_data=ntrain)
     dt = torch.bfloat16 if (dtype == "bf16" and dev.type == "cuda") else torch.float32
@@ -79,6 +82,15 @@ def run(cfg_file: str, per_gpu_batch: int, steps: int, warmup: int, opts=(), use
     el = float(t.item())
     m = step.meters.summary(reduce=True)
     n = info.world_size
+    same = None
+    if check_replicas and D.is_dist():
+        # after the timed steps: every rank's parameters (student, distiller modules,
+        # teacher) must equal rank 0's
+        from .parallel import state_checksum
+        c = state_checksum(distiller, step.flat, buffers=False)
+        allc = [torch.empty_like(c) for _ in range(n)]
+        torch.distributed.all_gather(allc, c)
+        same = all(torch.equal(allc[0], a) for a in allc)
     return {
         "seconds": el,
         "ms_per_step": 1000.0 * el / steps,
@@ -87,6 +99,9 @@ def run(cfg_file: str, per_gpu_batch: int, steps: int, warmup: int, opts=(), use
         "global_batch": n * per_gpu_batch,
         "final_loss": m["loss"],
         "graph": step.use_graph,
+        "graph_comm": step.graph_comm,
+        "comm_backend": info.backend,
+        "replicas_identical": same,
         "dtype": "bf16" if dt == torch.bfloat16 else "fp32",
         "rank": info.rank,
     }

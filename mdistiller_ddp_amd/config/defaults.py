@@ -94,6 +94,9 @@ CFG.DIST.BACKEND = "auto"            # auto -> nccl(RCCL) on GPU, gloo on CPU
 CFG.DIST.BUCKET_MB = 8.0             # gradient bucket size (MB of fp32)
 CFG.DIST.TIMEOUT_S = 600
 CFG.DIST.GRAD_DTYPE = "fp32"         # fp32 | bf16 wire format for gradient all-reduce
+CFG.DIST.GRAPH_COMM = "auto"         # capture | split | auto: all-reduce inside the step's
+                                     # hipGraph (RCCL, overlapped with backward) or between two graphs
+CFG.DIST.BROADCAST_INIT = True       # rank-0 broadcast of all params/buffers at step construction (C2)
 
 # Distillation methods -----------------------------------------------------
 CFG.KD = CN()

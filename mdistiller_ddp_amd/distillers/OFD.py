@@ -91,7 +91,9 @@ class OFD(Distiller):
                     vals.append(-3 * s)
             margins.append(torch.tensor(vals, dtype=torch.float32).reshape(1, -1, 1, 1))
         for i, m in enumerate(margins):
-            self.register_buffer(f"margin{i}", m)
+            # not persistent: the reference keeps the margins in a plain list, so
+            # its OFD checkpoints have no margin keys (strict resume must load them)
+            self.register_buffer(f"margin{i}", m, persistent=False)
         self._n_margins = len(margins)
 
     @property

@@ -65,6 +65,8 @@ class _ABFFuse(torch.autograd.Function):
         _ext.call("mda_abf_bwd", dout, x, y, att, weight.detach().reshape(2, 2 * C).contiguous(),
                   dx, dy, dyup, part, dW, db, N, h, w, hy, wy, C, nb.value, 1)
         if direct:
+            from ..parallel.grad_reducer import notify_grad
+            notify_grad(weight, *([bias] if need_b else []))
             return dx, dy, None, None
         return dx, dy, dW, db
 

@@ -145,6 +145,30 @@ class FlatOptimizer:
     def zero_grad(self, set_to_none: bool = False) -> None:
         self.flat.zero_grad()
 
+    # parameters without a gradient ------------------------------------------
+    def set_active(self, active) -> None:
+        """``active``: per-param booleans (flat.params order).  torch.optim
+        skips a parameter whose ``.grad`` is None -- no weight decay, no
+        momentum -- so the update runs only over the flat ranges of params
+        that receive a gradient (usually all: one launch)."""
+        f = self.flat
+        if all(active):
+            self._ranges = None
+            return
+        segs = sorted((o, o + ((p.numel() + ALIGN - 1) // ALIGN) * ALIGN)
+                      for p, o, a in zip(f.params, f.offsets, active) if a)
+        ranges = []
+        for s_, e_ in segs:
+            if ranges and ranges[-1][1] == s_:
+                ranges[-1][1] = e_
+            else:
+                ranges.append([s_, e_])
+        self._ranges = [tuple(r) for r in ranges]
+
+    def _spans(self):
+        r = getattr(self, "_ranges", None)
+        return [(0, self.flat.numel)] if r is None else r
+
     # torch.optim-format state (checkpoint compatibility with the reference) --
     def _unflatten(self, buf: torch.Tensor):
         f = self.flat
@@ -187,16 +211,18 @@ class FlatSGD(FlatOptimizer):
         norm = None
         if self.grad_clip > 0:
             norm = self._grad_norm(g)
-        if self.use_hip:
-            _ext.call("mda_sgd_step", f.data, g, self.buf, self.lr_t, self.momentum,
-                      self.weight_decay, self.grad_scale, norm, self.grad_clip, f.numel)
-            return
-        s = self.grad_scale * self._clip_coef_torch()
-        d = g * s + self.weight_decay * f.data
-        if self.momentum != 0:
-            self.buf.mul_(self.momentum).add_(d)
-            d = self.buf
-        f.data.sub_(self.lr_t * d)
+        for a, b in self._spans():
+            p_, g_, m_ = f.data[a:b], g[a:b], self.buf[a:b]
+            if self.use_hip:
+                _ext.call("mda_sgd_step", p_, g_, m_, self.lr_t, self.momentum,
+                          self.weight_decay, self.grad_scale, norm, self.grad_clip, b - a)
+                continue
+            s = self.grad_scale * self._clip_coef_torch()
+            d = g_ * s + self.weight_decay * p_
+            if self.momentum != 0:
+                m_.mul_(self.momentum).add_(d)
+                d = m_
+            p_.sub_(self.lr_t * d)
 
     def state_dict(self):
         bufs = self._unflatten(self.buf)
@@ -227,25 +253,27 @@ class FlatAdam(FlatOptimizer):
         g = f.grads[0]
         norm = self._grad_norm(g) if self.grad_clip > 0 else None
         self.step_t.add_(1.0)
-        if self.use_hip:
-            _ext.call("mda_adam_step", f.data, g, self.m1, self.m2, self.lr_t, self.step_t,
-                      self.b1, self.b2, self.eps, self.weight_decay, int(self.decoupled),
-                      self.grad_scale, norm, self.grad_clip, f.numel)
-            return
-        s = self.grad_scale * self._clip_coef_torch()
-        gv = g * s
-        lr = self.lr_t
-        if self.decoupled:
-            f.data.mul_(1 - lr * self.weight_decay)
-        else:
-            gv = gv + self.weight_decay * f.data
-        self.m1.mul_(self.b1).add_((1 - self.b1) * gv)
-        self.m2.mul_(self.b2).add_((1 - self.b2) * gv * gv)
-        t = self.step_t
-        bc1 = 1 - torch.pow(torch.tensor(self.b1, device=t.device), t)
-        bc2 = 1 - torch.pow(torch.tensor(self.b2, device=t.device), t)
-        denom = self.m2.sqrt() / bc2.sqrt() + self.eps
-        f.data.sub_((lr / bc1) * self.m1 / denom)
+        for a, b in self._spans():
+            p_, g_, m1, m2 = f.data[a:b], g[a:b], self.m1[a:b], self.m2[a:b]
+            if self.use_hip:
+                _ext.call("mda_adam_step", p_, g_, m1, m2, self.lr_t, self.step_t,
+                          self.b1, self.b2, self.eps, self.weight_decay, int(self.decoupled),
+                          self.grad_scale, norm, self.grad_clip, b - a)
+                continue
+            s = self.grad_scale * self._clip_coef_torch()
+            gv = g_ * s
+            lr = self.lr_t
+            if self.decoupled:
+                p_.mul_(1 - lr * self.weight_decay)
+            else:
+                gv = gv + self.weight_decay * p_
+            m1.mul_(self.b1).add_((1 - self.b1) * gv)
+            m2.mul_(self.b2).add_((1 - self.b2) * gv * gv)
+            t = self.step_t
+            bc1 = 1 - torch.pow(torch.tensor(self.b1, device=t.device), t)
+            bc2 = 1 - torch.pow(torch.tensor(self.b2, device=t.device), t)
+            denom = m2.sqrt() / bc2.sqrt() + self.eps
+            p_.sub_((lr / bc1) * m1 / denom)
 
     def state_dict(self):
         m1, m2 = self._unflatten(self.m1), self._unflatten(self.m2)

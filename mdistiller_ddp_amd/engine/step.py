@@ -15,7 +15,9 @@ This is the hot loop of the reference (`engine/trainer.py:257-321` base,
   GPU a CIFAR distillation step is ~300-600 small kernels, so this removes
   the dominant (launch-bound) cost.  With world > 1 the collectives stay
   outside the captured graphs (forward/backward graph -> RCCL all-reduce ->
-  optimizer graph) so the RCCL path never depends on collective capture.
+  optimizer graph) unless ``DIST.GRAPH_COMM`` captures them: with RCCL the
+  bucketed all-reduces are recorded inside the single step graph, issued
+  from the backward hooks, so they overlap the remaining backward kernels.
 * **Flat parameters** (:mod:`.optim`) -> one all-reduce, one optimizer launch.
 * **DOT** runs its two backwards into the two halves of one ``[2, n]``
   gradient buffer and reduces both with one collective (fixes SURVEY D4).
@@ -31,14 +33,38 @@ from .optim import FlatParams, FlatDOT, build_optimizer
 
 
 def topk_rank(preds: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
-    """Number of classes scored strictly above the target class.
+    """Position of the target class in a stable descending sort of ``preds``.
 
-    ``rank < k`` is the top-k hit test; computed with one compare + row sum
+    Classes ranked before the target: strictly larger logits, plus equal
+    logits at a lower class index (the order ``topk`` returns ties in), so a
+    tie with the target -- common with bf16 logits -- is not a free hit.
+    ``rank < k`` is the top-k hit test; computed with compares + a row sum
     instead of ``topk`` (whose multi-block ROCm path is not capture-safe and
     needs a sort), so it lives inside the captured step.
     """
-    t = preds.gather(1, target.reshape(-1, 1))
-    return (preds > t).sum(1)
+    tgt = target.reshape(-1, 1)
+    t = preds.gather(1, tgt)
+    idx = torch.arange(preds.shape[1], device=preds.device).reshape(1, -1)
+    return ((preds > t) | ((preds == t) & (idx < tgt))).sum(1)
+
+
+def autograd_reachable(roots) -> set:
+    """ids of the leaf tensors whose AccumulateGrad node is reachable from
+    ``roots``' autograd graphs (a graph walk; nothing is computed)."""
+    out, seen = set(), set()
+    stack = [r.grad_fn for r in roots if r.grad_fn is not None]
+    while stack:
+        fn = stack.pop()
+        if fn is None or id(fn) in seen:
+            continue
+        seen.add(id(fn))
+        v = getattr(fn, "variable", None)
+        if v is not None:
+            out.add(id(v))
+        for nxt, _ in fn.next_functions:
+            if nxt is not None:
+                stack.append(nxt)
+    return out
 
 
 class DeviceMeters:
@@ -152,8 +178,14 @@ class TrainStep:
             torch.backends.cudnn.benchmark = True
         if self.world > 1 and getattr(distiller, "collective_in_forward", False):
             self.use_graph = False  # its collectives must not be captured
+        if self.world > 1 and bool(cfg.DIST.get("BROADCAST_INIT", True)):
+            # DDP's constructor broadcast (reference tools/train.py:86, site C2):
+            # every parameter and buffer of the distiller from rank 0
+            from ..parallel import broadcast_initial_state
+            broadcast_initial_state(distiller, self.flat)
+        self.graph_comm = self._graph_comm_mode(cfg)
         self.reducer = GradReducer(self.flat, bucket_mb=float(cfg.DIST.BUCKET_MB),
-                                   overlap=not self.use_graph, wire_dtype=cfg.DIST.GRAD_DTYPE)
+                                   overlap=True, wire_dtype=cfg.DIST.GRAD_DTYPE)
         self.epoch_t = torch.zeros((), dtype=torch.float32, device=self.device)
         self._epoch = None
         self.meters = None
@@ -162,8 +194,28 @@ class TrainStep:
         self._graphs = None
         self._static = None
         self._dot_ready = not self.is_dot
+        self._reach_ready = False
         self._units = {}
         self._packs = None
+
+    def _graph_comm_mode(self, cfg) -> bool:
+        """True: the gradient all-reduce is captured inside the step's hipGraph.
+
+        Only RCCL collectives are capturable (gloo reduces on the host), so
+        ``auto`` means capture exactly when the process group is RCCL.
+        """
+        if self.world <= 1 or not self.use_graph:
+            return False
+        mode = str(cfg.DIST.get("GRAPH_COMM", "auto")).lower()
+        import torch.distributed as dist
+        rccl = dist.get_backend() == "nccl"
+        if mode == "capture":
+            if not rccl:
+                raise ValueError("DIST.GRAPH_COMM=capture needs the RCCL (nccl) backend")
+            return True
+        if mode == "split":
+            return False
+        return rccl
 
     # ------------------------------------------------------------------
     def set_epoch(self, epoch: float) -> None:
@@ -204,10 +256,16 @@ class TrainStep:
     def _dot_reachability(self, losses):
         """Which params receive task / KD gradients (DOT's momentum branches)."""
         ps = self.flat.params
-        gt = torch.autograd.grad(losses["loss_ce"], ps, retain_graph=True, allow_unused=True)
-        gk = torch.autograd.grad(losses["loss_kd"], ps, retain_graph=True, allow_unused=True)
-        self.opt.set_reachability([g is not None for g in gt], [g is not None for g in gk])
+        rt = autograd_reachable([losses["loss_ce"]])
+        rk = autograd_reachable([losses["loss_kd"]])
+        self.opt.set_reachability([id(p) in rt for p in ps], [id(p) in rk for p in ps])
         self._dot_ready = True
+
+    def _grad_reachability(self, losses):
+        """Params no loss reaches get no update (torch.optim skips grad-None params)."""
+        r = autograd_reachable([v for v in losses.values() if v.requires_grad])
+        self.opt.set_active([id(p) in r for p in self.flat.params])
+        self._reach_ready = True
 
     def _fwd_bwd(self, b: dict, overlap_comm: bool):
         self.flat.zero_grad()
@@ -227,6 +285,8 @@ class TrainStep:
             if packs is not None:
                 packs.disarm()
                 hip_train.set_active_packs(None)
+        if not self.is_dot and not self._reach_ready:
+            self._grad_reachability(losses)
         if self.is_dot:
             if not self._dot_ready:
                 self._dot_reachability(losses)
@@ -292,6 +352,15 @@ class TrainStep:
                 preds, losses = self._fwd_bwd(static, overlap_comm=False)
                 self._update(preds, static["target"], losses)
             g2 = None
+        elif self.graph_comm:
+            # one graph: bucket all-reduces are issued from the backward hooks
+            # while the rest of backward is being captured, so the replayed
+            # DAG overlaps them with the remaining gradient kernels
+            with torch.cuda.graph(g1, pool=pool, stream=s):
+                preds, losses = self._fwd_bwd(static, overlap_comm=True)
+                self._reduce()
+                self._update(preds, static["target"], losses)
+            g2 = None
         else:
             with torch.cuda.graph(g1, pool=pool, stream=s):
                 preds, losses = self._fwd_bwd(static, overlap_comm=False)
@@ -304,6 +373,8 @@ class TrainStep:
 
     def step(self, batch: dict):
         """Run one step; returns device ``(preds, losses)`` (no host sync)."""
+        from ..ops.hip_layers import bump_weight_generation
+        bump_weight_generation()  # parameters / BN stats change: inference packs are stale
         b = self._prep(batch)
         if not self.use_graph or self.steps_done < self.warmup_eager:
             out = self._eager(b)
@@ -333,7 +404,7 @@ class TrainStep:
             static[k].copy_(v, non_blocking=True)
         g1, g2 = self._graphs
         g1.replay()
-        if g2 is not None:
+        if g2 is not None:  # split mode: eager all-reduce between the graphs
             self._reduce()
             g2.replay()
         self.steps_done += 1
@@ -349,4 +420,6 @@ class TrainStep:
         return self.opt.state_dict()
 
     def load_state_dict(self, sd: dict) -> None:
+        from ..ops.hip_layers import bump_weight_generation
+        bump_weight_generation()
         self.opt.load_state_dict(sd)

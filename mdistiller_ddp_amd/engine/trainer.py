@@ -186,12 +186,16 @@ class BaseTrainer:
                 continue
             if b.is_floating_point() or b.dtype in (torch.int64, torch.int32, torch.long):
                 dist.broadcast(b.data, 0)
+        from ..ops.hip_layers import bump_weight_generation
+        bump_weight_generation()
 
     def model_state(self):
         return OrderedDict(("module." + k, v) for k, v in self.distiller.state_dict().items())
 
     def load_model_state(self, sd):
+        from ..ops.hip_layers import bump_weight_generation
         self.distiller.load_state_dict(strip_module(sd))
+        bump_weight_generation()
 
     def save(self, epoch, is_best):
         state = {"epoch": epoch, "model": self.model_state(),

@@ -83,6 +83,7 @@ def validate(val_loader, distiller, device=None, dtype=None):
     from ..parallel import dist_fn
     from ..parallel.dist import is_master
     from .step import topk_rank
+    from ..ops.nn import fp32_head
     distiller.eval()
     if device is None:
         device = next(distiller.parameters()).device
@@ -100,7 +101,7 @@ def validate(val_loader, distiller, device=None, dtype=None):
         if device.type == "cuda":
             image = image.contiguous(memory_format=torch.channels_last)
         target = target.to(device, non_blocking=True)
-        with torch.autocast("cuda", dtype=dtype, enabled=amp):
+        with torch.autocast("cuda", dtype=dtype, enabled=amp), fp32_head():
             out = distiller(image=image)
         out = out.float()
         rank = topk_rank(out, target)

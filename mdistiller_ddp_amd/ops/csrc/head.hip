@@ -147,9 +147,20 @@ meters_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target, i
   // one thread per row: C independent loads, no cross-lane reduction chain
   for (int r = threadIdx.x; r < B; r += blockDim.x) {
     const int64_t base = (int64_t)r * C;
-    const float t = io<T>::ld(preds, base + target[r]);
+    const int tg = (int)target[r];
+    const float t = io<T>::ld(preds, base + tg);
+    // rank of the target = classes ordered before it by topk: strictly larger
+    // logits, plus EQUAL logits at a lower class index (ties are frequent with
+    // bf16 logits and must not count as hits)
     int c0 = 0, c1 = 0, c2 = 0, c3 = 0, c = 0;
-    for (; c + 4 <= C; c += 4) {
+    for (; c + 4 <= tg; c += 4) {
+      c0 += io<T>::ld(preds, base + c) >= t;
+      c1 += io<T>::ld(preds, base + c + 1) >= t;
+      c2 += io<T>::ld(preds, base + c + 2) >= t;
+      c3 += io<T>::ld(preds, base + c + 3) >= t;
+    }
+    for (; c < tg; ++c) c0 += io<T>::ld(preds, base + c) >= t;
+    for (c = tg + 1; c + 4 <= C; c += 4) {
       c0 += io<T>::ld(preds, base + c) > t;
       c1 += io<T>::ld(preds, base + c + 1) > t;
       c2 += io<T>::ld(preds, base + c + 2) > t;

@@ -58,8 +58,24 @@ def bn_supported(x, bn) -> bool:
     return False
 
 
+# Bumped by every training step (and checkpoint load): the native optimizer
+# and BN-statistics kernels write parameters / running stats through raw
+# pointers, which does not advance ``Tensor._version``, so the packed-weight
+# caches of TRAINABLE layers are keyed on this generation as well.  Frozen
+# layers (the teacher) keep their pack for the whole run.
+_GEN = [0]
+
+
+def bump_weight_generation() -> None:
+    _GEN[0] += 1
+
+
 def _version_key(conv, bn):
     key = [conv.weight._version, conv.weight.data_ptr()]
+    trainable = conv.weight.requires_grad or (
+        bn is not None and bn.weight is not None and bn.weight.requires_grad)
+    if trainable:
+        key.append(("gen", _GEN[0]))
     if conv.bias is not None:
         key += [conv.bias._version]
     if bn is not None:

@@ -25,6 +25,7 @@ import torch
 import torch.nn as nn
 
 from . import _ext
+from ..parallel.grad_reducer import notify_grad
 
 _ACT = {"none": 0, "relu": 1, "relu6": 2}
 
@@ -297,6 +298,10 @@ class _ConvBNActTrain(torch.autograd.Function):
             _ext.call("mda_conv_wgrad", x, dy, part, target, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
                       stride, pad, Kp, sp, 1.0, 1 if direct_w else 0)
             dw = None if direct_w else target
+            if direct_w:
+                notify_grad(weight)
+        if direct_gb:
+            notify_grad(gamma, beta)
         dgamma = None if direct_gb else sums[1].clone()
         dbeta = None if direct_gb else sums[0].clone()
         return dx, dw, dgamma, dbeta, dres, None, None, None
@@ -334,6 +339,7 @@ def _bn_train_backward(ctx, dout, dpre, y, res, stats, gamma, beta, M, C, act):
     _ext.call("mda_bn_bwd_apply", dout, dpre, y, res, stats[2], stats[3], stats[0], stats[1],
               sums, dy, dres, M, C, act)
     if direct_gb:
+        notify_grad(gamma, beta)
         return dy, dres, None, None
     return dy, dres, sums[1].clone(), sums[0].clone()
 
@@ -379,6 +385,8 @@ def _dw_backward(ctx, dout, dpre):
         _ext.call("mda_dw_wgrad", x, dy, part, target, N, H, W, C, Ho, Wo, 3, 3, stride, pad,
                   nblk, 1 if direct_w else 0)
         dw = None if direct_w else target
+        if direct_w:
+            notify_grad(weight)
     return dx, dw, dgamma, dbeta, dres, None, None, None
 
 

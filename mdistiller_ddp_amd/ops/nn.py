@@ -131,6 +131,9 @@ class _PoolFC(torch.autograd.Function):
         dx = torch.empty((N, C, H, W), dtype=dtype, device=dev, memory_format=torch.channels_last)
         _ext.call("mda_pool_fc_bwd", dt, dlogits, dpooled, pooled, weight.detach(), dw, db, dx, N,
                   H * W, C, J, 1)
+        if direct_w or direct_b:
+            from ..parallel.grad_reducer import notify_grad
+            notify_grad(*([weight] if direct_w else []), *([bias] if direct_b else []))
         return (dx, None if direct_w else dw, None if direct_b else db)
 
 
@@ -147,12 +150,42 @@ def _pool_fc_native(x: torch.Tensor, fc: nn.Linear, kernel) -> bool:
     return x.dtype == torch.float32 and not torch.is_autocast_enabled("cuda")
 
 
+_FP32_HEAD = {"on": False}
+
+
+class fp32_head:
+    """Context: classifier heads pool and project in fp32 (evaluation).
+
+    The reference evaluates in fp32; under the bf16 step the logits would be
+    bf16, whose coarse rounding creates top-k ties.  ``validate`` enables this
+    so the scored logits come from an fp32 pool + fp32 GEMM of the features.
+    """
+
+    def __enter__(self):
+        self._prev = _FP32_HEAD["on"]
+        _FP32_HEAD["on"] = True
+        return self
+
+    def __exit__(self, *exc):
+        _FP32_HEAD["on"] = self._prev
+        return False
+
+
 def pool_linear(x: torch.Tensor, fc: nn.Linear, kernel: int | None = None):
     """``avg = avg_pool2d(x, kernel).flatten(1); (avg, fc(avg))`` -- the CNN head.
 
     With a global pool (``kernel`` == spatial size, or None) on the GPU this is
     one fused HIP launch forward and one backward (:class:`_PoolFC`).
     """
+    if _FP32_HEAD["on"] and not torch.is_grad_enabled():
+        with torch.autocast(x.device.type, enabled=False):
+            xf = x.float()
+            if kernel is None:
+                avg = xf.mean(dim=(2, 3))
+            else:
+                avg = F.avg_pool2d(xf, kernel).reshape(x.size(0), -1)
+            return avg, F.linear(avg, fc.weight.float(),
+                                 fc.bias.float() if fc.bias is not None else None)
     if _pool_fc_native(x, fc, kernel):
         return _PoolFC.apply(x, fc.weight, fc.bias)
     if kernel is None:

@@ -16,7 +16,13 @@ distiller's learnable parameters only:
 * the 1/world averaging is NOT a separate pass: the optimizer kernel scales
   by ``grad_scale = 1/world`` while it reads the gradient anyway;
 * DOT's two gradient sets are reduced (the reference's DDP syncs only the
-  first backward).
+  first backward), honouring the bf16 wire format too.
+
+Under hipGraph capture with the RCCL backend (``TrainStep`` graph-comm
+mode) the same hooks fire inside the captured backward, so each bucket's
+all-reduce is recorded as a fork onto RCCL's stream that joins back before
+the optimizer node: the graph itself overlaps communication with the rest
+of backward, and a replay has no host round-trip at all.
 
 Bucket size: xGMI is point-to-point (7 links/GPU); RCCL's ring all-reduce of
 an S-byte bucket costs ~latency + 2(N-1)/N * S / link_bw per channel, so a
@@ -31,6 +37,19 @@ import torch.distributed as dist
 
 from .dist import is_dist, get_world_size
 
+_ARMED: list = []  # reducers currently expecting gradients
+
+
+def notify_grad(*params) -> None:
+    """Native backward kernels that accumulate straight into a parameter's
+    flat ``.grad`` view (returning ``None`` to autograd, so no accumulate
+    hook fires) report the write here, which lets the bucket holding the
+    parameter launch its all-reduce as soon as it is complete."""
+    if _ARMED:
+        for r in list(_ARMED):
+            for p in params:
+                r.ready_param(p)
+
 
 class GradReducer:
     def __init__(self, flat, bucket_mb: float = 8.0, overlap: bool = True, group=None,
@@ -43,6 +62,7 @@ class GradReducer:
         self.wire_bf16 = wire_dtype == "bf16"
         self.bytes_reduced = 0  # bytes put on the wire (tests / accounting)
         self.calls = 0
+        self.early_launches = 0  # buckets launched from inside backward (overlap)
         bucket_elems = max(64, int(bucket_mb * (1 << 20) / 4))
         # buckets aligned to parameter boundaries, in flat (= backward) order
         order = sorted(range(len(flat.params)), key=lambda i: flat.offsets[i])
@@ -65,7 +85,15 @@ class GradReducer:
         for b, (_, _, idx) in enumerate(self.buckets):
             for i in idx:
                 self._param_bucket[i] = b
+        self._index = {id(p): i for i, p in enumerate(flat.params)}
+        # gradient contributions per parameter and step, learned on the first
+        # armed step (a "calibration" backward that launches nothing early):
+        # autograd's accumulate hook and the native kernels that write straight
+        # into the flat buffer (notify_grad) both count
+        self._expected = None
+        self._calib = None
         self._pending = []
+        self._next = 0
         self._works = {}
         self._hooks = []
         self._armed = False
@@ -81,13 +109,27 @@ class GradReducer:
     # ------------------------------------------------------------------
     def _make_hook(self, i):
         def hook(_p):
-            if not self._armed:
-                return
-            b = self._param_bucket[i]
-            self._pending[b] -= 1
-            if self._pending[b] == 0:
-                self._launch(b, async_op=True)
+            if self._armed:
+                self._ready(i)
         return hook
+
+    def _ready(self, i):
+        if self._calib is not None:
+            self._calib[i] += 1
+            return
+        b = self._param_bucket[i]
+        self._pending[b] -= 1
+        # strictly in bucket order: every rank issues the same collective
+        # sequence even if two buckets complete in a different order
+        while self._next < len(self.buckets) and self._pending[self._next] <= 0:
+            self._launch(self._next, async_op=True)
+            self._next += 1
+            self.early_launches += 1
+
+    def ready_param(self, p) -> None:
+        i = self._index.get(id(p))
+        if i is not None and self._armed:
+            self._ready(i)
 
     def _slice(self, b):
         s, e, _ = self.buckets[b]
@@ -109,14 +151,23 @@ class GradReducer:
         """Call before a backward whose gradients should be reduced on the fly."""
         if not self.enabled:
             return
-        self._pending = [len(idx) for (_, _, idx) in self.buckets]
         self._works = {}
+        self._next = 0
         self._armed = self.overlap
+        if not self._armed:
+            return
+        if self._expected is None:
+            self._calib = [0] * len(self.flat.params)
+        else:
+            self._pending = [sum(self._expected[i] for i in idx) for (_, _, idx) in self.buckets]
+        _ARMED.append(self)
 
     def finish(self) -> None:
         """Launch any bucket not yet launched and wait for all of them."""
         if not self.enabled:
             return
+        if self._calib is not None:
+            self._expected, self._calib = self._calib, None
         for b in range(len(self.buckets)):
             if b not in self._works:
                 self._launch(b, async_op=True)
@@ -127,6 +178,8 @@ class GradReducer:
                 t.copy_(tb)
         self._works = {}
         self._armed = False
+        if self in _ARMED:
+            _ARMED.remove(self)
 
     def reduce_all(self) -> None:
         """Non-overlapped reduction of the currently bound gradient set."""
@@ -145,9 +198,14 @@ class GradReducer:
             t = g.view(-1)
         else:
             t = g[sets[0]]
-        self.bytes_reduced += t.numel() * 4
+        self.bytes_reduced += t.numel() * (2 if self.wire_bf16 else 4)
         self.calls += 1
-        dist.all_reduce(t, group=self.group)
+        if self.wire_bf16:
+            tb = t.to(torch.bfloat16)
+            dist.all_reduce(tb, group=self.group)
+            t.copy_(tb)
+        else:
+            dist.all_reduce(t, group=self.group)
 
     def remove_hooks(self) -> None:
         for h in self._hooks:

@@ -8,6 +8,8 @@ D10, D15) plus plain DP correctness:
 * DOT reduces BOTH gradient sets;
 * CRD memory banks stay identical across ranks;
 * global rank is RANK, not LOCAL_RANK (multi-node simulation);
+* ranks seeded differently start identical (rank-0 broadcast, DDP's C2);
+* gradient buckets launch from inside backward (overlap) after calibration;
 * BN buffer sync before eval reproduces DDP's broadcast_buffers semantics.
 """
 import os
@@ -25,6 +27,12 @@ def _free_port():
     p = s.getsockname()[1]
     s.close()
     return p
+
+
+def _all_equal(dist, world, t):
+    allt = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(allt, t.contiguous())
+    return all(torch.equal(allt[0], a) for a in allt)
 
 
 def _worker(rank, world, port, scenario, outdir, local_rank_offset):
@@ -53,11 +61,18 @@ def _worker(rank, world, port, scenario, outdir, local_rank_offset):
     cfg.CRD.FEAT.STUDENT_DIM = 64
     cfg.CRD.FEAT.TEACHER_DIM = 64
     cfg.DIST.BUCKET_MB = 0.05  # several buckets even for a tiny student
-    torch.manual_seed(0)  # identical init on every rank
+    # DIFFERENT init on every rank: TrainStep's rank-0 broadcast (DDP's C2)
+    # must make the replicas identical anyway
+    torch.manual_seed(100 + rank)
     d = build_distiller(cfg, 100, "cpu", num_data=200)
     d.train()
     keys = ("image", "target", "index", "contrastive_index") if typ == "CRD" else ("image", "target")
     st = TrainStep(d, cfg, "cpu", trainer=trainer, dtype=torch.float32, batch_keys=keys)
+    from mdistiller_ddp_amd.parallel import state_checksum
+    c0 = state_checksum(d, st.flat, buffers=True)
+    g0 = [torch.empty_like(c0) for _ in range(world)]
+    dist.all_gather(g0, c0)
+    init_equal = all(torch.equal(g0[0], g) for g in g0)
     st.set_epoch(1.0)
     # different data per rank
     ld = SyntheticLoader("cifar100", 8, "cpu", steps_per_epoch=3, crd_k=32, num_data=200, seed=rank)
@@ -72,6 +87,9 @@ def _worker(rank, world, port, scenario, outdir, local_rank_offset):
     gathered = [torch.empty_like(flat) for _ in range(world)]
     dist.all_gather(gathered, flat)
     out = {"params_equal": all(torch.equal(gathered[0], g) for g in gathered),
+           "init_equal": init_equal, "early": st.reducer.early_launches,
+           "teacher_equal": _all_equal(dist, world, torch.cat(
+               [p.detach().reshape(-1) for p in d.teacher.parameters()])),
            "bytes": st.reducer.bytes_reduced, "calls": st.reducer.calls,
            "student_bytes": 4 * sum(p.numel() for p in d.get_learnable_parameters()),
            "flat_bytes": 4 * st.flat.numel * st.flat.num_grad_sets}
@@ -114,8 +132,13 @@ def _spawn(scenario, world=2, local_rank_offset=0):
 def test_dp_replicas_identical(scenario):
     res = _spawn(scenario)
     for r in res:
+        assert r["init_equal"]  # rank-0 broadcast at construction (C2)
+        assert r["teacher_equal"]
         assert r["params_equal"]
         assert r["bn_equal"]
+    # buckets launched from inside backward once the per-param gradient
+    # counts are calibrated (step 1): steps 2 and 3 overlap comm with backward
+    assert res[0]["early"] > 0
     r = res[0]
     # only student grads on the wire: 3 steps x flat buffer (+ the explicit reduce)
     assert r["bytes"] <= 4 * r["flat_bytes"]
@@ -136,6 +159,7 @@ def test_dp_dot_reduces_both_grad_sets():
 def test_dp_crd_memory_consistent():
     res = _spawn("crd")
     for r in res:
+        assert r["init_equal"]  # incl. both memory banks, broadcast at construction
         assert r["params_equal"]
         assert r["memory_equal"]
 
@@ -144,3 +168,35 @@ def test_global_rank_is_rank_not_local_rank():
     # simulate a second node: LOCAL_RANK differs from RANK
     res = _spawn("base", local_rank_offset=1)
     assert all(r["params_equal"] for r in res)
+
+
+def test_bench_self_launch_two_ranks_cpu():
+    """``python bench.py --gpus 2`` launches 2 ranks itself and reports n_gpus 2."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    env.pop("WORLD_SIZE", None)
+    for scaling, want_global in (("weak", 8), ("strong", 4)):
+        out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                              "--steps", "1", "--warmup", "1", "--batch", "4", "--global-batch", "4",
+                              "--scaling", scaling, "DISTILLER.STUDENT", "resnet8",
+                              "DISTILLER.TEACHER", "resnet20"],
+                             capture_output=True, text=True, timeout=600, env=env, cwd=root)
+        assert out.returncode == 0, out.stderr[-3000:]
+        line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1]
+        r = json.loads(line)
+        assert r["n_gpus"] == 2 and r["scaling"] == scaling
+        assert r["config"]["global_batch"] == want_global
+        assert r["replicas_identical"] is True
+
+
+def test_bench_refuses_mismatched_world():
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1")
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"],
+                         capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert out.returncode != 0 and "WORLD_SIZE" in (out.stderr + out.stdout)

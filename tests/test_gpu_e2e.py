@@ -84,3 +84,66 @@ def test_trainer_epoch_loop_gpu(tmp_path):
     t = trainer_dict["base"]("gpu_e2e", d, tr, va, cfg, device=torch.device("cuda"))
     t.train()
     assert (tmp_path / "gpu_e2e" / "latest").exists()
+    import yaml
+    log = yaml.safe_load((tmp_path / "gpu_e2e" / "worklog.yaml").read_text())
+    assert [e["epoch"] for e in log] == [1, 2]
+    for e in log:
+        assert 0.0 <= e["test_acc"] <= 100.0 and e["test_acc_top5"] >= e["test_acc"]
+        assert 0.0 < e["test_loss"] < 50.0
+        assert all(v == v for v in e["train_loss"].values())
+    # the two epochs evaluate different weights
+    assert log[0]["test_loss"] != log[1]["test_loss"]
+
+
+def test_validation_sees_updated_weights(tmp_path):
+    """Epoch-2 validation on the native (BN-folded, packed) path must score the
+    CURRENT weights: it equals the PyTorch-backend evaluation of the same state
+    and differs from epoch 1 (the packed-weight cache once went stale)."""
+    from mdistiller_ddp_amd.engine import trainer_dict
+    from mdistiller_ddp_amd.engine.utils import validate
+    from mdistiller_ddp_amd.data import get_dataset
+    from mdistiller_ddp_amd.ops.backend import use_backend
+    cfg = _cfg("KD")
+    cfg.DATASET.SYNTHETIC = True
+    cfg.DATASET.SYNTHETIC_SIZE = 512
+    cfg.SOLVER.EPOCHS = 2
+    cfg.SOLVER.LR = 0.2  # move the weights a lot in one epoch
+    cfg.LOG.PREFIX = str(tmp_path)
+    cfg.freeze()
+    tr, va, n, nc = get_dataset(cfg, torch.device("cuda"))
+    torch.manual_seed(0)
+    d = build_distiller(cfg, nc, "cuda", n)
+    t = trainer_dict["base"]("val_fresh", d, tr, va, cfg, device=torch.device("cuda"))
+    dev = torch.device("cuda")
+    t.train_epoch(1)
+    v1 = validate(va, d, dev, torch.bfloat16)
+    t.train_epoch(2)
+    v2 = validate(va, d, dev, torch.bfloat16)
+    with use_backend("torch"):
+        v2_ref = validate(va, d, dev, torch.float32)
+    assert abs(v1[2] - v2[2]) > 1e-3, (v1, v2)
+    assert abs(v2[2] - v2_ref[2]) / v2_ref[2] < 2e-2, (v2, v2_ref)
+    assert abs(v2[0] - v2_ref[0]) <= 3.0, (v2, v2_ref)
+
+
+@pytest.mark.parametrize("trainer", ["base", "dot"])
+def test_native_bf16_graph_matches_eager(trainer):
+    """20 steps of the NATIVE bf16 path (HIP conv/BN/loss/optimizer kernels):
+    hipGraph replay vs eager launches of the same kernels."""
+    torch.manual_seed(0)
+    cfg = _cfg("DKD" if trainer == "base" else "KD", trainer)
+    d1 = build_distiller(cfg, 100, "cuda")
+    d2 = copy.deepcopy(d1)
+    outs = []
+    for d, g in ((d1, True), (d2, False)):
+        d.train()
+        st = TrainStep(d, cfg, "cuda", trainer=trainer, use_graph=g, dtype=torch.bfloat16)
+        st.set_epoch(30.0)
+        ld = SyntheticLoader("cifar100", 64, "cuda", steps_per_epoch=20, channels_last=True)
+        for b in ld:
+            st.step(b)
+        torch.cuda.synchronize()
+        assert (st._graphs is not None) == g
+        outs.append(st.flat.data.clone())
+    rel = (outs[0] - outs[1]).norm() / outs[1].norm()
+    assert rel < 1e-2, rel

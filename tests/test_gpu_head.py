@@ -56,14 +56,17 @@ def test_pool_linear_accumulates_into_bound_grad():
                                atol=2e-2, rtol=1e-2)
 
 
+@pytest.mark.parametrize("ties", [False, True])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_meters_kernel(dtype):
+def test_meters_kernel(dtype, ties):
     from mdistiller_ddp_amd.engine.step import DeviceMeters
     torch.manual_seed(2)
     keys = ["loss_ce", "loss_kd"]
     m_h, m_r = DeviceMeters(DEV, keys), DeviceMeters(DEV, keys)
     for _ in range(3):
         preds = torch.randn(64, 100, device=DEV).to(dtype)
+        if ties:  # heavy ties with the target logit: stable-order rank, not a free hit
+            preds = torch.randint(0, 3, (64, 100), device=DEV).to(dtype)
         target = torch.randint(0, 100, (64,), device=DEV)
         losses = {"loss_ce": torch.rand((), device=DEV), "loss_kd": torch.rand((), device=DEV)}
         with use_backend("hip"):

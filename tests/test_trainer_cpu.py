@@ -147,3 +147,14 @@ def test_cli_train_and_auto_resume(tmp_path):
                        capture_output=True, text=True, env=env, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     assert "resumed from" in r.stdout and "at epoch 3" in r.stdout
+
+
+def test_topk_rank_breaks_ties_like_stable_sort():
+    import torch
+    from mdistiller_ddp_amd.engine.step import topk_rank
+    g = torch.Generator().manual_seed(0)
+    preds = torch.randint(0, 4, (256, 20), generator=g).float()
+    target = torch.randint(0, 20, (256,), generator=g)
+    order = torch.argsort(-preds, dim=1, stable=True)
+    want = (order == target.reshape(-1, 1)).float().argmax(1)
+    assert torch.equal(topk_rank(preds, target), want)

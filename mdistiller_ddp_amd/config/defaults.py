@@ -83,7 +83,9 @@ CFG.RUNTIME.DTYPE = "bf16"           # bf16 | fp32           (compute dtype on G
 CFG.RUNTIME.HIP_GRAPH = True         # capture fwd+bwd+step into a hipGraph
 CFG.RUNTIME.TEACHER_STREAM = True    # teacher forward on its own HIP stream
 CFG.RUNTIME.FOLD_TEACHER_BN = True   # fold frozen teacher BN into conv weights
-CFG.RUNTIME.PROFILE = False          # torch.profiler trace of a few steps
+CFG.RUNTIME.PROFILE = False          # torch.profiler trace + hipEvent step times of a window
+CFG.RUNTIME.PROFILE_START = 20       #   first profiled iteration of epoch 1
+CFG.RUNTIME.PROFILE_STEPS = 10       #   window length
 CFG.RUNTIME.MAX_ITERS_PER_EPOCH = 0  # >0: truncate epochs (smoke / CI)
 CFG.RUNTIME.FAULT_INJECT = ""        # "rank:step" -> raise on that rank at that step (tests)
 CFG.RUNTIME.CHECK_REPLICAS = 0       # >0: every N steps assert param checksums equal across ranks
@@ -94,7 +96,7 @@ CFG.DIST.BACKEND = "auto"            # auto -> nccl(RCCL) on GPU, gloo on CPU
 CFG.DIST.BUCKET_MB = 8.0             # gradient bucket size (MB of fp32)
 CFG.DIST.TIMEOUT_S = 600
 CFG.DIST.GRAD_DTYPE = "fp32"         # fp32 | bf16 wire format for gradient all-reduce
-CFG.DIST.GRAPH_COMM = "auto"         # capture | split | auto: all-reduce inside the step's
+CFG.DIST.GRAPH_COMM = "auto"         # capture | split | auto(=split): all-reduce inside the step's
                                      # hipGraph (RCCL, overlapped with backward) or between two graphs
 CFG.DIST.BROADCAST_INIT = True       # rank-0 broadcast of all params/buffers at step construction (C2)
 

@@ -201,8 +201,12 @@ class TrainStep:
     def _graph_comm_mode(self, cfg) -> bool:
         """True: the gradient all-reduce is captured inside the step's hipGraph.
 
-        Only RCCL collectives are capturable (gloo reduces on the host), so
-        ``auto`` means capture exactly when the process group is RCCL.
+        Only RCCL collectives are capturable (gloo reduces on the host).
+        ``auto`` = ``split``: RCCL rejects two ranks on one device, so the
+        single-GPU test box cannot exercise captured multi-rank collectives;
+        the split path (fwd+bwd graph -> eager async RCCL all-reduce -> optimizer
+        graph, no host synchronisation) is the one covered by the 2-rank GPU
+        test.  ``capture`` opts into the single graph.
         """
         if self.world <= 1 or not self.use_graph:
             return False
@@ -213,9 +217,7 @@ class TrainStep:
             if not rccl:
                 raise ValueError("DIST.GRAPH_COMM=capture needs the RCCL (nccl) backend")
             return True
-        if mode == "split":
-            return False
-        return rccl
+        return False  # split / auto
 
     # ------------------------------------------------------------------
     def set_epoch(self, epoch: float) -> None:

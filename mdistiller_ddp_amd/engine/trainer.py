@@ -80,6 +80,10 @@ class BaseTrainer:
         if cfg.EXPERIMENT.AMP and self.device.type == "cuda":
             dtype = torch.bfloat16  # reference AMP = fp16 autocast + GradScaler; bf16 needs no scaler
         self.dtype = dtype
+        from ..runtime import streams
+        from ..ops.hip_layers import set_fold_bn
+        streams.set_enabled(bool(cfg.RUNTIME.TEACHER_STREAM))
+        set_fold_bn(bool(cfg.RUNTIME.FOLD_TEACHER_BN))
         self.step = TrainStep(distiller, cfg, self.device, trainer=self.kind,
                               use_graph=bool(cfg.RUNTIME.HIP_GRAPH), dtype=dtype,
                               batch_keys=BATCH_KEYS[self.kind])
@@ -268,12 +272,17 @@ class BaseTrainer:
         freq = max(1, int(cfg.LOG.METRIC_FREQ))
         t0 = time.perf_counter()
         lr = cfg.SOLVER.LR
+        prof = StepProfiler(cfg, self.log_path, self.device) if epoch == 1 else None
         for idx, data in enumerate(self.train_loader):
             if idx >= max_iter:
                 break
             lr = adjust_learning_rate(epoch, idx, cfg, n_iter)
             self.step.set_lr(lr)
+            if prof is not None:
+                prof.before(idx)
             self.step.step(_as_batch(data, BATCH_KEYS[self.kind]))
+            if prof is not None:
+                prof.after(idx)
             self.global_step += 1
             if self._fault is not None and self._fault == (get_rank(), self.global_step):
                 raise RuntimeError(f"injected fault on rank {get_rank()} at step {self.global_step}")
@@ -289,6 +298,8 @@ class BaseTrainer:
                         epoch, dt, m["loss"], m["top1"], m["top5"]), "TRAIN"))
         if pbar is not None:
             pbar.close()
+        if prof is not None:
+            prof.close()
         train_m = self.step.meters.summary(reduce=True)
         self.sync_buffers()
         test_acc, test_acc_top5, test_loss = validate(self.val_loader, self.distiller, self.device,
@@ -310,6 +321,85 @@ class BaseTrainer:
             t = torch.tensor([self.best_acc], dtype=torch.float64, device=self.device)
             dist.broadcast(t, 0)
             self.best_acc = float(t.item())
+
+
+class StepProfiler:
+    """``RUNTIME.PROFILE``: in-framework profiling of a window of
+    training steps of the first epoch.
+
+    * hipEvent-bracketed device time of every step in the window (the wall
+      between events recorded on the step's stream before and after it) ->
+      ``<log>/step_times_rank<r>.txt``, read once at the end (no per-step sync);
+    * a ``torch.profiler`` trace of the same window (CPU + ROCm kernel activity)
+      -> ``<log>/profile_rank<r>.json`` (chrome trace) plus the kernel table
+      ``<log>/profile_rank<r>.txt``.
+
+    Window: ``RUNTIME.PROFILE_START`` .. ``+ RUNTIME.PROFILE_STEPS``.  Kernel
+    names are stable (``mda_*`` exports, named HIP kernels), so the table lines
+    up with ``rocprofv3 --kernel-trace --stats`` summaries.
+    """
+
+    def __init__(self, cfg, log_path, device):
+        self.on = bool(cfg.RUNTIME.PROFILE)
+        self.start = int(cfg.RUNTIME.PROFILE_START)
+        self.stop = self.start + int(cfg.RUNTIME.PROFILE_STEPS)
+        self.log_path = log_path
+        self.cuda = device.type == "cuda"
+        self.events = []
+        self.prof = None
+        self.rank = get_rank()
+
+    def before(self, idx):
+        if not self.on or not (self.start <= idx < self.stop):
+            return
+        if idx == self.start:
+            from torch.profiler import profile, ProfilerActivity
+            acts = [ProfilerActivity.CPU] + ([ProfilerActivity.CUDA] if self.cuda else [])
+            self.prof = profile(activities=acts, record_shapes=False)
+            self.prof.__enter__()
+        if self.cuda:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            self.events.append([e, None])
+        else:
+            self.events.append([time.perf_counter(), None])
+
+    def after(self, idx):
+        if not self.on or not (self.start <= idx < self.stop):
+            return
+        if self.cuda:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            self.events[-1][1] = e
+        else:
+            self.events[-1][1] = time.perf_counter()
+        if idx == self.stop - 1:
+            self.close()
+
+    def close(self):
+        if not self.on or (self.prof is None and not self.events):
+            return
+        if self.cuda:
+            torch.cuda.synchronize()
+            ms = [a.elapsed_time(b) for a, b in self.events if b is not None]
+        else:
+            ms = [1000.0 * (b - a) for a, b in self.events if b is not None]
+        os.makedirs(self.log_path, exist_ok=True)
+        with open(os.path.join(self.log_path, f"step_times_rank{self.rank}.txt"), "w") as f:
+            for i, v in enumerate(ms):
+                f.write(f"{self.start + i}\t{v:.4f}\n")
+            if ms:
+                f.write(f"# mean_ms\t{sum(ms) / len(ms):.4f}\n")
+        if self.prof is not None:
+            self.prof.__exit__(None, None, None)
+            base = os.path.join(self.log_path, f"profile_rank{self.rank}")
+            self.prof.export_chrome_trace(base + ".json")
+            key = "self_cuda_time_total" if self.cuda else "self_cpu_time_total"
+            with open(base + ".txt", "w") as f:
+                f.write(self.prof.key_averages().table(sort_by=key, row_limit=60))
+        self.prof = None
+        self.events = []
+        self.on = False
 
 
 class CRDTrainer(BaseTrainer):

@@ -32,8 +32,20 @@ def _needs_grad(x, conv, bn) -> bool:
     return False
 
 
+# RUNTIME.FOLD_TEACHER_BN: fold frozen BN into the packed conv weights (one
+# launch per teacher layer).  Off = conv kernel without BN, then PyTorch BN
+# (A/B and debugging only).
+_FOLD = {"on": True}
+
+
+def set_fold_bn(flag: bool) -> None:
+    _FOLD["on"] = bool(flag)
+
+
 def conv_supported(x, conv, bn) -> bool:
     if not (x.is_cuda and x.dim() == 4 and isinstance(conv, nn.Conv2d)):
+        return False
+    if bn is not None and not _FOLD["on"]:
         return False
     if conv.groups != 1:
         from .hip_train import dw_supported_geometry

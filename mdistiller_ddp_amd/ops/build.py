@@ -140,6 +140,28 @@ def build(kind: str = "all", verbose: bool = False, jobs: int | None = None) -> 
     return built
 
 
+SAN_FLAGS = ["-O1", "-g", "-fno-omit-frame-pointer", "-std=c++17", "-fopenmp",
+             "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined", f"-I{CSRC}"]
+
+
+def build_host_sanitized(out_dir: str | None = None) -> str:
+    """Build ``csrc/host/*.cpp`` + ``csrc/host/selftest/host_selftest.cpp``
+    into ONE executable under AddressSanitizer + UBSan.  CPU only:
+    GPU sanitizers are not available on the MI355X pool.  Returns its path;
+    running it exits 0 when every invariant held and no sanitizer fired."""
+    out_dir = out_dir or os.path.join(LIBDIR, "san")
+    os.makedirs(out_dir, exist_ok=True)
+    exe = os.path.join(out_dir, "host_selftest_asan")
+    srcs = _sources("host") + [os.path.join(CSRC, "host", "selftest", "host_selftest.cpp")]
+    cc = shutil.which("g++") or "g++"
+    _run([cc] + SAN_FLAGS + srcs + ["-o", exe])
+    return exe
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "asan":
+        exe = build_host_sanitized()
+        r = subprocess.run([exe])
+        sys.exit(r.returncode)
     out = build(sys.argv[1] if len(sys.argv) > 1 else "all", verbose=True)
     print("up to date" if not out else "\n".join(out))

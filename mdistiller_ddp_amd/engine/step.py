@@ -52,12 +52,14 @@ def autograd_reachable(roots) -> set:
     """ids of the leaf tensors whose AccumulateGrad node is reachable from
     ``roots``' autograd graphs (a graph walk; nothing is computed)."""
     out, seen = set(), set()
+    keep = []  # hold every visited node wrapper: a freed wrapper's id() gets reused
     stack = [r.grad_fn for r in roots if r.grad_fn is not None]
     while stack:
         fn = stack.pop()
         if fn is None or id(fn) in seen:
             continue
         seen.add(id(fn))
+        keep.append(fn)
         v = getattr(fn, "variable", None)
         if v is not None:
             out.add(id(v))

@@ -40,11 +40,17 @@ def test_distiller_graph_steps(typ):
     st.set_epoch(1.0)
     ld = SyntheticLoader("cifar100", 32, "cuda", steps_per_epoch=8, crd_k=cfg.CRD.NCE.K,
                          num_data=2000, channels_last=True)
+    before = [p.detach().clone() for p in st.flat.params]
     for b in ld:
         preds, losses = st.step(b)
     torch.cuda.synchronize()
     m = st.meters.summary(reduce=False)
     assert all(v == v and abs(v) < 1e6 for v in m.values()), m
+    # the optimizer really stepped: every student weight moved
+    names = {id(p): n for n, p in d.named_parameters()}
+    stuck = [names[id(p)] for p, b0 in zip(st.flat.params, before)
+             if names[id(p)].startswith("student.") and torch.equal(p.detach(), b0)]
+    assert not stuck, stuck
 
 
 @pytest.mark.parametrize("trainer", ["base", "dot"])

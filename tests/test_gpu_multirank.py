@@ -63,6 +63,7 @@ def _worker(rank, world, port, scenario, outdir):
     dist.all_gather(allc, c0)
     out = {"init_equal": all(torch.equal(allc[0], a) for a in allc)}
     st.set_epoch(1.0)
+    init = st.flat.data.clone()
     ld = SyntheticLoader("cifar100", 32, dev, steps_per_epoch=20, channels_last=True, seed=rank)
     for b in ld:
         st.step(b)
@@ -74,6 +75,7 @@ def _worker(rank, world, port, scenario, outdir):
     dist.all_gather(allf, flat)
     out["params_equal"] = all(torch.equal(allf[0], a) for a in allf)
     out["finite"] = bool(torch.isfinite(flat).all())
+    out["moved"] = float((flat - init).norm() / init.norm())
     m = st.meters.summary(reduce=True)
     out["loss"] = m["loss"]
     if scenario == "dkd":
@@ -109,6 +111,7 @@ def test_two_ranks_one_gpu_graph_replicas(scenario):
         assert r["graph"] and r["split"], r
         assert r["params_equal"], r
         assert r["finite"], r
+        assert r["moved"] > 1e-4, r  # the optimizer really stepped
         assert r["loss"] == r["loss"] and abs(r["loss"]) < 1e6
     if scenario == "dkd":
         assert res[0]["grad_rel"] < 1e-5, res[0]

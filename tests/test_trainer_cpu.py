@@ -158,3 +158,37 @@ def test_topk_rank_breaks_ties_like_stable_sort():
     order = torch.argsort(-preds, dim=1, stable=True)
     want = (order == target.reshape(-1, 1)).float().argmax(1)
     assert torch.equal(topk_rank(preds, target), want)
+
+
+import pytest
+
+
+@pytest.mark.parametrize("trainer,typ", [("base", "DKD"), ("dot", "KD"), ("base", "REVIEWKD")])
+def test_every_learnable_param_is_updated(trainer, typ):
+    """Every parameter that a loss reaches moves after a step (the reachability
+    walk that skips grad-less params must find all of them)."""
+    import torch
+    from mdistiller_ddp_amd.config import get_cfg
+    from mdistiller_ddp_amd.engine.build import build_distiller
+    from mdistiller_ddp_amd.engine.step import TrainStep, autograd_reachable
+    from mdistiller_ddp_amd.data.synthetic import SyntheticLoader
+    cfg = get_cfg()
+    cfg.DISTILLER.TYPE = typ
+    cfg.DISTILLER.TEACHER = "resnet20"
+    cfg.DISTILLER.STUDENT = "resnet8"
+    cfg.DISTILLER.RANDOM_TEACHER = True
+    cfg.SOLVER.TRAINER = trainer
+    if typ == "REVIEWKD":
+        cfg.REVIEWKD.IN_CHANNELS = [16, 32, 64, 64]
+        cfg.REVIEWKD.OUT_CHANNELS = [16, 32, 64, 64]
+    torch.manual_seed(0)
+    d = build_distiller(cfg, 100, "cpu")
+    d.train()
+    st = TrainStep(d, cfg, "cpu", trainer=trainer)
+    st.set_epoch(5.0)
+    before = [p.detach().clone() for p in st.flat.params]
+    for b in SyntheticLoader("cifar100", 8, "cpu", steps_per_epoch=2):
+        st.step(b)
+    names = {id(p): n for n, p in d.named_parameters()}
+    stuck = [names[id(p)] for p, b0 in zip(st.flat.params, before) if torch.equal(p.detach(), b0)]
+    assert not stuck, stuck

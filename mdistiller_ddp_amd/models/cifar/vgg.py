@@ -12,6 +12,7 @@ import math
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ...ops.nn import MaxPool2d
 from .._base import ModelBase
 from .._seq import run_seq
 
@@ -35,10 +36,10 @@ class VGG(nn.Module, ModelBase):
         self.block2 = self._make_layers(cfg[2], batch_norm, cfg[1][-1])
         self.block3 = self._make_layers(cfg[3], batch_norm, cfg[2][-1])
         self.block4 = self._make_layers(cfg[4], batch_norm, cfg[3][-1])
-        self.pool0 = nn.MaxPool2d(kernel_size=2, stride=2)
-        self.pool1 = nn.MaxPool2d(kernel_size=2, stride=2)
-        self.pool2 = nn.MaxPool2d(kernel_size=2, stride=2)
-        self.pool3 = nn.MaxPool2d(kernel_size=2, stride=2)
+        self.pool0 = MaxPool2d(kernel_size=2, stride=2)
+        self.pool1 = MaxPool2d(kernel_size=2, stride=2)
+        self.pool2 = MaxPool2d(kernel_size=2, stride=2)
+        self.pool3 = MaxPool2d(kernel_size=2, stride=2)
         self.pool4 = nn.AdaptiveAvgPool2d((1, 1))
         self.classifier = nn.Linear(512, num_classes)
         self._initialize_weights()
@@ -81,7 +82,7 @@ class VGG(nn.Module, ModelBase):
         layers = []
         for v in cfg:
             if v == "M":
-                layers += [nn.MaxPool2d(kernel_size=2, stride=2)]
+                layers += [MaxPool2d(kernel_size=2, stride=2)]
             else:
                 conv2d = nn.Conv2d(in_channels, v, kernel_size=3, padding=1)
                 layers += [conv2d, nn.BatchNorm2d(v), nn.ReLU(inplace=True)] if batch_norm \

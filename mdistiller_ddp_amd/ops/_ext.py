@@ -37,10 +37,16 @@ SIGNATURES = {
     "mda_conv_fwd": "pppppppp" + "i" * 15 + "s",
     "mda_conv_plan": "iiipp",
     "mda_conv_dgrad": "pppp" + "i" * 14 + "s",
-    "mda_conv_wgrad": "pppp" + "i" * 13 + "fis",
+    "mda_conv_wgrad": "pppp" + "i" * 13 + "fiis",
+    "mda_pad_channels": "ippiiis",
+    # max pooling (csrc/pool.hip)
+    "mda_maxpool_fwd": "ppp" + "i" * 9 + "s",
+    "mda_maxpool_bwd": "ppp" + "i" * 9 + "s",
+    "mda_pack_conv_weights_pad": "pp" + "i" * 6 + "s",
     "mda_wgrad_plan": "iiip",
     "mda_pack_conv_weights": "ppp" + "i" * 6 + "s",
     "mda_pack_conv_weights_multi": "piis",
+    "mda_pack_tiles": "iiiip",
     # depthwise 3x3 conv (csrc/dwconv.hip)
     "mda_dw_pack": "pppiis",
     "mda_dw_fwd": "ppppppp" + "i" * 11 + "s",

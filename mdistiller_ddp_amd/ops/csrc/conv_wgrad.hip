@@ -232,7 +232,8 @@ conv_wgrad_kernel(const WgParams p) {
 // coalesced; the OIHW write is the only scattered access.
 __global__ void __launch_bounds__(256)
 wgrad_reduce_kernel(const float* __restrict__ partial, float* __restrict__ grad, int splits,
-                    int Cout, int Cin, int KH, int KW, int Kp, float scale, int accumulate) {
+                    int Cout, int Cin, int KH, int KW, int Kp, float scale, int accumulate,
+                    int cin_keep) {
   const int K = Cin * KH * KW;
   const int64_t total = (int64_t)Cout * K;
   const int64_t sstride = (int64_t)Cout * Kp;
@@ -252,7 +253,9 @@ wgrad_reduce_kernel(const float* __restrict__ partial, float* __restrict__ grad,
     }
     for (; s < splits; ++s) a0 += partial[src + s * sstride];
     const float a = (a0 + a1) + (a2 + a3);
-    const int64_t dst = ((int64_t)co * Cin + ci) * KH * KW + tap;
+    // channel-padded stems (Cin 3 -> 8): only the real input channels exist in grad
+    if (ci >= cin_keep) continue;
+    const int64_t dst = ((int64_t)co * cin_keep + ci) * KH * KW + tap;
     grad[dst] = (accumulate ? grad[dst] : 0.f) + scale * a;
   }
 }
@@ -287,59 +290,147 @@ pack_kernel(const float* __restrict__ w, bf16_t* __restrict__ wf, bf16_t* __rest
   }
 }
 
-// All layers of a network in one launch.  table[l] = {w, wf, wt (0 = none),
-// Cout, Cin, KH, KW, Kp, KpT, start} (int64), start = first global element
-// of layer l; layer l covers Cout*Kp forward elements then, with wt, the
-// Cin*(KpT - KH*KW*Cout) dgrad padding zeros.
+// All layers of a network in one launch, as tiled transposes through LDS.
+// table[l] = {w, wf, wt (0 = none), Cout, Cin, KH, KW, Kp, KpT, tile0} (int64),
+// tile0 = first tile of layer l.  A tile is T co x T ci x all taps
+// (T = 64 for 1x1, 32 up to 3x3, 16 for larger kernels), loaded with
+// coalesced reads of the OIHW fp32 rows (taps contiguous per (co, ci)) and
+// written as T-long contiguous runs of both packed layouts:
+//   wf[co][tap*Cin + ci]   and   wt[ci][tap*Cout + co].
+// Padding columns (k >= K, and the dgrad tail) are never touched: they are
+// zeroed once by the per-layer pack at registration and stay zero.
+// (The previous element-per-thread version scattered 2-byte stores at
+// stride KpT and took 232 us for a ResNet-18.)
 constexpr int PACK_MAX_LAYERS = 128;
 constexpr int PACK_FIELDS = 10;
+constexpr int PACK_LDS_FLOATS = 13056;  // >= max over T of T*(T*KHKW + 1)
+
+__device__ __forceinline__ int pack_tile_dim(int khkw) {
+  return khkw == 1 ? 64 : (khkw <= 9 ? 32 : 16);
+}
 
 __global__ void __launch_bounds__(256)
-pack_multi_kernel(const int64_t* __restrict__ table, int L, int64_t total) {
+pack_multi_kernel(const int64_t* __restrict__ table, int L) {
   __shared__ int64_t tb[PACK_MAX_LAYERS * PACK_FIELDS];
+  __shared__ float sm[PACK_LDS_FLOATS];
   for (int i = threadIdx.x; i < L * PACK_FIELDS; i += blockDim.x) tb[i] = table[i];
   __syncthreads();
   int l = 0;
+  while (l + 1 < L && (int64_t)blockIdx.x >= tb[(l + 1) * PACK_FIELDS + 9]) ++l;
+  const int64_t* e = tb + l * PACK_FIELDS;
+  const float* w = (const float*)e[0];
+  bf16_t* wf = (bf16_t*)e[1];
+  bf16_t* wt = (bf16_t*)e[2];
+  const int Cout = (int)e[3], Cin = (int)e[4], KHKW = (int)(e[5] * e[6]);
+  const int Kp = (int)e[7], KpT = (int)e[8];
+  const int T = pack_tile_dim(KHKW);
+  const int tci = (Cin + T - 1) / T;
+  const int t = (int)(blockIdx.x - e[9]);
+  const int co0 = (t / tci) * T, ci0 = (t - (t / tci) * tci) * T;
+  const int nco = min(T, Cout - co0), nci = min(T, Cin - ci0);
+  const int RS = T * KHKW + 1;  // LDS row stride (odd: conflict-free column walks)
+  // load: rows co0..co0+nco, each a contiguous run of nci*KHKW floats
+  const int run = nci * KHKW;
+  for (int i = threadIdx.x; i < nco * run; i += blockDim.x) {
+    const int r = i / run, c = i - (i / run) * run;
+    sm[r * RS + c] = w[((int64_t)(co0 + r) * Cin + ci0) * KHKW + c];
+  }
+  __syncthreads();
+  // wf[co][tap*Cin + ci]: runs over ci
+  for (int i = threadIdx.x; i < nco * KHKW * nci; i += blockDim.x) {
+    const int r = i / (KHKW * nci), rem = i - r * (KHKW * nci);
+    const int tap = rem / nci, ci = rem - tap * nci;
+    wf[(int64_t)(co0 + r) * Kp + tap * Cin + ci0 + ci] = f2bf(sm[r * RS + ci * KHKW + tap]);
+  }
+  if (wt) {  // wt[ci][tap*Cout + co]: runs over co
+    for (int i = threadIdx.x; i < nci * KHKW * nco; i += blockDim.x) {
+      const int ci = i / (KHKW * nco), rem = i - ci * (KHKW * nco);
+      const int tap = rem / nco, r = rem - tap * nco;
+      wt[(int64_t)(ci0 + ci) * KpT + tap * Cout + co0 + r] = f2bf(sm[r * RS + ci * KHKW + tap]);
+    }
+  }
+}
+
+// Stem support: the 3-channel image conv would gather 2-byte elements one
+// at a time; padding the input to 8 channels (zeros) puts it on the 16-byte
+// vector loaders, at 8/3 the (tiny) stem MFMA work.
+// x: [M, C] NHWC fp32 or bf16 -> y: [M, Cp] bf16, channels >= C zero.
+template <typename T>
+__global__ void __launch_bounds__(256)
+pad_channels_kernel(const T* __restrict__ x, bf16_t* __restrict__ y, int64_t M, int C, int Cp) {
+  for (int64_t m = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; m < M;
+       m += (int64_t)gridDim.x * blockDim.x) {
+    if (Cp == 8) {
+      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int c = 0; c < C; ++c) v[c] = io<T>::ld(x, m * C + c);
+      *(uint4*)(y + m * 8) = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
+                                        pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+    } else {
+      for (int c = 0; c < Cp; ++c) y[m * Cp + c] = f2bf(c < C ? io<T>::ld(x, m * C + c) : 0.f);
+    }
+  }
+}
+
+// forward operand of a channel-padded conv: wf[co][(kh*KW+kw)*Cp + ci] =
+// w[co][ci][kh][kw] for ci < C, else 0; k >= KH*KW*Cp zero.
+__global__ void __launch_bounds__(256)
+pack_pad_kernel(const float* __restrict__ w, bf16_t* __restrict__ wf, int Cout, int C, int Cp,
+                int KH, int KW, int Kp) {
+  const int64_t total = (int64_t)Cout * Kp;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
-    while (l + 1 < L && i >= tb[(l + 1) * PACK_FIELDS + 9]) ++l;  // i only grows per thread
-    const int64_t* e = tb + l * PACK_FIELDS;
-    const float* w = (const float*)e[0];
-    bf16_t* wf = (bf16_t*)e[1];
-    bf16_t* wt = (bf16_t*)e[2];
-    const int Cout = (int)e[3], Cin = (int)e[4], KH = (int)e[5], KW = (int)e[6];
-    const int Kp = (int)e[7], KpT = (int)e[8];
-    const int64_t li = i - e[9];
-    const int64_t nf = (int64_t)Cout * Kp;
-    if (li < nf) {
-      const int co = (int)(li / Kp);
-      const int k = (int)(li - (int64_t)co * Kp);
-      float v = 0.f;
-      if (k < KH * KW * Cin) {
-        const int tap = k / Cin, ci = k - (k / Cin) * Cin;
-        const int kh = tap / KW, kw = tap - kh * KW;
-        v = w[(((int64_t)co * Cin + ci) * KH + kh) * KW + kw];
-        if (wt) wt[(int64_t)ci * KpT + tap * Cout + co] = f2bf(v);
-      }
-      wf[li] = f2bf(v);
-    } else if (wt) {
-      const int64_t pi = li - nf;
-      const int w_ = KpT - KH * KW * Cout;
-      const int ci = (int)(pi / w_);
-      const int j = (int)(pi - (int64_t)ci * w_);
-      wt[(int64_t)ci * KpT + KH * KW * Cout + j] = 0;
+    const int co = (int)(i / Kp), k = (int)(i - (i / Kp) * Kp);
+    float v = 0.f;
+    if (k < KH * KW * Cp) {
+      const int tap = k / Cp, ci = k - tap * Cp;
+      if (ci < C) v = w[(((int64_t)co * C + ci) * KH + tap / KW) * KW + tap % KW];
     }
+    wf[i] = f2bf(v);
   }
 }
 
 }  // namespace
 
+MDA_API int mda_pad_channels(int64_t dt, const void* x, void* y, int64_t M, int64_t C, int64_t Cp,
+                             hipStream_t st) {
+  if (C > Cp || C > 8 || M <= 0) return (int)hipErrorInvalidValue;
+  const int blocks = (int)std::min<int64_t>((M + 255) / 256, 4096);
+  if (dt == DT_F32)
+    hipLaunchKernelGGL(pad_channels_kernel<float>, dim3(blocks), dim3(256), 0, st,
+                       (const float*)x, (bf16_t*)y, M, (int)C, (int)Cp);
+  else
+    hipLaunchKernelGGL(pad_channels_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st,
+                       (const bf16_t*)x, (bf16_t*)y, M, (int)C, (int)Cp);
+  MDA_CHECK_LAUNCH();
+}
+
+MDA_API int mda_pack_conv_weights_pad(const float* w, void* wf, int64_t Cout, int64_t C, int64_t Cp,
+                                      int64_t KH, int64_t KW, int64_t Kp, hipStream_t st) {
+  if (C > Cp || Kp < KH * KW * Cp) return (int)hipErrorInvalidValue;
+  const int64_t total = Cout * Kp;
+  const int blocks = (int)std::min<int64_t>((total + 255) / 256, 1024);
+  hipLaunchKernelGGL(pack_pad_kernel, dim3(blocks), dim3(256), 0, st, w, (bf16_t*)wf, (int)Cout,
+                     (int)C, (int)Cp, (int)KH, (int)KW, (int)Kp);
+  MDA_CHECK_LAUNCH();
+}
+
+// total = number of tiles over all layers (see pack_multi_kernel; mda_pack_tiles
+// gives a layer's count).  The packed buffers' padding must already be zero.
 MDA_API int mda_pack_conv_weights_multi(const int64_t* table, int64_t L, int64_t total,
                                         hipStream_t st) {
-  if (L <= 0 || L > PACK_MAX_LAYERS || total <= 0) return (int)hipErrorInvalidValue;
-  int blocks = (int)std::min<int64_t>((total + 255) / 256, 2048);
-  hipLaunchKernelGGL(pack_multi_kernel, dim3(blocks), dim3(256), 0, st, table, (int)L, total);
+  if (L <= 0 || L > PACK_MAX_LAYERS || total <= 0 || total > (1 << 30))
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(pack_multi_kernel, dim3((unsigned)total), dim3(256), 0, st, table, (int)L);
   MDA_CHECK_LAUNCH();
+}
+
+// Tiles of one layer in mda_pack_conv_weights_multi.
+MDA_API int mda_pack_tiles(int64_t Cout, int64_t Cin, int64_t KH, int64_t KW, int64_t* tiles) {
+  const int64_t khkw = KH * KW;
+  const int64_t T = khkw == 1 ? 64 : (khkw <= 9 ? 32 : 16);
+  if (khkw > 49) return (int)hipErrorInvalidValue;  // PACK_LDS_FLOATS sizing
+  *tiles = ((Cout + T - 1) / T) * ((Cin + T - 1) / T);
+  return 0;
 }
 
 MDA_API int mda_wgrad_plan(int64_t M, int64_t Cout, int64_t Kp, int64_t* splits) {
@@ -355,8 +446,10 @@ MDA_API int mda_wgrad_plan(int64_t M, int64_t Cout, int64_t Kp, int64_t* splits)
 MDA_API int mda_conv_wgrad(const void* x, const void* dy, float* partial, float* grad, int64_t N,
                            int64_t H, int64_t W, int64_t Cin, int64_t Ho, int64_t Wo, int64_t Cout,
                            int64_t KH, int64_t KW, int64_t stride, int64_t pad, int64_t Kp,
-                           int64_t splits, float scale, int64_t accumulate, hipStream_t st) {
+                           int64_t splits, float scale, int64_t accumulate, int64_t cin_keep,
+                           hipStream_t st) {
   if (Cout % 8 || Kp % TK) return (int)hipErrorInvalidValue;
+  if (cin_keep <= 0 || cin_keep > Cin) cin_keep = Cin;
   WgParams p;
   p.x = (const bf16_t*)x; p.dy = (const bf16_t*)dy; p.partial = partial;
   p.N = N; p.H = H; p.W = W; p.Cin = Cin; p.Ho = Ho; p.Wo = Wo; p.Cout = Cout; p.KH = KH;
@@ -383,7 +476,7 @@ MDA_API int mda_conv_wgrad(const void* x, const void* dy, float* partial, float*
   int blocks = (int)std::min<int64_t>((total + 255) / 256, 1024);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, partial, grad,
                      (int)splits, (int)Cout, (int)Cin, (int)KH, (int)KW, (int)Kp, scale,
-                     (int)accumulate);
+                     (int)accumulate, (int)cin_keep);
   MDA_CHECK_LAUNCH();
 }
 

@@ -134,6 +134,11 @@ pool_fc_bwd_kernel(const T* __restrict__ dl, const T* __restrict__ dpooled,
   }
 }
 
+// One wave per row (lanes stride over the C classes; ImageNet's 1000-class
+// rows took 100 us as one thread per row in a single block).  Hit counts are
+// integers, so the per-block fp64 atomic adds are exact and order-free
+// (deterministic); block 0 also adds the loss values and the sample/step
+// counts.
 template <typename T>
 __global__ void __launch_bounds__(256)
 meters_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target, int B, int C,
@@ -143,50 +148,150 @@ meters_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target, i
   __shared__ int s_hits[2];
   if (threadIdx.x < 2) s_hits[threadIdx.x] = 0;
   __syncthreads();
-  int h1 = 0, h5 = 0;
-  // one thread per row: C independent loads, no cross-lane reduction chain
-  for (int r = threadIdx.x; r < B; r += blockDim.x) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r = blockIdx.x * 4 + wid;
+  if (r < B) {
     const int64_t base = (int64_t)r * C;
     const int tg = (int)target[r];
     const float t = io<T>::ld(preds, base + tg);
     // rank of the target = classes ordered before it by topk: strictly larger
     // logits, plus EQUAL logits at a lower class index (ties are frequent with
     // bf16 logits and must not count as hits)
-    int c0 = 0, c1 = 0, c2 = 0, c3 = 0, c = 0;
-    for (; c + 4 <= tg; c += 4) {
-      c0 += io<T>::ld(preds, base + c) >= t;
-      c1 += io<T>::ld(preds, base + c + 1) >= t;
-      c2 += io<T>::ld(preds, base + c + 2) >= t;
-      c3 += io<T>::ld(preds, base + c + 3) >= t;
+    int cnt = 0;
+    for (int c = lane; c < C; c += 64) {
+      const float v = io<T>::ld(preds, base + c);
+      cnt += (v > t) || (v == t && c < tg);
     }
-    for (; c < tg; ++c) c0 += io<T>::ld(preds, base + c) >= t;
-    for (c = tg + 1; c + 4 <= C; c += 4) {
-      c0 += io<T>::ld(preds, base + c) > t;
-      c1 += io<T>::ld(preds, base + c + 1) > t;
-      c2 += io<T>::ld(preds, base + c + 2) > t;
-      c3 += io<T>::ld(preds, base + c + 3) > t;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+    if (lane == 0) {
+      if (cnt < 1) atomicAdd(&s_hits[0], 1);
+      if (cnt < 5) atomicAdd(&s_hits[1], 1);
     }
-    for (; c < C; ++c) c0 += io<T>::ld(preds, base + c) > t;
-    const int cnt = c0 + c1 + c2 + c3;
-    h1 += cnt < 1;
-    h5 += cnt < 5;
   }
-  if (h1) atomicAdd(&s_hits[0], h1);
-  if (h5) atomicAdd(&s_hits[1], h5);
   __syncthreads();
   if (threadIdx.x == 0) {
-    const float* ls[4] = {l0, l1, l2, l3};
-    double total = 0.0;
-    for (int i = 0; i < nloss; ++i) {
-      const double v = (double)*ls[i];
-      buf[1 + i] += v;
-      total += v;
+    if (s_hits[0]) atomicAdd(&buf[nloss + 1], (double)s_hits[0]);
+    if (s_hits[1]) atomicAdd(&buf[nloss + 2], (double)s_hits[1]);
+    if (blockIdx.x == 0) {
+      const float* ls[4] = {l0, l1, l2, l3};
+      double total = 0.0;
+      for (int i = 0; i < nloss; ++i) {
+        const double v = (double)*ls[i];
+        buf[1 + i] += v;
+        total += v;
+      }
+      buf[0] += total;
+      buf[nloss + 3] += (double)B;
+      buf[nloss + 4] += 1.0;
     }
-    buf[0] += total;
-    buf[nloss + 1] += (double)s_hits[0];
-    buf[nloss + 2] += (double)s_hits[1];
-    buf[nloss + 3] += (double)B;
-    buf[nloss + 4] += 1.0;
+  }
+}
+
+// ---- tiled head backward for large heads (ImageNet: J = 1000, C = 512..2048)
+// Two small GEMMs, one launch: blocks [0, nW) compute dW/db tiles
+// (64 j x 64 c, reduction over the batch), blocks [nW, nW + nX) compute
+// d(feature) tiles (16 n x 64 c, reduction over the J logits) and broadcast
+// them over the HW positions.  Reduction operands are staged through LDS in
+// chunks of 32; each thread owns a 4x4 (dW) or 1x4 (dx) register tile.
+constexpr int HB_TJ = 64, HB_TC = 64, HB_TN = 16, HB_R = 32;
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+pool_fc_bwd_tiled_kernel(const T* __restrict__ dl, const T* __restrict__ dpooled,
+                         const T* __restrict__ pooled, const float* __restrict__ W,
+                         float* __restrict__ dW, float* __restrict__ db, T* __restrict__ dx, int N,
+                         int HW, int C, int J, float inv_hw, int accum, int nW) {
+  __shared__ float sa[HB_R][HB_TJ + 1];
+  __shared__ float sb[HB_R][HB_TC + 4];
+  const int tid = threadIdx.x;
+  const int ctiles = (C + HB_TC - 1) / HB_TC;
+  if ((int)blockIdx.x < nW) {
+    if (dW == nullptr && db == nullptr) return;
+    const int jt = blockIdx.x / ctiles, ct = blockIdx.x - jt * ctiles;
+    const int j0 = jt * HB_TJ, c0 = ct * HB_TC;
+    const int tj = (tid >> 4) * 4, tc = (tid & 15) * 4;
+    float acc[4][4] = {};
+    float dbacc = 0.f;
+    for (int n0 = 0; n0 < N; n0 += HB_R) {
+      for (int i = tid; i < HB_R * HB_TJ; i += 256) {
+        const int r = i / HB_TJ, jj = i - r * HB_TJ;
+        const int n = n0 + r, j = j0 + jj;
+        sa[r][jj] = (n < N && j < J) ? io<T>::ld(dl, (int64_t)n * J + j) : 0.f;
+      }
+      for (int i = tid; i < HB_R * HB_TC; i += 256) {
+        const int r = i / HB_TC, cc = i - r * HB_TC;
+        const int n = n0 + r, c = c0 + cc;
+        sb[r][cc] = (n < N && c < C) ? io<T>::ld(pooled, (int64_t)n * C + c) : 0.f;
+      }
+      __syncthreads();
+#pragma unroll 4
+      for (int r = 0; r < HB_R; ++r) {
+        float a[4], b[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) { a[u] = sa[r][tj + u]; b[u] = sb[r][tc + u]; }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) acc[u][v] += a[u] * b[v];
+      }
+      if (db != nullptr && ct == 0 && tid < HB_TJ)
+        for (int r = 0; r < HB_R; ++r) dbacc += sa[r][tid];
+      __syncthreads();
+    }
+    if (dW != nullptr) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int j = j0 + tj + u;
+        if (j >= J) continue;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int c = c0 + tc + v;
+          if (c >= C) continue;
+          float* o = dW + (int64_t)j * C + c;
+          *o = accum ? *o + acc[u][v] : acc[u][v];
+        }
+      }
+    }
+    if (db != nullptr && ct == 0 && tid < HB_TJ && j0 + tid < J)
+      db[j0 + tid] = accum ? db[j0 + tid] + dbacc : dbacc;
+    return;
+  }
+  // ---- dx tile: rows n0..n0+15, channels c0..c0+63
+  const int b = blockIdx.x - nW;
+  const int nt = b / ctiles, ct = b - nt * ctiles;
+  const int n0 = nt * HB_TN, c0 = ct * HB_TC;
+  const int tn = tid >> 4, tc = (tid & 15) * 4;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int r0 = 0; r0 < J; r0 += HB_R) {
+    for (int i = tid; i < HB_R * HB_TN; i += 256) {
+      const int r = i / HB_TN, nn = i - r * HB_TN;
+      const int j = r0 + r, n = n0 + nn;
+      sa[r][nn] = (n < N && j < J) ? io<T>::ld(dl, (int64_t)n * J + j) : 0.f;
+    }
+    for (int i = tid; i < HB_R * HB_TC; i += 256) {
+      const int r = i / HB_TC, cc = i - r * HB_TC;
+      const int j = r0 + r, c = c0 + cc;
+      sb[r][cc] = (j < J && c < C) ? W[(int64_t)j * C + c] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int r = 0; r < HB_R; ++r) {
+      const float a = sa[r][tn];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) acc[v] += a * sb[r][tc + v];
+    }
+    __syncthreads();
+  }
+  const int n = n0 + tn;
+  if (n >= N) return;
+  T* dxn = dx + (int64_t)n * HW * C;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int c = c0 + tc + v;
+    if (c >= C) continue;
+    const float val = ((dpooled ? io<T>::ld(dpooled, (int64_t)n * C + c) : 0.f) + acc[v]) * inv_hw;
+    for (int p = 0; p < HW; ++p) io<T>::st(dxn, (int64_t)p * C + c, val);
   }
 }
 
@@ -215,6 +320,21 @@ MDA_API int mda_pool_fc_bwd(int64_t dt, const void* dl, const void* dpooled, con
                             const float* W, float* dW, float* db, void* dx, int64_t N, int64_t HW,
                             int64_t C, int64_t J, int64_t accum, hipStream_t st) {
   if (N <= 0 || C <= 0 || J <= 0 || N > 16384 || J > 16384) return (int)hipErrorInvalidValue;
+  if ((int64_t)J * C > (1 << 16)) {  // large head: tiled GEMM blocks
+    const int ct = (int)((C + HB_TC - 1) / HB_TC);
+    const int nW = (int)((J + HB_TJ - 1) / HB_TJ) * ct;
+    const int nX = (int)((N + HB_TN - 1) / HB_TN) * ct;
+    if (dt == DT_F32)
+      hipLaunchKernelGGL(pool_fc_bwd_tiled_kernel<float>, dim3(nW + nX), dim3(256), 0, st,
+                         (const float*)dl, (const float*)dpooled, (const float*)pooled, W, dW, db,
+                         (float*)dx, (int)N, (int)HW, (int)C, (int)J, 1.f / HW, (int)accum, nW);
+    else
+      hipLaunchKernelGGL(pool_fc_bwd_tiled_kernel<bf16_t>, dim3(nW + nX), dim3(256), 0, st,
+                         (const bf16_t*)dl, (const bf16_t*)dpooled, (const bf16_t*)pooled, W, dW,
+                         db, (bf16_t*)dx, (int)N, (int)HW, (int)C, (int)J, 1.f / HW, (int)accum,
+                         nW);
+    MDA_CHECK_LAUNCH();
+  }
   const size_t lds = (size_t)(N > J ? N : J) * sizeof(float);
   const dim3 grid((unsigned)(J + N));
   if (dt == DT_F32)
@@ -234,11 +354,12 @@ MDA_API int mda_meters_update(int64_t dt, const void* preds, const int64_t* targ
                               int64_t C, const float* l0, const float* l1, const float* l2,
                               const float* l3, int64_t nloss, double* buf, hipStream_t st) {
   if (nloss < 0 || nloss > 4 || B <= 0) return (int)hipErrorInvalidValue;
+  const dim3 grid((unsigned)((B + 3) / 4));
   if (dt == DT_F32)
-    hipLaunchKernelGGL(meters_kernel<float>, dim3(1), dim3(256), 0, st, (const float*)preds, target,
+    hipLaunchKernelGGL(meters_kernel<float>, grid, dim3(256), 0, st, (const float*)preds, target,
                        (int)B, (int)C, l0, l1, l2, l3, (int)nloss, buf);
   else
-    hipLaunchKernelGGL(meters_kernel<bf16_t>, dim3(1), dim3(256), 0, st, (const bf16_t*)preds,
+    hipLaunchKernelGGL(meters_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)preds,
                        target, (int)B, (int)C, l0, l1, l2, l3, (int)nloss, buf);
   MDA_CHECK_LAUNCH();
 }

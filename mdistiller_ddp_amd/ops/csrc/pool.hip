@@ -1,0 +1,133 @@
+// Max pooling on NHWC bf16 activations (survey K4): the ImageNet ResNet stem
+// pool (3x3 / s2 / p1 on the 112x112 stem output) and the CIFAR VGG 2x2
+// pools.  Forward writes the pooled map and, per output element, the window
+// offset of its maximum (uint8); backward is a GATHER over the <= ceil(k/s)^2
+// windows that contain each input pixel, so it is deterministic and
+// atomic-free.  8 channels (16 bytes) per thread; ties keep the first
+// maximum in window order, as PyTorch does.
+#include "common.h"
+
+namespace {
+
+struct PoolParams {
+  int N, H, W, C, Ho, Wo, k, s, p;
+};
+
+__global__ void __launch_bounds__(256)
+maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, uint8_t* __restrict__ idx,
+                   PoolParams q) {
+  const int C8 = q.C / 8;
+  const int64_t total = (int64_t)q.N * q.Ho * q.Wo * C8;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int c8 = (int)(t % C8);
+    const int64_t pix = t / C8;
+    const int ow = (int)(pix % q.Wo);
+    const int64_t r = pix / q.Wo;
+    const int oh = (int)(r % q.Ho);
+    const int n = (int)(r / q.Ho);
+    float best[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; bi[e] = 0; }
+    const int h0 = oh * q.s - q.p, w0 = ow * q.s - q.p;
+    for (int kh = 0; kh < q.k; ++kh) {
+      const int ih = h0 + kh;
+      if ((unsigned)ih >= (unsigned)q.H) continue;
+      for (int kw = 0; kw < q.k; ++kw) {
+        const int iw = w0 + kw;
+        if ((unsigned)iw >= (unsigned)q.W) continue;
+        const uint4 v = *(const uint4*)(x + (((int64_t)n * q.H + ih) * q.W + iw) * q.C + c8 * 8);
+        const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float a = __uint_as_float(u[e] << 16), b = __uint_as_float(u[e] & 0xffff0000u);
+          // first maximum wins; NaN propagates (as torch)
+          if (a > best[2 * e] || (a != a && best[2 * e] == best[2 * e])) { best[2 * e] = a; bi[2 * e] = (uint8_t)(kh * q.k + kw); }
+          if (b > best[2 * e + 1] || (b != b && best[2 * e + 1] == best[2 * e + 1])) { best[2 * e + 1] = b; bi[2 * e + 1] = (uint8_t)(kh * q.k + kw); }
+        }
+      }
+    }
+    const int64_t o = pix * q.C + c8 * 8;
+    *(uint4*)(y + o) = make_uint4(pack_bf16x2(best[0], best[1]), pack_bf16x2(best[2], best[3]),
+                                  pack_bf16x2(best[4], best[5]), pack_bf16x2(best[6], best[7]));
+    if (idx) {
+      uint2 packed;
+      packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
+      packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
+      *(uint2*)(idx + o) = packed;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256)
+maxpool_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ idx,
+                   bf16_t* __restrict__ dx, PoolParams q) {
+  const int C8 = q.C / 8;
+  const int64_t total = (int64_t)q.N * q.H * q.W * C8;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int c8 = (int)(t % C8);
+    const int64_t pix = t / C8;
+    const int iw = (int)(pix % q.W);
+    const int64_t r = pix / q.W;
+    const int ih = (int)(r % q.H);
+    const int n = (int)(r / q.H);
+    // outputs whose window holds (ih, iw): oh*s - p <= ih <= oh*s - p + k - 1
+    const int ohl = max(0, (ih + q.p - q.k + q.s) / q.s), ohh = min(q.Ho - 1, (ih + q.p) / q.s);
+    const int owl = max(0, (iw + q.p - q.k + q.s) / q.s), owh = min(q.Wo - 1, (iw + q.p) / q.s);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int oh = ohl; oh <= ohh; ++oh) {
+      const int kh = ih - (oh * q.s - q.p);
+      if (kh < 0 || kh >= q.k) continue;
+      for (int ow = owl; ow <= owh; ++ow) {
+        const int kw = iw - (ow * q.s - q.p);
+        if (kw < 0 || kw >= q.k) continue;
+        const uint8_t off = (uint8_t)(kh * q.k + kw);
+        const int64_t o = (((int64_t)n * q.Ho + oh) * q.Wo + ow) * q.C + c8 * 8;
+        const uint2 iv = *(const uint2*)(idx + o);
+        const uint4 g = *(const uint4*)(dy + o);
+        const uint32_t gu[4] = {g.x, g.y, g.z, g.w};
+        const uint32_t iu[2] = {iv.x, iv.y};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint8_t w = (uint8_t)(iu[e >> 2] >> (8 * (e & 3)));
+          const float gv = (e & 1) ? __uint_as_float(gu[e >> 1] & 0xffff0000u)
+                                   : __uint_as_float(gu[e >> 1] << 16);
+          if (w == off) acc[e] += gv;
+        }
+      }
+    }
+    *(uint4*)(dx + pix * q.C + c8 * 8) =
+        make_uint4(pack_bf16x2(acc[0], acc[1]), pack_bf16x2(acc[2], acc[3]),
+                   pack_bf16x2(acc[4], acc[5]), pack_bf16x2(acc[6], acc[7]));
+  }
+}
+
+inline int grid_for(int64_t n) {
+  int64_t b = (n + 255) / 256;
+  return (int)(b < 1 ? 1 : (b > 8192 ? 8192 : b));
+}
+
+}  // namespace
+
+// x [N, H, W, C] bf16 (C % 8 == 0) -> y [N, Ho, Wo, C] bf16, idx [N, Ho, Wo, C] uint8 (or null).
+MDA_API int mda_maxpool_fwd(const void* x, void* y, void* idx, int64_t N, int64_t H, int64_t W,
+                            int64_t C, int64_t Ho, int64_t Wo, int64_t k, int64_t s, int64_t p,
+                            hipStream_t st) {
+  if (C % 8 || k < 1 || k > 15 || s < 1 || p < 0 || 2 * p > k) return (int)hipErrorInvalidValue;
+  PoolParams q{(int)N, (int)H, (int)W, (int)C, (int)Ho, (int)Wo, (int)k, (int)s, (int)p};
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(N * Ho * Wo * C / 8)), dim3(256), 0, st,
+                     (const bf16_t*)x, (bf16_t*)y, (uint8_t*)idx, q);
+  MDA_CHECK_LAUNCH();
+}
+
+MDA_API int mda_maxpool_bwd(const void* dy, const void* idx, void* dx, int64_t N, int64_t H,
+                            int64_t W, int64_t C, int64_t Ho, int64_t Wo, int64_t k, int64_t s,
+                            int64_t p, hipStream_t st) {
+  if (C % 8 || k < 1 || k > 15 || s < 1 || p < 0) return (int)hipErrorInvalidValue;
+  PoolParams q{(int)N, (int)H, (int)W, (int)C, (int)Ho, (int)Wo, (int)k, (int)s, (int)p};
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(N * H * W * C / 8)), dim3(256), 0, st,
+                     (const bf16_t*)dy, (const uint8_t*)idx, (bf16_t*)dx, q);
+  MDA_CHECK_LAUNCH();
+}

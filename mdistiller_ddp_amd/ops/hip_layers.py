@@ -112,6 +112,9 @@ def _packed(conv, bn):
         s = g / torch.sqrt(bn.running_var.float() + bn.eps)
         w = w * s.reshape(-1, 1, 1, 1)
         b = beta + (b - bn.running_mean.float()) * s
+    from .hip_train import needs_channel_pad
+    if needs_channel_pad(w.shape[1]):  # stem: input padded to 8 channels
+        w = torch.nn.functional.pad(w, (0, 0, 0, 0, 0, 8 - w.shape[1]))
     K = w.shape[1] * w.shape[2] * w.shape[3]
     Kp = (K + 63) // 64 * 64
     wp = torch.zeros(cout, Kp, dtype=torch.bfloat16, device=w.device)
@@ -170,7 +173,8 @@ def conv_bn_act(x, conv, bn, act, residual, want_preact):
     if conv.groups != 1:
         return _dw_conv_bn_act(x, conv, bn, act, residual, want_preact)
     wp, bias = _packed(conv, bn)
-    x = _nhwc_bf16(x)
+    from .hip_train import needs_channel_pad, pad_channels8
+    x = pad_channels8(x) if needs_channel_pad(x.shape[1]) else _nhwc_bf16(x)
     N, Cin, H, W = x.shape
     Cout = conv.out_channels
     KH, KW = conv.kernel_size

@@ -99,7 +99,9 @@ class PackCache:
         rows, start = [], 0
         for e in self.entries.values():
             Cout, Cin, KH, KW, Kp, KpT = e["meta"]
-            n = Cout * Kp + (Cin * (KpT - KH * KW * Cout) if e["wt"] is not None else 0)
+            t = ctypes.c_int64(0)
+            _ext.call("mda_pack_tiles", Cout, Cin, KH, KW, t)
+            n = t.value  # tiles of this layer (padding stays zero from registration)
             w = e["weight"]
             rows.append([w.data_ptr(), e["wf"].data_ptr(), e["wt"].data_ptr() if e["wt"] is not None else 0,
                          Cout, Cin, KH, KW, Kp, KpT, start])
@@ -110,7 +112,8 @@ class PackCache:
         self._dirty = False
 
     def pack_all(self, device) -> bool:
-        if not self.entries or len(self.entries) > 128:
+        if not self.entries or len(self.entries) > 128 or any(
+                e["meta"][2] * e["meta"][3] > 49 for e in self.entries.values()):
             return False
         capturing = torch.cuda.is_current_stream_capturing()
         stale = self._table is None or self._dirty or any(
@@ -138,6 +141,35 @@ def _cl_bf16(t):
     if t.dtype != torch.bfloat16:
         t = t.to(torch.bfloat16)
     return t.contiguous(memory_format=torch.channels_last)
+
+
+def needs_channel_pad(cin: int) -> bool:
+    """3-channel image convs run on the 16-byte vector loaders with the input
+    zero-padded to 8 channels (``mda_pad_channels``)."""
+    return cin < 8 and cin % 8 != 0
+
+
+def pad_channels8(x):
+    """NCHW-logical (any layout) fp32/bf16 image -> bf16 channels_last with 8
+    channels (zeros beyond the real ones), one launch.  Cached per tensor
+    version and stream, so a second consumer on the same stream (e.g. two
+    stems) reuses it."""
+    key = (x._version, torch.cuda.current_stream(x.device).cuda_stream)
+    cache = getattr(x, "_mda_pad8", None)
+    if cache is not None and cache[0] == key:
+        return cache[1]
+    xc = x.contiguous(memory_format=torch.channels_last)
+    if xc.dtype not in (torch.float32, torch.bfloat16):
+        xc = xc.float()
+    N, C, H, W = xc.shape
+    y = torch.empty((N, 8, H, W), dtype=torch.bfloat16, device=x.device,
+                    memory_format=torch.channels_last)
+    _ext.call("mda_pad_channels", 0 if xc.dtype == torch.float32 else 1, xc, y, N * H * W, C, 8)
+    try:
+        x._mda_pad8 = (key, y)
+    except Exception:  # noqa: BLE001 -- caching is optional
+        pass
+    return y
 
 
 def train_supported(x, conv, bn) -> bool:
@@ -212,7 +244,10 @@ class _ConvBNActTrain(torch.autograd.Function):
             return _dw_forward(ctx, x, weight, gamma, beta, residual, stride, pad, act, bn,
                                want_preact)
         ctx.kind = "dense"
-        x = _cl_bf16(x)
+        need_dx = ctx.needs_input_grad[0]
+        cin_w = weight.shape[1]
+        chpad = (not need_dx) and needs_channel_pad(cin_w)
+        x = pad_channels8(x) if chpad else _cl_bf16(x)
         N, Cin, H, W = x.shape
         Cout, _, KH, KW = weight.shape
         Ho = (H + 2 * pad - KH) // stride + 1
@@ -220,12 +255,17 @@ class _ConvBNActTrain(torch.autograd.Function):
         M = N * Ho * Wo
         K = KH * KW * Cin
         Kp = (K + 63) // 64 * 64
-        need_dx = ctx.needs_input_grad[0]
         KpT = (KH * KW * Cout + 63) // 64 * 64
         dev = x.device
+        ctx.cin_keep = cin_w if chpad else 0
         packs = _ACTIVE[0]
-        ent = packs.lookup(weight, need_dx) if packs is not None else None
-        if ent is not None:  # packed for this step by PackCache.pack_all
+        ent = packs.lookup(weight, need_dx) if (packs is not None and not chpad) else None
+        if chpad:  # stem: forward operand with zero weights for the pad channels
+            wf = torch.empty(Cout, Kp, dtype=torch.bfloat16, device=dev)
+            wt = None
+            _ext.call("mda_pack_conv_weights_pad", weight.detach().contiguous(), wf, Cout, cin_w,
+                      Cin, KH, KW, Kp)
+        elif ent is not None:  # packed for this step by PackCache.pack_all
             wf, wt = ent["wf"], ent["wt"]
         else:
             wf = torch.empty(Cout, Kp, dtype=torch.bfloat16, device=dev)
@@ -296,7 +336,7 @@ class _ConvBNActTrain(torch.autograd.Function):
             direct_w = weight.grad is not None and weight.grad.is_contiguous()
             target = weight.grad if direct_w else torch.empty_like(weight, memory_format=torch.contiguous_format)
             _ext.call("mda_conv_wgrad", x, dy, part, target, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
-                      stride, pad, Kp, sp, 1.0, 1 if direct_w else 0)
+                      stride, pad, Kp, sp, 1.0, 1 if direct_w else 0, ctx.cin_keep)
             dw = None if direct_w else target
             if direct_w:
                 notify_grad(weight)
@@ -432,7 +472,7 @@ def conv_wgrad(x, dy, weight_shape, stride, pad):
     part = torch.empty(sp * Cout * Kp, dtype=torch.float32, device=x.device)
     out = torch.empty(weight_shape, dtype=torch.float32, device=x.device)
     _ext.call("mda_conv_wgrad", x, dy, part, out, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
-              Kp, sp, 1.0, 0)
+              Kp, sp, 1.0, 0, 0)
     return out
 
 

@@ -198,3 +198,62 @@ def pool_linear(x: torch.Tensor, fc: nn.Linear, kernel: int | None = None):
 def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
     """(N, C, H, W) -> (N, C), fp32-accumulated."""
     return x.float().mean(dim=(2, 3)).to(x.dtype)
+
+
+class _MaxPoolNHWC(torch.autograd.Function):
+    """k x k / stride / pad max pool on the HIP kernels (csrc/pool.hip):
+    forward stores the argmax window offset (uint8), backward gathers."""
+
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        from . import _ext
+        xc = x.contiguous(memory_format=torch.channels_last)
+        N, C, H, W = xc.shape
+        Ho = (H + 2 * p - k) // s + 1
+        Wo = (W + 2 * p - k) // s + 1
+        y = torch.empty((N, C, Ho, Wo), dtype=x.dtype, device=x.device,
+                        memory_format=torch.channels_last)
+        need = ctx.needs_input_grad[0]
+        idx = torch.empty((N, Ho, Wo, C), dtype=torch.uint8, device=x.device) if need else None
+        _ext.call("mda_maxpool_fwd", xc, y, idx, N, H, W, C, Ho, Wo, k, s, p)
+        ctx.save_for_backward(idx)
+        ctx.meta = (N, C, H, W, Ho, Wo, k, s, p)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import _ext
+        idx, = ctx.saved_tensors
+        N, C, H, W, Ho, Wo, k, s, p = ctx.meta
+        dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        dx = torch.empty((N, C, H, W), dtype=torch.bfloat16, device=dy.device,
+                         memory_format=torch.channels_last)
+        _ext.call("mda_maxpool_bwd", dy, idx, dx, N, H, W, C, Ho, Wo, k, s, p)
+        return dx, None, None, None
+
+
+def _pair1(v):
+    if isinstance(v, (tuple, list)):
+        return v[0] if len(set(v)) == 1 else None
+    return v
+
+
+def max_pool2d(x: torch.Tensor, kernel_size, stride=None, padding=0) -> torch.Tensor:
+    """``F.max_pool2d`` with a native NHWC bf16 path (square windows, no dilation)."""
+    k = _pair1(kernel_size)
+    s = _pair1(stride if stride is not None else kernel_size)
+    p = _pair1(padding)
+    if (k is not None and s is not None and p is not None and x.dim() == 4 and hip_enabled_for(x)
+            and x.dtype == torch.bfloat16 and x.shape[1] % 8 == 0 and 2 * p <= k
+            and x.shape[2] + 2 * p >= k and x.shape[3] + 2 * p >= k):
+        return _MaxPoolNHWC.apply(x, int(k), int(s), int(p))
+    return F.max_pool2d(x, kernel_size, stride, padding)
+
+
+class MaxPool2d(nn.MaxPool2d):
+    """Drop-in ``nn.MaxPool2d`` (same state_dict / repr) running :func:`max_pool2d`."""
+
+    def forward(self, x):
+        if self.dilation not in (1, (1, 1)) or self.ceil_mode or self.return_indices:
+            return super().forward(x)
+        return max_pool2d(x, self.kernel_size, self.stride, self.padding)

@@ -10,7 +10,8 @@ pytestmark = pytest.mark.gpu
 
 SHAPES = [
     # N, Cin, H, Cout, k, stride, pad
-    (64, 3, 32, 32, 3, 1, 1),     # r32x4 stem (scalar loader)
+    (64, 3, 32, 32, 3, 1, 1),     # r32x4 stem (input padded to 8 channels)
+    (8, 3, 64, 64, 7, 2, 3),      # ImageNet 7x7/s2 stem (padded)
     (64, 32, 32, 64, 3, 1, 1),    # layer1 first conv
     (64, 64, 32, 64, 3, 1, 1),
     (64, 64, 32, 128, 3, 2, 1),   # stride-2 transition

@@ -13,7 +13,8 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-@pytest.mark.parametrize("N,C,HW,J", [(64, 256, 8, 100), (5, 64, 8, 10), (16, 512, 7, 1000), (3, 48, 4, 7)])
+@pytest.mark.parametrize("N,C,HW,J", [(64, 256, 8, 100), (5, 64, 8, 10), (16, 512, 7, 1000), (3, 48, 4, 7),
+                                     (64, 2048, 7, 1000), (33, 1024, 7, 1000)])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_pool_linear(N, C, HW, J, dtype):
     torch.manual_seed(0)
@@ -41,18 +42,19 @@ def test_pool_linear(N, C, HW, J, dtype):
     torch.testing.assert_close(fc.bias.grad, gb_r, atol=tol * 8, rtol=tol)
 
 
-def test_pool_linear_accumulates_into_bound_grad():
+@pytest.mark.parametrize("C,J", [(64, 10), (512, 300)])  # fused / tiled backward
+def test_pool_linear_accumulates_into_bound_grad(C, J):
     torch.manual_seed(1)
-    fc = torch.nn.Linear(64, 10).to(DEV)
+    fc = torch.nn.Linear(C, J).to(DEV)
     fc.weight.grad = torch.ones_like(fc.weight)
     fc.bias.grad = torch.ones_like(fc.bias)
-    x = torch.randn(4, 64, 8, 8, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x = torch.randn(4, C, 8, 8, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     with use_backend("hip"):
         _, out = mnn.pool_linear(x, fc, 8)
     out.float().sum().backward()
     avg = F.avg_pool2d(x.float(), 8).flatten(1)
-    torch.testing.assert_close(fc.bias.grad, torch.ones(10, device=DEV) + 4, atol=1e-5, rtol=0)
-    torch.testing.assert_close(fc.weight.grad, 1 + avg.bfloat16().float().sum(0).expand(10, 64),
+    torch.testing.assert_close(fc.bias.grad, torch.ones(J, device=DEV) + 4, atol=1e-5, rtol=0)
+    torch.testing.assert_close(fc.weight.grad, 1 + avg.bfloat16().float().sum(0).expand(J, C),
                                atol=2e-2, rtol=1e-2)
 
 

@@ -1,0 +1,45 @@
+"""Native NHWC max pooling (csrc/pool.hip) vs PyTorch fp32, and the
+channel-padded stem input (csrc/conv_wgrad.hip::pad_channels)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from mdistiller_ddp_amd.ops import nn as mnn
+from mdistiller_ddp_amd.ops import hip_train
+from mdistiller_ddp_amd.ops.backend import use_backend
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("N,C,H,k,s,p", [(4, 64, 112, 3, 2, 1), (8, 64, 32, 2, 2, 0),
+                                         (3, 16, 15, 3, 2, 1), (2, 256, 8, 2, 2, 0),
+                                         (2, 8, 9, 3, 1, 1)])
+def test_maxpool_fwd_bwd(N, C, H, k, s, p):
+    torch.manual_seed(0)
+    # distinct values: no ties, so the argmax (and gradient) is unambiguous
+    x = torch.randperm(N * C * H * H, device="cuda").float().reshape(N, C, H, H) / (N * C * H * H)
+    x = x.to(torch.bfloat16)
+    x = x + 0 * x  # keep bf16
+    xr = x.float().requires_grad_(True)
+    yr = F.max_pool2d(xr, k, s, p)
+    g = torch.randn_like(yr).to(torch.bfloat16).float()
+    yr.backward(g)
+    xh = x.contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    with use_backend("hip"):
+        y = mnn.max_pool2d(xh, k, s, p)
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    y.backward(g.to(torch.bfloat16))
+    torch.testing.assert_close(y.float(), yr.detach(), atol=0, rtol=0)
+    torch.testing.assert_close(xh.grad.float(), xr.grad, atol=2e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_pad_channels8(dtype):
+    x = torch.randn(3, 3, 17, 19, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
+    y = hip_train.pad_channels8(x)
+    assert y.shape == (3, 8, 17, 19) and y.dtype == torch.bfloat16
+    torch.testing.assert_close(y[:, :3].float(), x.to(torch.bfloat16).float(), atol=0, rtol=0)
+    assert torch.count_nonzero(y[:, 3:]) == 0
+    assert hip_train.pad_channels8(x) is y  # cached for the same version / stream
+    x.add_(1.0)
+    assert hip_train.pad_channels8(x) is not y

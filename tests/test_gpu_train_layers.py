@@ -14,7 +14,8 @@ pytestmark = pytest.mark.gpu
 
 SHAPES = [
     # N, Cin, H, Cout, k, stride, pad, x_grad
-    (16, 3, 32, 32, 3, 1, 1, False),    # stem
+    (16, 3, 32, 32, 3, 1, 1, False),    # stem (input padded to 8 channels)
+    (4, 3, 56, 64, 7, 2, 3, False),     # ImageNet 7x7/s2 stem
     (16, 32, 32, 64, 3, 1, 1, True),
     (16, 64, 32, 64, 3, 1, 1, True),
     (16, 64, 32, 128, 3, 2, 1, True),   # stride 2 dgrad
@@ -154,3 +155,32 @@ def test_pack_cache_matches_per_layer_packing():
             assert st._packs.entries and st._packs._table is not None
         out.append(st.flat.data.clone())
     torch.testing.assert_close(out[0], out[1], rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("shapes", [
+    [(64, 3, 3, 3), (64, 64, 3, 3), (128, 64, 1, 1), (256, 128, 3, 3)],
+    [(64, 3, 7, 7), (32, 24, 3, 3), (40, 72, 1, 1), (512, 512, 3, 3), (24, 8, 5, 5)],
+])
+def test_pack_multi_equals_per_layer_pack(shapes):
+    """The one-launch tiled multi-layer pack writes exactly what the per-layer
+    pack writes (both operand layouts, padding untouched and zero)."""
+    torch.manual_seed(0)
+    cache = hip_train.PackCache()
+    ref, bufs = [], []
+    for (co, ci, kh, kw) in shapes:
+        w = torch.randn(co, ci, kh, kw, device="cuda")
+        wf_r, wt_r, Kp, KpT = hip_train.pack_weights(w, True)
+        ref.append((wf_r, wt_r))
+        # registration-time pack (zeros the padding), then scribble the live part
+        wf, wt, _, _ = hip_train.pack_weights(w, True)
+        K, KT = kh * kw * ci, kh * kw * co
+        wf[:, :K] = 7.0
+        wt[:, :KT] = 7.0
+        cache.entries[id(w)] = dict(weight=w, wf=wf, wt=wt, meta=(co, ci, kh, kw, Kp, KpT))
+        bufs.append((w, wf, wt))
+    cache._dirty = True
+    assert cache.pack_all(torch.device("cuda"))
+    torch.cuda.synchronize()
+    for (wf_r, wt_r), (_, wf, wt) in zip(ref, bufs):
+        assert torch.equal(wf, wf_r)
+        assert torch.equal(wt, wt_r)

@@ -58,7 +58,44 @@ struct ConvParams {
   int N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, K, Kp, M, act;
   int steps_per_split;
   int x_bytes, w_bytes;  // buffer-descriptor ranges (< 2 GiB, checked on the host)
+  int hrows, himgs, hpb; // halo kernels: output rows per image, images, pixels per block
+  // strided dgrad by output parity (glds kernel): gridDim.z = par*par classes x
+  // zsplits K-splits; class (ph, pw) owns the dx pixels whose (ih+pad) % par == ph
+  // (resp. pw) and only the taps kh = ph (mod par), kw = pw (mod par): the
+  // 1 - 1/par^2 of the taps that cannot contribute are never multiplied.
+  int par, zsplits;
 };
+
+// Parity class of the strided-dgrad decomposition.
+struct ParClass {
+  int ih0, iw0, Hc, Wc, Mc;    // first dx row/col of the class, class extent, rows
+  int kh0, kw0, nkh, nkw;      // first tap and tap counts (step par)
+};
+
+__device__ __forceinline__ ParClass par_class(const ConvParams& p, int cls) {
+  // GEMM view of dgrad: p.H/p.W = dy extent, p.Ho/p.Wo = dx extent, p.stride = s
+  ParClass c;
+  const int s = p.par;
+  const int ph = cls / s, pw = cls - (cls / s) * s;
+  c.ih0 = ((ph - p.pad) % s + s) % s;
+  c.iw0 = ((pw - p.pad) % s + s) % s;
+  c.Hc = p.Ho > c.ih0 ? (p.Ho - c.ih0 + s - 1) / s : 0;
+  c.Wc = p.Wo > c.iw0 ? (p.Wo - c.iw0 + s - 1) / s : 0;
+  c.Mc = p.N * c.Hc * c.Wc;
+  c.kh0 = ph;
+  c.kw0 = pw;
+  c.nkh = p.KH > ph ? (p.KH - ph + s - 1) / s : 0;
+  c.nkw = p.KW > pw ? (p.KW - pw + s - 1) / s : 0;
+  return c;
+}
+
+// class row -> global dx pixel index
+__device__ __forceinline__ int par_row(const ConvParams& p, const ParClass& c, int m) {
+  const int hw = c.Hc * c.Wc;
+  const int n = m / hw, r = m - n * hw;
+  const int i = r / c.Wc, j = r - (r / c.Wc) * c.Wc;
+  return (n * p.Ho + c.ih0 + p.par * i) * p.Wo + c.iw0 + p.par * j;
+}
 
 // Buffer loads: 32-bit per-lane byte offsets against a wave-uniform
 // descriptor; an offset past the range returns zeros, which is how padding
@@ -145,7 +182,8 @@ struct ConvSmem {
 // have finished every read of `smem` (barrier) before calling.
 template <int BM, int BN>
 __device__ __forceinline__ void conv_epilogue(const ConvParams& p, const f32x4 (&acc)[BM / 32][BN / 32],
-                                              char* smem, int m0, int n0) {
+                                              char* smem, int m0, int n0, int rows = BM,
+                                              const ParClass* pc = nullptr) {
   constexpr int MI = BM / 32, NI = BN / 32;
   constexpr int CS = ConvSmem<BM, BN>::CS;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -168,19 +206,22 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, const f32x4 (
   const int c8 = tid % TPR;
   const int rr = tid / TPR;
   const int co = n0 + c8 * 8;
-  const bool split = gridDim.z > 1;
+  const int zsplit = pc ? (int)blockIdx.z % p.zsplits : (int)blockIdx.z;
+  const bool split = pc ? p.zsplits > 1 : gridDim.z > 1;
+  const int mlim = pc ? pc->Mc : p.M;
   if ((p.Cout & 7) == 0) {
     if (co >= p.Cout) return;
     float sc[8], bi[8];
     if (!split) load_scale_bias8(p, co, sc, bi);
 #pragma unroll 2
-    for (int r0 = rr; r0 < BM; r0 += RPP) {
-      const int m = m0 + r0;
-      if (m >= p.M) break;
+    for (int r0 = rr; r0 < rows; r0 += RPP) {
+      int m = m0 + r0;
+      if (m >= mlim) break;
+      if (pc) m = par_row(p, *pc, m);
       const float4 lo = *(const float4*)&Cs[r0 * CS + c8 * 8];
       const float4 hi = *(const float4*)&Cs[r0 * CS + c8 * 8 + 4];
       if (split) {
-        float* dst = p.partial + ((int64_t)blockIdx.z * p.M + m) * p.Cout + co;
+        float* dst = p.partial + ((int64_t)zsplit * p.M + m) * p.Cout + co;
         *(float4*)dst = lo;
         *(float4*)(dst + 4) = hi;
       } else {
@@ -189,14 +230,15 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, const f32x4 (
       }
     }
   } else {
-    for (int r0 = rr; r0 < BM; r0 += RPP) {
-      const int m = m0 + r0;
-      if (m >= p.M) break;
+    for (int r0 = rr; r0 < rows; r0 += RPP) {
+      int m = m0 + r0;
+      if (m >= mlim) break;
+      if (pc) m = par_row(p, *pc, m);
       for (int e = 0; e < 8; ++e) {
         if (co + e >= p.Cout) break;
         const float a = Cs[r0 * CS + c8 * 8 + e];
         if (split)
-          p.partial[((int64_t)blockIdx.z * p.M + m) * p.Cout + co + e] = a;
+          p.partial[((int64_t)zsplit * p.M + m) * p.Cout + co + e] = a;
         else
           epilogue_store(p, m, co + e, a);
       }
@@ -494,13 +536,21 @@ conv_glds_kernel(const ConvParams p) {
   const uint32_t wave_off = (uint32_t)__builtin_amdgcn_readfirstlane(wid) * 1024u;
   const int HoWo = p.Ho * p.Wo;
   const bf16_t* const zero = (const bf16_t*)g_zero16;
+  // strided-dgrad parity class (see ConvParams::par); pc == nullptr otherwise
+  const bool PAR = DGRAD && FASTK && p.par > 1;
+  ParClass pcv;
+  if (PAR) {
+    pcv = par_class(p, (int)blockIdx.z / p.zsplits);
+    if (m0 >= pcv.Mc) return;                             // whole block past this class
+  }
+  const int mlim = PAR ? pcv.Mc : p.M;
 
   int a_img[AROWS], a_ih0[AROWS], a_iw0[AROWS];
 #pragma unroll
   for (int j = 0; j < AROWS; ++j) {
     const int m = m0 + trow + 32 * j;
-    const bool ok = m < p.M;
-    const int mm = ok ? m : 0;
+    const bool ok = m < mlim;
+    const int mm = ok ? (PAR ? par_row(p, pcv, m) : m) : 0;
     const int n = mm / HoWo;
     const int r = mm - n * HoWo;
     const int oh = r / p.Wo;
@@ -524,10 +574,11 @@ conv_glds_kernel(const ConvParams p) {
     b_row[j] = p.w + (int64_t)(b_ok[j] ? co : 0) * p.Kp + chunk * 8;
   }
 
-  const int total_steps = p.Kp / BK;
-  const int s_begin = blockIdx.z * p.steps_per_split;
-  const int s_end = min(total_steps, s_begin + p.steps_per_split);
   const int cin_blocks = p.Cin / BK;
+  const int total_steps = PAR ? pcv.nkh * pcv.nkw * cin_blocks : p.Kp / BK;
+  const int zs = PAR ? (int)blockIdx.z % p.zsplits : (int)blockIdx.z;
+  const int s_begin = zs * p.steps_per_split;
+  const int s_end = min(total_steps, s_begin + p.steps_per_split);
 
   // issue every copy of stage s into LDS buffer buf (always NL per wave)
   auto issue = [&](int s, int buf) {
@@ -535,7 +586,13 @@ conv_glds_kernel(const ConvParams p) {
     s = live ? s : s_begin;
     int tap, c0;
     bool kok = live;
-    if (FASTK) {
+    if (PAR) {  // class tap t -> real tap; the weight column follows the real tap
+      const int t = s / cin_blocks, cb = s - t * cin_blocks;
+      const int th = t / max(pcv.nkw, 1), tw = t - th * max(pcv.nkw, 1);
+      tap = (pcv.kh0 + p.par * th) * p.KW + pcv.kw0 + p.par * tw;
+      c0 = cb * BK + chunk * 8;
+      s = tap * cin_blocks + cb;
+    } else if (FASTK) {
       tap = s / cin_blocks;
       c0 = (s - tap * cin_blocks) * BK + chunk * 8;
     } else {
@@ -620,7 +677,7 @@ conv_glds_kernel(const ConvParams p) {
     cbuf = cbuf == 2 ? 0 : cbuf + 1;
   }
   vm_wait_barrier<0>();  // drain the zero-page prefetches; all reads done before the C tile
-  conv_epilogue<BM, BN>(p, acc, smem, m0, n0);
+  conv_epilogue<BM, BN>(p, acc, smem, m0, n0, BM, PAR ? &pcv : nullptr);
 }
 
 // ---------------------------------------------------------------------------
@@ -640,6 +697,13 @@ conv_glds_kernel(const ConvParams p) {
 constexpr int HALO_BM = 128;
 constexpr int HALO_PIECES = 7;                        // patch DMA pieces (32 rows each)
 constexpr int HALO_PROWS = HALO_PIECES * 32;          // 224 patch rows max
+constexpr int HALO1_PIECES = 8;                       // single-chunk kernel: 256 rows
+constexpr int HALO1_PROWS = HALO1_PIECES * 32;
+// A block owns hpb <= 128 output pixels: hrows whole output rows of one
+// image (W * hrows <= 128, hrows | H), or himgs whole images (H*W*himgs <=
+// 128).  Maps whose width does not divide 128 (ImageNet 56 / 28 / 14 / 7)
+// leave the MFMA rows past hpb idle (<= 23 %) instead of falling back to the
+// im2col gather kernels, which re-read every input pixel 9 times.
 
 template <int BN>
 struct HaloSmem {
@@ -665,16 +729,16 @@ conv_halo_kernel(const ConvParams p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  const int m0 = blockIdx.x * BM;
+  const int PB = p.hpb;                       // output pixels of this block (<= BM)
+  const int m0 = blockIdx.x * PB;
   const int n0 = blockIdx.y * BN;
   const uint32_t wave_off = (uint32_t)__builtin_amdgcn_readfirstlane(wid) * 1024u;
   const bf16_t* const zero = (const bf16_t*)g_zero16;
 
-  // block geometry: R output rows per block; IMGS images of RH rows each
+  // block geometry: IMGS images of RH output rows each
   const int W = p.W, H = p.H;
-  const int R = BM / W;
-  const int IMGS = R > H ? R / H : 1;
-  const int RH = R > H ? H : R;
+  const int IMGS = p.himgs;
+  const int RH = p.hrows;
   const int PW = W + 2;                       // patch row length (pixels)
   const int PH = RH + 2;                      // patch rows per image
   const int grow0 = m0 / W;                   // first global output row (n*H + oh)
@@ -749,7 +813,8 @@ conv_halo_kernel(const ConvParams p) {
   int a_prow[MI];
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
-    const int ml = wm * (BM / 2) + i * 16 + frow;   // local output pixel
+    int ml = wm * (BM / 2) + i * 16 + frow;         // local output pixel
+    if (ml >= PB) ml = 0;                           // idle MFMA row (masked at the store)
     const int lr = ml / W, c = ml - (ml / W) * W;   // local output row, column
     const int img = lr / RH, r = lr - img * RH;
     a_prow[i] = (img * PH + r) * PW + c;
@@ -805,7 +870,7 @@ conv_halo_kernel(const ConvParams p) {
     pbuf ^= 1;
   }
   vm_wait_barrier<0>();
-  conv_epilogue<BM, BN>(p, acc, smem, m0, n0);
+  conv_epilogue<BM, BN>(p, acc, smem, m0, n0, PB);
 }
 
 // Single-chunk (Cin == 64) halo variant: the block's one patch is staged
@@ -816,7 +881,7 @@ conv_halo_kernel(const ConvParams p) {
 // workloads.  Still two blocks per CU.
 template <int BN>
 struct Halo1Smem {
-  static constexpr int PATCH = HALO_PROWS * 128;
+  static constexpr int PATCH = HALO1_PROWS * 128;
   static constexpr int BT = BN * 128;
   static constexpr int RING = (81920 - PATCH) / BT > 9 ? 9 : (81920 - PATCH) / BT;
   static constexpr int PIPE = PATCH + RING * BT;
@@ -840,16 +905,16 @@ conv_halo1_kernel(const ConvParams p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  const int m0 = blockIdx.x * BM;
+  const int PB = p.hpb;                       // output pixels of this block (<= BM)
+  const int m0 = blockIdx.x * PB;
   const int n0 = blockIdx.y * BN;
   const uint32_t wave_off = (uint32_t)__builtin_amdgcn_readfirstlane(wid) * 1024u;
   const bf16_t* const zero = (const bf16_t*)g_zero16;
 
-  // block geometry: R output rows per block; IMGS images of RH rows each
+  // block geometry: IMGS images of RH output rows each
   const int W = p.W, H = p.H;
-  const int R = BM / W;
-  const int IMGS = R > H ? R / H : 1;
-  const int RH = R > H ? H : R;
+  const int IMGS = p.himgs;
+  const int RH = p.hrows;
   const int PW = W + 2;                       // patch row length (pixels)
   const int PH = RH + 2;                      // patch rows per image
   const int grow0 = m0 / W;                   // first global output row (n*H + oh)
@@ -859,11 +924,11 @@ conv_halo1_kernel(const ConvParams p) {
   // patch DMA: piece j covers patch rows 32j..32j+31; this thread's row/chunk
   const int trow = tid >> 3;
   const int chunk = (tid & 7) ^ ((trow >> 1) & 7);  // (32j + trow) >> 1 & 7 == trow >> 1 & 7
-  int p_src[HALO_PIECES];                     // element offset of the patch pixel, or -1
+  int p_src[HALO1_PIECES];                    // element offset of the patch pixel, or -1
   {
     const int P = IMGS * PH * PW;
 #pragma unroll
-    for (int j = 0; j < HALO_PIECES; ++j) {
+    for (int j = 0; j < HALO1_PIECES; ++j) {
       const int pr = 32 * j + trow;
       int off = -1;
       if (pr < P) {
@@ -922,7 +987,8 @@ conv_halo1_kernel(const ConvParams p) {
   int a_prow[MI];
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
-    const int ml = wm * (BM / 2) + i * 16 + frow;   // local output pixel
+    int ml = wm * (BM / 2) + i * 16 + frow;         // local output pixel
+    if (ml >= PB) ml = 0;                           // idle MFMA row (masked at the store)
     const int lr = ml / W, c = ml - (ml / W) * W;   // local output row, column
     const int img = lr / RH, r = lr - img * RH;
     a_prow[i] = (img * PH + r) * PW + c;
@@ -956,7 +1022,7 @@ conv_halo1_kernel(const ConvParams p) {
 
   // prologue: the (only) patch, then weight tiles of steps 0 .. RING-2
 #pragma unroll
-  for (int j = 0; j < HALO_PIECES; ++j) issue_piece(c_begin, 0, j);
+  for (int j = 0; j < HALO1_PIECES; ++j) issue_piece(c_begin, 0, j);
 #pragma unroll
   for (int s0 = 0; s0 < RING - 1; ++s0) issue_b(s0, s0);
 #pragma unroll
@@ -968,7 +1034,7 @@ conv_halo1_kernel(const ConvParams p) {
     compute(0, tap % RING, tap);
   }
   vm_wait_barrier<0>();
-  conv_epilogue<BM, BN>(p, acc, smem, m0, n0);
+  conv_epilogue<BM, BN>(p, acc, smem, m0, n0, PB);
 }
 
 // Split-K combine: y = epilogue(sum_z partial[z]) in fixed z order.
@@ -1004,26 +1070,50 @@ __global__ void __launch_bounds__(256) conv_splitk_epilogue(const ConvParams p, 
   }
 }
 
-// 3x3 / stride 1 / pad 1 "same" conv whose rows tile BM = 128 exactly and
-// whose input patch fits HALO_PROWS rows (CIFAR 32x32, 16x16, 8x8 maps).
-bool halo_eligible(const ConvParams& p) {
+// 3x3 / stride 1 / pad 1 "same" conv with Cin % 64 == 0 whose block
+// geometry (see HALO_BM) has a patch of at most `max_rows` rows; fills
+// p.hrows / p.himgs / p.hpb.
+bool halo_geometry(ConvParams& p, int max_rows) {
+  if (p.KH != 3 || p.KW != 3 || p.stride != 1 || p.pad != 1) return false;
+  if (p.Ho != p.H || p.Wo != p.W || p.Cin % BK || p.Kp != 9 * p.Cin) return false;
+  if (p.W > HALO_BM) return false;
+  int imgs = 1, rows = 0;
+  if (p.H * p.W <= HALO_BM) {
+    imgs = HALO_BM / (p.H * p.W);
+    rows = p.H;
+  } else {
+    for (int r = HALO_BM / p.W; r >= 1; --r)
+      if (p.H % r == 0) { rows = r; break; }
+  }
+  if (rows <= 0 || imgs * (rows + 2) * (p.W + 2) > max_rows) return false;
+  const int pb = imgs * rows * p.W;
+  if (4 * pb < 3 * HALO_BM && !(p.H * p.W <= HALO_BM)) return false;  // < 75 % rows busy
+  p.hrows = rows;
+  p.himgs = imgs;
+  p.hpb = pb;
+  return true;
+}
+
+bool halo_eligible(ConvParams& p) {
   static const bool on = [] {
     const char* e = getenv("MDA_CONV_HALO");
     return !(e && e[0] == '0');
   }();
   if (!on) return false;
-  if (p.KH != 3 || p.KW != 3 || p.stride != 1 || p.pad != 1) return false;
-  if (p.Ho != p.H || p.Wo != p.W || p.Cin % BK || p.Kp != 9 * p.Cin) return false;
-  if (p.W > HALO_BM || HALO_BM % p.W) return false;
-  const int R = HALO_BM / p.W;
-  if (R <= p.H ? (p.H % R) : (R % p.H)) return false;
-  const int imgs = R > p.H ? R / p.H : 1, rh = R > p.H ? p.H : R;
-  return imgs * (rh + 2) * (p.W + 2) <= HALO_PROWS;
+  return halo_geometry(p, p.Cin == BK ? HALO1_PROWS : HALO_PROWS);
 }
 
 bool use_halo1() {
   static const bool on = [] {
     const char* e = getenv("MDA_CONV_HALO1");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+bool use_par_dgrad() {
+  static const bool on = [] {
+    const char* e = getenv("MDA_DGRAD_PARITY");
     return !(e && e[0] == '0');
   }();
   return on;
@@ -1096,11 +1186,18 @@ int dispatch(ConvParams& p, int mode, int64_t tile, int64_t splits, hipStream_t 
   if (tile == 0 || splits == 0) mda_conv_plan(p.M, p.Cout, p.Kp, &tile, &splits);
   if (splits > 1 && p.partial == nullptr) return (int)hipErrorInvalidValue;
   int rc;
-  if (halo) {  // halo kernel: split over 64-channel chunks, BM = 128
+  if (halo) {
+    const int nchunks = p.Cin / BK;
+    // the multi-chunk kernel double-buffers patches of at most HALO_PROWS rows
+    if (!(nchunks == 1 && splits == 1 && use_halo1()) &&
+        p.himgs * (p.hrows + 2) * (p.W + 2) > HALO_PROWS)
+      halo = 0;
+  }
+  if (halo) {  // halo kernel: split over 64-channel chunks, hpb pixels per block
     const int nchunks = p.Cin / BK;
     p.steps_per_split = (int)((nchunks + splits - 1) / splits);
     const int bn = p.Cout <= 32 ? 32 : 64;
-    dim3 grid((p.M + HALO_BM - 1) / HALO_BM, (p.Cout + bn - 1) / bn, (int)splits);
+    dim3 grid((p.M + p.hpb - 1) / p.hpb, (p.Cout + bn - 1) / bn, (int)splits);
     if (nchunks == 1 && splits == 1 && use_halo1()) {
       if (bn == 32) {
         if (halo == 2) hipLaunchKernelGGL((conv_halo1_kernel<32, true>), grid, dim3(256), 0, st, p);
@@ -1115,6 +1212,25 @@ int dispatch(ConvParams& p, int mode, int64_t tile, int64_t splits, hipStream_t 
     } else {
       if (halo == 2) hipLaunchKernelGGL((conv_halo_kernel<64, true>), grid, dim3(256), 0, st, p);
       else hipLaunchKernelGGL((conv_halo_kernel<64, false>), grid, dim3(256), 0, st, p);
+    }
+    rc = (int)hipGetLastError();
+  } else if (p.par > 1) {
+    // strided dgrad by parity class (glds kernel, Cout % 64 == 0 only)
+    const int s2 = p.par * p.par;
+    const int steps = ((p.KH + p.par - 1) / p.par) * ((p.KW + p.par - 1) / p.par) * (p.Cin / BK);
+    p.zsplits = (int)splits;
+    p.steps_per_split = (int)((steps + splits - 1) / splits);
+    const int bm = (int)(tile / 1000), bn = (int)(tile % 1000);
+    const int mc = p.N * ((p.Ho + p.par - 1) / p.par) * ((p.Wo + p.par - 1) / p.par);
+    dim3 grid((mc + bm - 1) / bm, (p.Cout + bn - 1) / bn, s2 * (int)splits);
+    switch (tile) {
+      case 128128: hipLaunchKernelGGL((conv_glds_kernel<128, 128, LOAD_DGRAD_FAST>), grid, dim3(256), 0, st, p); break;
+      case 128064: hipLaunchKernelGGL((conv_glds_kernel<128, 64, LOAD_DGRAD_FAST>), grid, dim3(256), 0, st, p); break;
+      case 128032: hipLaunchKernelGGL((conv_glds_kernel<128, 32, LOAD_DGRAD_FAST>), grid, dim3(256), 0, st, p); break;
+      case 64128: hipLaunchKernelGGL((conv_glds_kernel<64, 128, LOAD_DGRAD_FAST>), grid, dim3(256), 0, st, p); break;
+      case 64064: hipLaunchKernelGGL((conv_glds_kernel<64, 64, LOAD_DGRAD_FAST>), grid, dim3(256), 0, st, p); break;
+      case 64032: hipLaunchKernelGGL((conv_glds_kernel<64, 32, LOAD_DGRAD_FAST>), grid, dim3(256), 0, st, p); break;
+      default: return (int)hipErrorInvalidValue;
     }
     rc = (int)hipGetLastError();
   } else {
@@ -1153,6 +1269,8 @@ MDA_API int mda_conv_fwd(const void* x, const void* w, const float* scale, const
   p.N = N; p.H = H; p.W = W; p.Cin = Cin; p.Ho = Ho; p.Wo = Wo; p.Cout = Cout; p.KH = KH;
   p.KW = KW; p.stride = stride; p.pad = pad; p.K = KH * KW * Cin; p.Kp = Kp; p.M = N * Ho * Wo;
   p.act = act;
+  p.par = 0;
+  p.zsplits = 1;
   int mode = (Cin % BK == 0) ? LOAD_FAST : (Cin % 8 == 0 ? LOAD_VEC8 : LOAD_SCALAR);
   return dispatch(p, mode, tile, splits, st, halo_eligible(p) ? 1 : 0);
 }
@@ -1174,6 +1292,10 @@ MDA_API int mda_conv_dgrad(const void* dy, const void* wt, void* dx, float* part
   p.KW = KW; p.stride = stride; p.pad = pad; p.K = KH * KW * Cout; p.Kp = Kp; p.M = N * H * W;
   p.act = 0;
   int mode = (Cout % BK == 0) ? LOAD_DGRAD_FAST : LOAD_DGRAD_VEC8;
+  p.par = 0;
+  p.zsplits = 1;
+  // strided dgrad: one GEMM per output-parity class with only its taps
+  if (stride > 1 && mode == LOAD_DGRAD_FAST && use_glds() && use_par_dgrad()) p.par = (int)stride;
   // stride-1 3x3 pad-1 dgrad is a "same" conv of dy with the mirrored taps
   return dispatch(p, mode, tile, splits, st, halo_eligible(p) ? 2 : 0);
 }

@@ -143,7 +143,7 @@ def _pool_fc_native(x: torch.Tensor, fc: nn.Linear, kernel) -> bool:
     N, C, H, W = x.shape
     if kernel not in (None, H) or H != W or fc.in_features != C or fc.weight.dtype != torch.float32:
         return False
-    if C > 8192 or fc.out_features * C > (1 << 20) or N > 16384:
+    if C > 8192 or fc.out_features * C > (1 << 24) or N > 16384:
         return False
     if x.dtype == torch.bfloat16:
         return True

@@ -69,3 +69,46 @@ def test_teacher_forward_matches_torch():
             out, feats = m(x)
     rel = (out.float() - ref).norm() / ref.norm()
     assert rel < 3e-2, rel
+
+
+DGRAD_SHAPES = [
+    # N, Cin, H, Cout, k, stride, pad   (dgrad: dx of conv(x))
+    (4, 64, 32, 128, 3, 2, 1),    # parity classes 1/2/2/4 taps
+    (2, 64, 56, 128, 3, 2, 1),    # ImageNet layer2 transition
+    (3, 32, 15, 64, 3, 2, 1),     # odd extent
+    (2, 64, 32, 128, 1, 2, 0),    # 1x1 / s2: three classes have no taps
+    (2, 8, 30, 64, 7, 2, 3),      # 7x7 / s2 (stem-like)
+    (2, 64, 16, 64, 3, 1, 1),     # stride 1 (halo)
+    (2, 64, 56, 64, 3, 1, 1),     # stride 1, width 56 (halo, 112-pixel blocks)
+    (2, 128, 28, 128, 3, 1, 1),   # width 28, two channel chunks
+    (2, 128, 14, 128, 3, 1, 1),   # width 14 (98-pixel blocks)
+    (4, 256, 7, 256, 3, 1, 1),    # 7x7 maps, two images per block
+]
+
+
+@pytest.mark.parametrize("shape", DGRAD_SHAPES)
+def test_conv_dgrad_matches_autograd(shape):
+    from mdistiller_ddp_amd.ops import hip_train
+    N, Cin, H, Cout, k, s, p = shape
+    torch.manual_seed(0)
+    w = torch.randn(Cout, Cin, k, k, device="cuda") / (Cin * k * k) ** 0.5
+    x = torch.randn(N, Cin, H, H, device="cuda").requires_grad_(True)
+    y = F.conv2d(x, w.to(torch.bfloat16).float(), stride=s, padding=p)
+    g = torch.randn_like(y).to(torch.bfloat16).float()
+    y.backward(g)
+    dx = hip_train.conv_dgrad(g.to(torch.bfloat16), w, x.shape, s, p)
+    torch.testing.assert_close(dx.float(), x.grad, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 56, 64, 3, 1, 1), (2, 128, 28, 128, 3, 1, 1),
+                                   (2, 256, 14, 256, 3, 1, 1), (4, 512, 7, 512, 3, 1, 1)])
+def test_conv_forward_imagenet_widths(shape):
+    """Halo kernel with blocks of whole rows that do not fill 128 pixels."""
+    N, Cin, H, Cout, k, s, p = shape
+    torch.manual_seed(0)
+    conv = nn.Conv2d(Cin, Cout, k, s, p, bias=False).cuda().eval()
+    x = torch.randn(N, Cin, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    ref = F.conv2d(x.float(), conv.weight.to(torch.bfloat16).float(), stride=s, padding=p)
+    with torch.no_grad():
+        out, _ = hip_layers.conv_bn_act(x, conv, None, "none", None, False)
+    torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=3e-2)

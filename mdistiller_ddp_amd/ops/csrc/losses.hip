@@ -115,46 +115,64 @@ logit_loss_kernel(const TS* __restrict__ s, const TT* __restrict__ t,
         kd_row = wave_sum(kl) * T * T;
       } else {
         // ---- DKD: TCKD (binary gt/other) + NCKD (softmax over non-gt) ---
-        float zs = 0.f, zt = 0.f, zs_o = 0.f, zt_o = 0.f, es_g = 0.f, et_g = 0.f;
+        // The non-target softmaxes are normalised by their OWN maxima (the
+        // reference's -1000*gt_mask does the same): with a dominant target
+        // logit (gap > ~88 at T = 1) every non-target exp under the full
+        // maximum underflows to 0 and log(0) made the loss infinite.
+        float ms_o = -INFINITY, mt_o = -INFINITY;
 #pragma unroll
         for (int i = 0; i < NPL; ++i) {
-          int c = lane + 64 * i;
-          float es = __expf(sv[i] * inv_T - ms);
-          float et = __expf(tv[i] * inv_T - mt);
-          if (c == y) { es_g = es; et_g = et; }
-          else { zs_o += es; zt_o += et; }
+          if (lane + 64 * i != y) {
+            ms_o = fmaxf(ms_o, sv[i] * inv_T);
+            mt_o = fmaxf(mt_o, tv[i] * inv_T);
+          }
+        }
+        ms_o = wave_max(ms_o);
+        mt_o = wave_max(mt_o);
+        float zs_o = 0.f, zt_o = 0.f;
+#pragma unroll
+        for (int i = 0; i < NPL; ++i) {
+          if (lane + 64 * i != y) {
+            zs_o += __expf(sv[i] * inv_T - ms_o);
+            zt_o += __expf(tv[i] * inv_T - mt_o);
+          }
         }
         zs_o = wave_sum(zs_o);
         zt_o = wave_sum(zt_o);
-        es_g = wave_sum(es_g);
-        et_g = wave_sum(et_g);
-        zs = zs_o + es_g;
-        zt = zt_o + et_g;
-        // binary distributions
-        const float ps_g = es_g / zs, ps_o = zs_o / zs;
-        const float pt_g = et_g / zt, pt_o = zt_o / zt;
-        float tckd = 0.f;
-        if (pt_g > 0.f) tckd += pt_g * (__logf(pt_g) - __logf(ps_g));
-        if (pt_o > 0.f) tckd += pt_o * (__logf(pt_o) - __logf(ps_o));
-        // non-target distributions
         const float lzs_o = __logf(zs_o), lzt_o = __logf(zt_o);
+        // binary (target, other) distributions in the log domain:
+        // log P(other) = log sum_{j != y} exp(z_j) = m_o + log Z_o
+        const float sy = s_y * inv_T;
+        float ty = 0.f;
+#pragma unroll
+        for (int i = 0; i < NPL; ++i)
+          if (lane + 64 * i == y) ty = tv[i] * inv_T;
+        ty = wave_sum(ty);
+        const float ls_o_raw = ms_o + lzs_o, lt_o_raw = mt_o + lzt_o;
+        const float ls_n = fmaxf(sy, ls_o_raw) + __logf(1.f + __expf(-fabsf(sy - ls_o_raw)));
+        const float lt_n = fmaxf(ty, lt_o_raw) + __logf(1.f + __expf(-fabsf(ty - lt_o_raw)));
+        const float lps_g = sy - ls_n, lps_o = ls_o_raw - ls_n;
+        const float lpt_g = ty - lt_n, lpt_o = lt_o_raw - lt_n;
+        const float ps_g = __expf(lps_g), pt_g = __expf(lpt_g);
+        float tckd = 0.f;
+        if (pt_g > 0.f) tckd += pt_g * (lpt_g - lps_g);
+        const float pt_o = __expf(lpt_o);
+        if (pt_o > 0.f) tckd += pt_o * (lpt_o - lps_o);
         float nckd = 0.f;
         const float gs = kd_w * T * invB;
-        const float tck_coef = (pt_g - ps_g) / ps_o;  // for j != gt: p_j * coef
+        const float tck = pt_g - ps_g;  // d TCKD / d z_j = q_j (pt_g - ps_g) for j != gt
 #pragma unroll
         for (int i = 0; i < NPL; ++i) {
           int c = lane + 64 * i;
           if (c < C) {
-            float zsj = sv[i] * inv_T - ms, ztj = tv[i] * inv_T - mt;
             float gz;
             if (c == y) {
               gz = alpha * (ps_g - pt_g);
             } else {
-              float lq = zsj - lzs_o, lp = ztj - lzt_o;
-              float ph = __expf(lp), qh = __expf(lq);
+              const float lq = sv[i] * inv_T - ms_o - lzs_o, lp = tv[i] * inv_T - mt_o - lzt_o;
+              const float ph = __expf(lp), qh = __expf(lq);
               nckd += ph * (lp - lq);
-              float pj = __expf(zsj) / zs;
-              gz = alpha * pj * tck_coef + beta * (qh - ph);
+              gz = alpha * qh * tck + beta * (qh - ph);
             }
             io<TG>::st(g_kd, base + c, gs * gz);
           }

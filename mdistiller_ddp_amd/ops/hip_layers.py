@@ -67,7 +67,45 @@ def conv_supported(x, conv, bn) -> bool:
 
 
 def bn_supported(x, bn) -> bool:
-    return False
+    """Inference BN (+res) (+act) on an existing activation: frozen statistics
+    -> per-channel scale/shift (cached per version), one ``mda_bn_apply``."""
+    if not (x.is_cuda and x.dim() == 4 and isinstance(bn, nn.BatchNorm2d)):
+        return False
+    if bn.training or not bn.track_running_stats or x.shape[1] % 8:
+        return False
+    if torch.is_grad_enabled() and (x.requires_grad or (bn.weight is not None and bn.weight.requires_grad)):
+        return False
+    return x.dtype == torch.bfloat16 or _autocast_bf16()
+
+
+@torch.no_grad()
+def _bn_affine(bn):
+    key = tuple(t._version for t in (bn.weight, bn.bias, bn.running_mean, bn.running_var)
+                if t is not None)
+    if bn.weight is not None and bn.weight.requires_grad:
+        key = key + (("gen", _GEN[0]),)
+    cache = getattr(bn, "_mda_affine", None)
+    if cache is not None and cache[0] == key:
+        return cache[1], cache[2]
+    C = bn.running_mean.numel()
+    dev = bn.running_mean.device
+    g = bn.weight.float() if bn.weight is not None else torch.ones(C, device=dev)
+    b = bn.bias.float() if bn.bias is not None else torch.zeros(C, device=dev)
+    sc = (g / torch.sqrt(bn.running_var.float() + bn.eps)).contiguous()
+    sh = (b - bn.running_mean.float() * sc).contiguous()
+    bn._mda_affine = (key, sc, sh)
+    return sc, sh
+
+
+def bn_act(x, bn, act, residual, want_preact):
+    sc, sh = _bn_affine(bn)
+    x = _nhwc_bf16(x)
+    N, C, H, W = x.shape
+    out = torch.empty_like(x)
+    pre = torch.empty_like(x) if want_preact else None
+    res = _nhwc_bf16(residual) if residual is not None else None
+    _ext.call("mda_bn_apply", x, sc, sh, res, out, pre, N * H * W, C, _ACT[act])
+    return out, pre
 
 
 # Bumped by every training step (and checkpoint load): the native optimizer

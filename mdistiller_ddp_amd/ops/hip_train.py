@@ -476,6 +476,176 @@ def conv_wgrad(x, dy, weight_shape, stride, pad):
     return out
 
 
+# ---------------------------------------------------------------------------
+# Pre-activation networks (WRN, reference models/cifar/wrn.py:39-48): convs
+# WITHOUT a following BN (residual add / activation fused into the conv
+# epilogue) and BN + residual + activation on an existing tensor.
+
+def conv_train_supported(x, conv) -> bool:
+    """Dense conv (no BN after it) of a trainable layer on the native kernels."""
+    if not (x.is_cuda and x.dim() == 4 and isinstance(conv, nn.Conv2d) and conv.groups == 1):
+        return False
+    if conv.bias is not None or conv.dilation != (1, 1) or conv.padding_mode != "zeros":
+        return False
+    if conv.stride[0] != conv.stride[1] or not isinstance(conv.padding, tuple) or conv.padding[0] != conv.padding[1]:
+        return False
+    if conv.kernel_size[0] != conv.kernel_size[1]:
+        return False
+    if conv.out_channels % 8 or (conv.in_channels % 8 and x.requires_grad):
+        return False
+    if not conv.weight.requires_grad:
+        return False
+    if x.dtype != torch.bfloat16 and not (torch.is_autocast_enabled("cuda")
+                                          and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+        return False
+    return torch.is_grad_enabled()
+
+
+def _act_mask(dout, out, act):
+    if act == 1:
+        return torch.where(out > 0, dout, torch.zeros((), dtype=dout.dtype, device=dout.device))
+    if act == 2:
+        return torch.where((out > 0) & (out < 6), dout, torch.zeros((), dtype=dout.dtype, device=dout.device))
+    return dout
+
+
+class _ConvTrain(torch.autograd.Function):
+    """out = act(conv(x) + residual): ONE conv launch (residual and activation in
+    the epilogue); backward = activation mask (if any) + dgrad + wgrad."""
+
+    @staticmethod
+    def forward(ctx, x, weight, residual, meta, want_preact):
+        stride, pad, act = meta
+        need_dx = ctx.needs_input_grad[0]
+        cin_w = weight.shape[1]
+        chpad = (not need_dx) and needs_channel_pad(cin_w)
+        x = pad_channels8(x) if chpad else _cl_bf16(x)
+        N, Cin, H, W = x.shape
+        Cout, _, KH, KW = weight.shape
+        Ho = (H + 2 * pad - KH) // stride + 1
+        Wo = (W + 2 * pad - KW) // stride + 1
+        M = N * Ho * Wo
+        Kp = (KH * KW * Cin + 63) // 64 * 64
+        KpT = (KH * KW * Cout + 63) // 64 * 64
+        dev = x.device
+        packs = _ACTIVE[0]
+        ent = packs.lookup(weight, need_dx) if (packs is not None and not chpad) else None
+        if chpad:
+            wf = torch.empty(Cout, Kp, dtype=torch.bfloat16, device=dev)
+            wt = None
+            _ext.call("mda_pack_conv_weights_pad", weight.detach().contiguous(), wf, Cout, cin_w,
+                      Cin, KH, KW, Kp)
+        elif ent is not None:
+            wf, wt = ent["wf"], ent["wt"]
+        else:
+            wf = torch.empty(Cout, Kp, dtype=torch.bfloat16, device=dev)
+            wt = torch.empty(Cin, KpT, dtype=torch.bfloat16, device=dev) if need_dx else None
+            wc = weight.detach()
+            if packs is not None and wc.is_contiguous() and wc.dtype == torch.float32:
+                packs.register(weight, wf, wt, Cout, Cin, KH, KW, Kp, KpT)
+            _ext.call("mda_pack_conv_weights", wc.contiguous(), wf, wt, Cout, Cin, KH, KW, Kp, KpT)
+        from .hip_layers import conv_plan
+        tile, splits = conv_plan(M, Cout, Kp)
+        part = torch.empty(splits * M * Cout, dtype=torch.float32, device=dev) if splits > 1 else None
+        res = _cl_bf16(residual) if residual is not None else None
+        out = torch.empty((N, Cout, Ho, Wo), dtype=torch.bfloat16, device=dev,
+                          memory_format=torch.channels_last)
+        pre = torch.empty_like(out) if (want_preact or act != 0) else None
+        _ext.call("mda_conv_fwd", x, wf, None, None, res, out, pre, part, N, H, W, Cin, Ho, Wo,
+                  Cout, KH, KW, stride, pad, Kp, act, tile, splits)
+        ctx.save_for_backward(x, wt, weight, pre if act != 0 else None)
+        ctx.meta = (N, Cin, H, W, Cout, Ho, Wo, KH, KW, stride, pad, Kp, KpT, act)
+        ctx.cin_keep = cin_w if chpad else 0
+        ctx.has_res = residual is not None
+        return out, (pre if want_preact else None)
+
+    @staticmethod
+    def backward(ctx, dout, dpre):
+        x, wt, weight, pre = ctx.saved_tensors
+        N, Cin, H, W, Cout, Ho, Wo, KH, KW, stride, pad, Kp, KpT, act = ctx.meta
+        M = N * Ho * Wo
+        dev = x.device
+        dz = None
+        if dout is not None:
+            dz = _act_mask(_cl_bf16(dout), pre, act)
+        if dpre is not None:
+            dz = _cl_bf16(dpre) if dz is None else dz + _cl_bf16(dpre)
+        dz = _cl_bf16(dz)
+        dres = dz if (ctx.has_res and ctx.needs_input_grad[2]) else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty((N, Cin, H, W), dtype=torch.bfloat16, device=dev,
+                             memory_format=torch.channels_last)
+            from .hip_layers import conv_plan
+            tile, splits = conv_plan(N * H * W, Cin, KpT)
+            part = torch.empty(splits * N * H * W * Cin, dtype=torch.float32, device=dev) if splits > 1 else None
+            _ext.call("mda_conv_dgrad", dz, wt, dx, part, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
+                      stride, pad, KpT, tile, splits)
+        dw = None
+        if ctx.needs_input_grad[1]:
+            sp = _wgrad_splits(M, Cout, Kp)
+            part = torch.empty(sp * Cout * Kp, dtype=torch.float32, device=dev)
+            direct_w = weight.grad is not None and weight.grad.is_contiguous()
+            target = weight.grad if direct_w else torch.empty_like(weight, memory_format=torch.contiguous_format)
+            _ext.call("mda_conv_wgrad", x, dz, part, target, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
+                      stride, pad, Kp, sp, 1.0, 1 if direct_w else 0, ctx.cin_keep)
+            dw = None if direct_w else target
+            if direct_w:
+                notify_grad(weight)
+        return dx, dw, dres, None, None
+
+
+def conv_act_train(x, conv, act, residual, want_preact):
+    out, pre = _ConvTrain.apply(x, conv.weight, residual,
+                                (conv.stride[0], conv.padding[0], _ACT[act]), bool(want_preact))
+    return out, pre
+
+
+def bn_train_supported(x, bn) -> bool:
+    if not (x.is_cuda and x.dim() == 4 and isinstance(bn, nn.BatchNorm2d)):
+        return False
+    if not bn.training or not bn.track_running_stats or bn.momentum is None:
+        return False
+    if bn.weight is None or bn.bias is None or x.shape[1] % 8 or x.shape[1] > 2048:
+        return False
+    if x.dtype != torch.bfloat16 and not (torch.is_autocast_enabled("cuda")
+                                          and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+        return False
+    return torch.is_grad_enabled()
+
+
+class _BNActTrain(torch.autograd.Function):
+    """Training BN (+ residual) (+ activation) of an existing activation: batch
+    statistics (+ running-stat update) and apply, 3 launches; backward 3."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, residual, bn, act, want_preact):
+        y = _cl_bf16(x)
+        N, C, H, W = y.shape
+        M = N * H * W
+        out, pre, res, stats = _bn_train_forward(y, M, C, gamma, beta, bn, residual, act,
+                                                 want_preact)
+        ctx.save_for_backward(y, res, stats, gamma, beta)
+        ctx.meta = (M, C, act)
+        ctx.has_res = residual is not None
+        return out, pre
+
+    @staticmethod
+    def backward(ctx, dout, dpre):
+        y, res, stats, gamma, beta = ctx.saved_tensors
+        M, C, act = ctx.meta
+        dy, dres, dgamma, dbeta = _bn_train_backward(ctx, dout, dpre, y, res, stats, gamma, beta,
+                                                     M, C, act)
+        if not (ctx.has_res and ctx.needs_input_grad[3]):
+            dres = None
+        return dy, dgamma, dbeta, dres, None, None, None
+
+
+def bn_act_train(x, bn, act, residual, want_preact):
+    out, pre = _BNActTrain.apply(x, bn.weight, bn.bias, residual, bn, _ACT[act], bool(want_preact))
+    return out, pre
+
+
 def conv_bn_act_train(x, conv, bn, act, residual, want_preact):
     meta = (conv.stride[0], conv.padding[0], _ACT[act])
     if conv.groups != 1:

@@ -52,6 +52,8 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d | None = No
         from . import hip_train
         if _TRAIN_KERNELS["on"] and hip_train.train_supported(x, conv, bn):
             return hip_train.conv_bn_act_train(x, conv, bn, act, residual, want_preact)
+        if _TRAIN_KERNELS["on"] and bn is None and hip_train.conv_train_supported(x, conv):
+            return hip_train.conv_act_train(x, conv, act, residual, want_preact)
     # the raw convolution (not ``conv(x)``): modules that route their own
     # forward through this op -- e.g. the detection Conv2d with a norm child --
     # must not recurse
@@ -71,6 +73,9 @@ def bn_act(x: torch.Tensor, bn: nn.BatchNorm2d, act: str = "relu",
         from . import hip_layers
         if hip_layers.bn_supported(x, bn):
             return hip_layers.bn_act(x, bn, act, residual, want_preact)
+        from . import hip_train
+        if _TRAIN_KERNELS["on"] and hip_train.bn_train_supported(x, bn):
+            return hip_train.bn_act_train(x, bn, act, residual, want_preact)
     y = _bn(x, bn)
     if residual is not None:
         y = y + residual

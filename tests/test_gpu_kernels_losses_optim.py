@@ -48,20 +48,24 @@ def test_ce_kd(B, C, dtype):
         torch.testing.assert_close(a, b, atol=tol * max(1.0, b.abs().max().item()), rtol=tol)
 
 
-@pytest.mark.parametrize("B,C", [(64, 100), (9, 1000), (33, 200)])
+@pytest.mark.parametrize("B,C,gap,T", [(64, 100, 5.0, 4.0), (9, 1000, 5.0, 4.0), (33, 200, 5.0, 4.0),
+                                       (16, 1000, 150.0, 1.0), (16, 100, 400.0, 4.0)])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_ce_dkd(B, C, dtype):
+def test_ce_dkd(B, C, gap, T, dtype):
+    """Includes near-one-hot teachers (target gap >> 88 at T): the non-target
+    softmax must be normalised by its own maximum, as the reference's
+    -1000*gt_mask does, or every non-target probability underflows."""
     torch.manual_seed(1)
     s = (torch.randn(B, C, device=DEV) * 3).to(dtype)
     t = (torch.randn(B, C, device=DEV) * 3).to(dtype)
     y = torch.randint(0, C, (B,), device=DEV)
-    t[torch.arange(B), y] += 5  # confident teacher (realistic)
+    t[torch.arange(B), y] += gap  # confident teacher
 
     def ref(s_, t_, y_):
-        return L.cross_entropy(s_, y_), L.dkd_loss_ref(s_, t_.float(), y_, 1.0, 8.0, 4.0)
+        return L.cross_entropy(s_, y_), L.dkd_loss_ref(s_, t_.float(), y_, 1.0, 8.0, T)
 
     def hip(s_, t_, y_):
-        return L.ce_dkd(s_, t_, y_, 1.0, 1.0, 8.0, 4.0)
+        return L.ce_dkd(s_, t_, y_, 1.0, 1.0, 8.0, T)
 
     r = _ref_grads(ref, s, t, y)
     h = _hip_grads(hip, s, t, y)

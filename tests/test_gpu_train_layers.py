@@ -100,14 +100,15 @@ def test_dgrad_wgrad_kernels_exact_inputs(shape):
         assert rel_x < 1e-2, rel_x
 
 
-def test_student_train_step_uses_native_path():
-    """A full resnet8x4 training forward/backward through the native path vs an
+@pytest.mark.parametrize("name", ["resnet8x4", "wrn_16_2", "vgg8", "MobileNetV2", "ShuffleV2"])
+def test_student_train_step_uses_native_path(name):
+    """A full student training forward/backward through the native path vs an
     fp32 PyTorch reference: its gradient error must be in the same band as the
     stock bf16 (MIOpen) path's."""
-    from mdistiller_ddp_amd.models.cifar import resnet8x4
+    from mdistiller_ddp_amd.models import cifar_model_dict
     from mdistiller_ddp_amd.ops.backend import use_backend
     torch.manual_seed(0)
-    m1 = resnet8x4(num_classes=100).cuda().to(memory_format=torch.channels_last)
+    m1 = cifar_model_dict[name][0](num_classes=100).cuda().to(memory_format=torch.channels_last)
     m2 = copy.deepcopy(m1)
     m3 = copy.deepcopy(m1)
     x = torch.randn(32, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
@@ -184,3 +185,34 @@ def test_pack_multi_equals_per_layer_pack(shapes):
     for (wf_r, wt_r), (_, wf, wt) in zip(ref, bufs):
         assert torch.equal(wf, wf_r)
         assert torch.equal(wt, wt_r)
+
+
+def test_wrn_convs_take_native_training_path():
+    """Pre-activation WRN: every conv (no BN after it) and every BN+ReLU of a
+    training forward dispatches to the native kernels."""
+    from mdistiller_ddp_amd.models import cifar_model_dict
+    from mdistiller_ddp_amd.ops.backend import use_backend
+    calls = {"conv": 0, "bn": 0}
+    orig_c, orig_b = hip_train.conv_act_train, hip_train.bn_act_train
+
+    def cc(*a, **k):
+        calls["conv"] += 1
+        return orig_c(*a, **k)
+
+    def cb(*a, **k):
+        calls["bn"] += 1
+        return orig_b(*a, **k)
+
+    hip_train.conv_act_train, hip_train.bn_act_train = cc, cb
+    try:
+        m = cifar_model_dict["wrn_16_2"][0](num_classes=100).cuda().to(memory_format=torch.channels_last)
+        x = torch.randn(8, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+        with use_backend("hip"), torch.autocast("cuda", dtype=torch.bfloat16):
+            logits, _ = m(x)
+        logits.float().sum().backward()
+    finally:
+        hip_train.conv_act_train, hip_train.bn_act_train = orig_c, orig_b
+    n_conv = sum(1 for mod in m.modules() if isinstance(mod, nn.Conv2d))
+    n_bn = sum(1 for mod in m.modules() if isinstance(mod, nn.BatchNorm2d))
+    assert calls["conv"] == n_conv - sum(1 for b in m.modules() if hasattr(b, "bn2")), calls
+    assert calls["bn"] == n_bn - sum(1 for b in m.modules() if hasattr(b, "bn2")), calls

@@ -66,11 +66,8 @@ class OFD(Distiller):
         self.ce_loss_weight = cfg.OFD.LOSS.CE_WEIGHT
         self.feat_loss_weight = cfg.OFD.LOSS.FEAT_WEIGHT
         self._teacher_train_bn = bool(cfg.OFD.TEACHER_TRAIN_BN)
-        # Train-mode teacher BN under a captured bf16 step drifted from eager and
-        # went non-finite on MI355X (eager bf16 tracks fp32 eager to 2e-4, and
-        # the eval-mode teacher captures fine): keep this mode eager.
-        # Evidence: scripts/gpu_ab_ofd.sh, profiles/r1_ofd_graph_ab.md.
-        self.graph_capturable = not self._teacher_train_bn
+        # the train-mode teacher BN runs on the native capture-safe kernels, so
+        # the whole step is captured (round 1 had to run this mode eagerly)
         self.init_ofd_modules(self.teacher.get_stage_channels()[1:],
                               self.student.get_stage_channels()[1:],
                               self.teacher.get_bn_before_relu(),

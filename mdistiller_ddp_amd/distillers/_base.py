@@ -95,12 +95,11 @@ class Distiller(nn.Module):
         Returns a :class:`~..runtime.streams.TeacherOutput`; call ``.get()``
         after issuing the student forward so the two overlap on the GPU.
         """
-        if self._teacher_train_bn:  # OFD (SURVEY D17): BN stats update, same stream
-            # fp32 even inside a bf16 step: bf16 MIOpen train-mode BN replayed
-            # from a hipGraph drifted from eager and went non-finite
-            # (scripts/gpu_ab_ofd.sh); fp32 graph == fp32 eager exactly.
-            with torch.no_grad(), torch.autocast("cuda", enabled=False):
-                return streams.TeacherOutput(self.teacher(image.float()))
+        # OFD (SURVEY D17) keeps the teacher's BN in training mode: on the GPU its
+        # layers run as native conv + batch-statistics BN (ops/hip_train.py::
+        # conv_trainbn_nograd), which is capture-safe -- MIOpen's bf16 train-mode
+        # BN replayed from a hipGraph went non-finite run to run (r1 evidence,
+        # profiles/r1_ofd_graph_ab.md)
         return streams.run_teacher_async(self.teacher, image)
 
     def forward_train(self, **kwargs):

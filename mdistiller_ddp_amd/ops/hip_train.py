@@ -646,6 +646,42 @@ def bn_act_train(x, bn, act, residual, want_preact):
     return out, pre
 
 
+# ---------------------------------------------------------------------------
+# Frozen conv + TRAIN-mode BN without autograd: the OFD teacher (reference
+# distillers/OFD.py:114-121 keeps the teacher's BN in training mode, so its
+# forward normalises with batch statistics and updates running statistics).
+# MIOpen's train-mode BN replayed from a hipGraph in bf16 went non-finite run
+# to run (profiles/r1_ofd_graph_ab.md); these kernels are capture-safe.
+
+def trainbn_nograd_supported(x, conv, bn) -> bool:
+    if torch.is_grad_enabled() and (x.requires_grad or conv.weight.requires_grad):
+        return False
+    if not (x.is_cuda and x.dim() == 4 and isinstance(conv, nn.Conv2d) and conv.groups == 1):
+        return False
+    if bn is None or not bn.training or not bn.track_running_stats or bn.momentum is None:
+        return False
+    if conv.bias is not None or conv.dilation != (1, 1) or conv.padding_mode != "zeros":
+        return False
+    if conv.stride[0] != conv.stride[1] or not isinstance(conv.padding, tuple) or conv.padding[0] != conv.padding[1]:
+        return False
+    if conv.kernel_size[0] != conv.kernel_size[1] or conv.out_channels % 8 or conv.out_channels > 2048:
+        return False
+    return x.dtype == torch.bfloat16 or (torch.is_autocast_enabled("cuda")
+                                         and torch.get_autocast_dtype("cuda") == torch.bfloat16)
+
+
+@torch.no_grad()
+def conv_trainbn_nograd(x, conv, bn, act, residual, want_preact):
+    from .hip_layers import conv_bn_act as conv_infer
+    y, _ = conv_infer(x, conv, None, "none", None, False)  # packed once per weight version
+    N, C, Ho, Wo = y.shape
+    gamma = bn.weight if bn.weight is not None else torch.ones(C, device=y.device)
+    beta = bn.bias if bn.bias is not None else torch.zeros(C, device=y.device)
+    out, pre, _, _ = _bn_train_forward(y, N * Ho * Wo, C, gamma, beta, bn, residual, _ACT[act],
+                                       want_preact)
+    return out, pre
+
+
 def conv_bn_act_train(x, conv, bn, act, residual, want_preact):
     meta = (conv.stride[0], conv.padding[0], _ACT[act])
     if conv.groups != 1:

@@ -54,6 +54,8 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d | None = No
             return hip_train.conv_bn_act_train(x, conv, bn, act, residual, want_preact)
         if _TRAIN_KERNELS["on"] and bn is None and hip_train.conv_train_supported(x, conv):
             return hip_train.conv_act_train(x, conv, act, residual, want_preact)
+        if hip_train.trainbn_nograd_supported(x, conv, bn):
+            return hip_train.conv_trainbn_nograd(x, conv, bn, act, residual, want_preact)
     # the raw convolution (not ``conv(x)``): modules that route their own
     # forward through this op -- e.g. the detection Conv2d with a norm child --
     # must not recurse

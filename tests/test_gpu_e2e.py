@@ -153,3 +153,29 @@ def test_native_bf16_graph_matches_eager(trainer):
         outs.append(st.flat.data.clone())
     rel = (outs[0] - outs[1]).norm() / outs[1].norm()
     assert rel < 1e-2, rel
+
+
+def test_ofd_train_bn_teacher_graph_bf16_tracks_fp32_eager():
+    """OFD with the reference's train-mode teacher BN: the native bf16 hipGraph
+    step stays finite and tracks the fp32 eager PyTorch step (round 1 had to
+    run this mode eagerly in fp32: MIOpen's captured bf16 train-BN went NaN)."""
+    from mdistiller_ddp_amd.ops.backend import use_backend
+    torch.manual_seed(0)
+    cfg = _cfg("OFD")
+    assert cfg.OFD.TEACHER_TRAIN_BN
+    d1 = build_distiller(cfg, 100, "cuda")
+    d2 = copy.deepcopy(d1)
+    losses = []
+    for d, g, dt, be in ((d1, True, torch.bfloat16, "auto"), (d2, False, torch.float32, "torch")):
+        with use_backend(be):
+            d.train()
+            st = TrainStep(d, cfg, "cuda", use_graph=g, dtype=dt)
+            st.set_epoch(1.0)
+            ld = SyntheticLoader("cifar100", 64, "cuda", steps_per_epoch=30, channels_last=True)
+            for b in ld:
+                st.step(b)
+            torch.cuda.synchronize()
+            assert (st._graphs is not None) == g
+            losses.append(st.meters.summary(reduce=False)["loss"])
+    assert all(v == v and abs(v) < 1e6 for v in losses), losses
+    assert abs(losses[0] - losses[1]) / abs(losses[1]) < 2e-2, losses

@@ -42,7 +42,11 @@ _WSS: dict = {}
 
 
 def _ws(device):
-    key = torch.device(device).index or 0
+    # one scratch buffer PER STREAM: the teacher's train-mode BN (OFD) runs on
+    # the teacher stream concurrently with the student's BN kernels, and a
+    # shared partials buffer raced under hipGraph replay (NaN OFD losses)
+    dev = torch.device(device)
+    key = (dev.index or 0, torch.cuda.current_stream(dev).cuda_stream)
     w = _WSS.get(key)
     if w is None:
         w = _WSS[key] = _WS(device)

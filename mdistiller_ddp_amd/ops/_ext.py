@@ -36,6 +36,7 @@ SIGNATURES = {
     # convolution (csrc/conv_igemm.hip)
     "mda_conv_fwd": "pppppppp" + "i" * 15 + "s",
     "mda_conv_plan": "iiipp",
+    "mda_conv_fwd_bnstats": "ppppp" + "i" * 15 + "p" * 8 + "ff" + "ps",
     "mda_conv_dgrad": "pppp" + "i" * 14 + "s",
     "mda_conv_wgrad": "pppp" + "i" * 13 + "fiis",
     "mda_pad_channels": "ippiiis",
@@ -61,6 +62,7 @@ SIGNATURES = {
     "mda_bn_tune": "ii",
     "mda_bn_stats2": "piip" + "pppp" + "pppp" + "ffps",
     "mda_bn_bwd_reduce2": "pppppppp" + "iii" + "pppp" + "s",
+    "mda_bn_finalize": "piii" + "pppppppp" + "ffps",
     # CRD memory (csrc/crd.hip)
     "mda_crd_scores": "ppppiiifs",
     "mda_crd_grad": "ppppppiiifs",

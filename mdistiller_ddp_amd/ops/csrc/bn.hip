@@ -529,3 +529,18 @@ MDA_API int mda_bn_bwd_reduce2(const void* dout, const void* dpre, const void* y
                      dbeta);
   MDA_CHECK_LAUNCH();
 }
+
+// Channel-parallel finalize of externally produced statistics partials
+// partial[nblk][2][C] (the conv epilogue's, csrc/conv_igemm.hip).
+MDA_API int mda_bn_finalize(const float* partial, int64_t nblk, int64_t M, int64_t C,
+                            const float* gamma, const float* beta, float* running_mean,
+                            float* running_var, float* mean, float* rstd, float* scale,
+                            float* shift, float momentum, float eps, int64_t* nbt,
+                            hipStream_t st) {
+  if (C % 8 || C > 2048 || nblk <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_finalize_kernel<0>, dim3((unsigned)((C + 7) / 8)), dim3(256), 0, st,
+                     partial, (int)nblk, (int)M, (int)C, gamma, beta, running_mean, running_var,
+                     mean, rstd, scale, shift, momentum, eps, nbt, (float*)nullptr,
+                     (float*)nullptr, (float*)nullptr);
+  MDA_CHECK_LAUNCH();
+}

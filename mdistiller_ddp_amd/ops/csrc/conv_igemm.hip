@@ -64,6 +64,10 @@ struct ConvParams {
   // (resp. pw) and only the taps kh = ph (mod par), kw = pw (mod par): the
   // 1 - 1/par^2 of the taps that cannot contribute are never multiplied.
   int par, zsplits;
+  // training BN: per-block per-channel sum / sum of squares of the stored
+  // (bf16-rounded) output, stats_part[blockIdx.x][2][Cout] (raw output only:
+  // no scale/bias/residual/activation, no split-K)
+  float* stats_part;
 };
 
 // Parity class of the strided-dgrad decomposition.
@@ -209,6 +213,47 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, const f32x4 (
   const int zsplit = pc ? (int)blockIdx.z % p.zsplits : (int)blockIdx.z;
   const bool split = pc ? p.zsplits > 1 : gridDim.z > 1;
   const int mlim = pc ? pc->Mc : p.M;
+  if (p.stats_part != nullptr) {
+    // raw bf16 output + BN statistics partials of this block's rows.  No early
+    // return before the barrier: threads past Cout just contribute zeros.
+    float s1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, s2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const bool cok = co < p.Cout;
+    for (int r0 = rr; r0 < rows; r0 += RPP) {
+      const int m = m0 + r0;
+      if (m >= mlim || !cok) break;
+      const float4 lo = *(const float4*)&Cs[r0 * CS + c8 * 8];
+      const float4 hi = *(const float4*)&Cs[r0 * CS + c8 * 8 + 4];
+      const uint4 o = make_uint4(pack_bf16x2(lo.x, lo.y), pack_bf16x2(lo.z, lo.w),
+                                 pack_bf16x2(hi.x, hi.y), pack_bf16x2(hi.z, hi.w));
+      *(uint4*)(p.y + (int64_t)m * p.Cout + co) = o;
+      const uint32_t u[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float a = __uint_as_float(u[e] << 16), b = __uint_as_float(u[e] & 0xffff0000u);
+        s1[2 * e] += a; s2[2 * e] += a * a;
+        s1[2 * e + 1] += b; s2[2 * e + 1] += b * b;
+      }
+    }
+    __syncthreads();  // every read of the C tile is done: reuse it for the reduction
+    float* red = Cs;  // [2][RPP][BN]
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[(0 * RPP + rr) * BN + c8 * 8 + e] = s1[e];
+      red[(1 * RPP + rr) * BN + c8 * 8 + e] = s2[e];
+    }
+    __syncthreads();
+    if (tid < 2 * BN) {
+      const int q = tid / BN, c = tid - q * BN;
+      float a0 = 0.f, a1 = 0.f;
+      for (int r = 0; r < RPP; r += 2) {
+        a0 += red[(q * RPP + r) * BN + c];
+        a1 += red[(q * RPP + r + 1) * BN + c];
+      }
+      if (n0 + c < p.Cout)
+        p.stats_part[((int64_t)blockIdx.x * 2 + q) * p.Cout + n0 + c] = a0 + a1;
+    }
+    return;
+  }
   if ((p.Cout & 7) == 0) {
     if (co >= p.Cout) return;
     float sc[8], bi[8];
@@ -1271,6 +1316,7 @@ MDA_API int mda_conv_fwd(const void* x, const void* w, const float* scale, const
   p.act = act;
   p.par = 0;
   p.zsplits = 1;
+  p.stats_part = nullptr;
   int mode = (Cin % BK == 0) ? LOAD_FAST : (Cin % 8 == 0 ? LOAD_VEC8 : LOAD_SCALAR);
   return dispatch(p, mode, tile, splits, st, halo_eligible(p) ? 1 : 0);
 }
@@ -1294,8 +1340,66 @@ MDA_API int mda_conv_dgrad(const void* dy, const void* wt, void* dx, float* part
   int mode = (Cout % BK == 0) ? LOAD_DGRAD_FAST : LOAD_DGRAD_VEC8;
   p.par = 0;
   p.zsplits = 1;
+  p.stats_part = nullptr;
   // strided dgrad: one GEMM per output-parity class with only its taps
   if (stride > 1 && mode == LOAD_DGRAD_FAST && use_glds() && use_par_dgrad()) p.par = (int)stride;
   // stride-1 3x3 pad-1 dgrad is a "same" conv of dy with the mirrored taps
   return dispatch(p, mode, tile, splits, st, halo_eligible(p) ? 2 : 0);
+}
+
+// Training conv + BN statistics, two launches: the conv writes the raw bf16
+// output AND per-block channel partials of its rows from the epilogue (the
+// output is never re-read for statistics), then the channel-parallel finalize
+// (csrc/bn.hip) produces mean / rstd / scale / shift and the running-stat
+// update.  Falls back to conv + mda_bn_stats2 when the conv is split over K
+// (the partial sums are only final after the split-K combine).
+// partial: >= max(nblk * 2 * Cout, 2 * 2048 * 512) floats (the BN workspace).
+extern "C" int mda_bn_finalize(const float* partial, int64_t nblk, int64_t M, int64_t C,
+                               const float* gamma, const float* beta, float* running_mean,
+                               float* running_var, float* mean, float* rstd, float* scale,
+                               float* shift, float momentum, float eps, int64_t* nbt,
+                               hipStream_t st);
+extern "C" int mda_bn_stats2(const void* y, int64_t M, int64_t C, float* partial,
+                             const float* gamma, const float* beta, float* running_mean,
+                             float* running_var, float* mean, float* rstd, float* scale,
+                             float* shift, float momentum, float eps, int64_t* nbt,
+                             hipStream_t st);
+
+MDA_API int mda_conv_fwd_bnstats(const void* x, const void* w, void* y, float* partial,
+                                 float* bn_partial, int64_t bn_partial_cap, int64_t N, int64_t H,
+                                 int64_t W, int64_t Cin, int64_t Ho, int64_t Wo, int64_t Cout,
+                                 int64_t KH, int64_t KW, int64_t stride, int64_t pad, int64_t Kp,
+                                 int64_t tile, int64_t splits, const float* gamma,
+                                 const float* beta, float* running_mean, float* running_var,
+                                 float* mean, float* rstd, float* scale, float* shift,
+                                 float momentum, float eps, int64_t* nbt, hipStream_t st) {
+  ConvParams p;
+  p.x = (const bf16_t*)x; p.w = (const bf16_t*)w; p.scale = nullptr; p.bias = nullptr;
+  p.res = nullptr; p.y = (bf16_t*)y; p.preact = nullptr; p.partial = partial;
+  p.N = N; p.H = H; p.W = W; p.Cin = Cin; p.Ho = Ho; p.Wo = Wo; p.Cout = Cout; p.KH = KH;
+  p.KW = KW; p.stride = stride; p.pad = pad; p.K = KH * KW * Cin; p.Kp = Kp; p.M = N * Ho * Wo;
+  p.act = 0;
+  p.par = 0;
+  p.zsplits = 1;
+  p.stats_part = nullptr;
+  if (Cout % 8 || Cout > 2048) return (int)hipErrorInvalidValue;
+  int mode = (Cin % BK == 0) ? LOAD_FAST : (Cin % 8 == 0 ? LOAD_VEC8 : LOAD_SCALAR);
+  if (tile == 0 || splits == 0) mda_conv_plan(p.M, p.Cout, p.Kp, &tile, &splits);
+  const int halo = halo_eligible(p) ? 1 : 0;
+  // M-blocks of the launch that will run (see dispatch)
+  int64_t nblk;
+  if (halo && !(!((Cin / BK) == 1 && splits == 1 && use_halo1()) &&
+                p.himgs * (p.hrows + 2) * (p.W + 2) > HALO_PROWS))
+    nblk = (p.M + p.hpb - 1) / p.hpb;
+  else
+    nblk = (p.M + tile / 1000 - 1) / (tile / 1000);
+  const bool fused = splits == 1 && nblk * 2 * Cout <= bn_partial_cap;
+  if (fused) p.stats_part = bn_partial;
+  int rc = dispatch(p, mode, tile, splits, st, halo);
+  if (rc) return rc;
+  if (fused)
+    return mda_bn_finalize(bn_partial, nblk, p.M, Cout, gamma, beta, running_mean, running_var,
+                           mean, rstd, scale, shift, momentum, eps, nbt, st);
+  return mda_bn_stats2(y, p.M, Cout, bn_partial, gamma, beta, running_mean, running_var, mean,
+                       rstd, scale, shift, momentum, eps, nbt, st);
 }

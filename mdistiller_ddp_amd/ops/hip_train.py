@@ -2,10 +2,11 @@
 
 One autograd node per layer:
 
-forward   pack weights (fp32 OIHW -> bf16 GEMM operands, 1 launch)
-          conv          (MFMA implicit GEMM, raw output y)
-          bn_stats      (per-block partials + channel-parallel finalize: batch mean /
-                         rstd, scale/shift, running-stat update)
+forward   pack weights (fp32 OIHW -> bf16 GEMM operands, one launch for all layers)
+          conv          (MFMA implicit GEMM, raw output y; the epilogue also writes the
+                         per-block BN statistics partials from the tile it just stored)
+          bn_finalize   (channel-parallel: batch mean / rstd, scale/shift, running-stat
+                         update)
           bn_apply      (z = y*scale + shift + res, out = act(z), optional preact)
 backward  bn_bwd_reduce (dgamma / dbeta accumulated straight into the flat grad buffer)
           bn_bwd_apply  (dy, and dz for the residual branch)
@@ -283,13 +284,13 @@ class _ConvBNActTrain(torch.autograd.Function):
         part = torch.empty(splits * M * Cout, dtype=torch.float32, device=dev) if splits > 1 else None
         y = torch.empty((N, Cout, Ho, Wo), dtype=torch.bfloat16, device=dev,
                         memory_format=torch.channels_last)
-        _ext.call("mda_conv_fwd", x, wf, None, None, None, y, None, part, N, H, W, Cin, Ho, Wo,
-                  Cout, KH, KW, stride, pad, Kp, 0, tile, splits)
         ws = _ws(dev)
         stats = torch.empty(4, Cout, dtype=torch.float32, device=dev)  # mean, rstd, scale, shift
-        _ext.call("mda_bn_stats2", y, M, Cout, ws.partial, gamma.detach(), beta.detach(),
-                  bn.running_mean, bn.running_var, stats[0], stats[1], stats[2], stats[3],
-                  float(bn.momentum), float(bn.eps), bn.num_batches_tracked)
+        # conv whose epilogue emits the BN statistics partials + finalize (2 launches)
+        _ext.call("mda_conv_fwd_bnstats", x, wf, y, part, ws.partial, ws.partial.numel(), N, H, W,
+                  Cin, Ho, Wo, Cout, KH, KW, stride, pad, Kp, tile, splits, gamma.detach(),
+                  beta.detach(), bn.running_mean, bn.running_var, stats[0], stats[1], stats[2],
+                  stats[3], float(bn.momentum), float(bn.eps), bn.num_batches_tracked)
         res = _cl_bf16(residual) if residual is not None else None
         out = torch.empty_like(y)
         pre = torch.empty_like(y) if want_preact else None

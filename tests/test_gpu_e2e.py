@@ -179,3 +179,38 @@ def test_ofd_train_bn_teacher_graph_bf16_tracks_fp32_eager():
             losses.append(st.meters.summary(reduce=False)["loss"])
     assert all(v == v and abs(v) < 1e6 for v in losses), losses
     assert abs(losses[0] - losses[1]) / abs(losses[1]) < 2e-2, losses
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("typ", ["KD", "DKD"])
+def test_native_bf16_tracks_fp32_over_300_steps(typ):
+    """300 optimizer steps: the native bf16 hipGraph trajectory's loss tracks the
+    fp32 PyTorch eager trajectory (last-50-step mean within 5 %) and both
+    actually learn (the 4 repeated synthetic batches get memorised)."""
+    from mdistiller_ddp_amd.ops.backend import use_backend
+    torch.manual_seed(0)
+    cfg = _cfg(typ)
+    cfg.SOLVER.LR = 0.05
+    d1 = build_distiller(cfg, 100, "cuda")
+    d2 = copy.deepcopy(d1)
+    curves = []
+    for d, g, dt, be in ((d1, True, torch.bfloat16, "auto"), (d2, False, torch.float32, "torch")):
+        with use_backend(be):
+            d.train()
+            st = TrainStep(d, cfg, "cuda", use_graph=g, dtype=dt)
+            st.set_epoch(30.0)
+            ld = SyntheticLoader("cifar100", 64, "cuda", steps_per_epoch=300, channels_last=True)
+            first = last = None
+            for i, b in enumerate(ld):
+                if i == 50:
+                    first = st.meters.summary(reduce=False)["loss"]
+                    st.meters.reset()
+                if i == 250:
+                    st.meters.reset()
+                st.step(b)
+            torch.cuda.synchronize()
+            last = st.meters.summary(reduce=False)["loss"]
+            curves.append((first, last))
+    (f_n, l_n), (f_r, l_r) = curves
+    assert l_n < 0.8 * f_n and l_r < 0.8 * f_r, curves  # both learn
+    assert abs(l_n - l_r) / abs(l_r) < 0.05, curves

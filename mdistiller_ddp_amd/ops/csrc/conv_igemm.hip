@@ -750,25 +750,30 @@ constexpr int HALO1_PROWS = HALO1_PIECES * 32;
 // leave the MFMA rows past hpb idle (<= 23 %) instead of falling back to the
 // im2col gather kernels, which re-read every input pixel 9 times.
 
-template <int BN>
+// RING = weight tiles in flight + 1.  RING 3 (80 KB: two blocks per CU) is
+// the generic kernel; RING 8 (120 KB, one block per CU, prefetch 7 taps
+// ahead) is for grids of about one block per CU (the 16x16 / 8x8 CIFAR
+// stages and ImageNet's deep stages), where nothing else hides the L2
+// round trip of each tap's weight tile.
+template <int BN, int RING = 3>
 struct HaloSmem {
   static constexpr int PATCH = HALO_PROWS * 128;      // bytes per patch buffer
   static constexpr int BT = BN * 128;                 // bytes per weight tile
-  static constexpr int PIPE = 2 * PATCH + 3 * BT;
+  static constexpr int PIPE = 2 * PATCH + RING * BT;
   static constexpr int CTILE = ConvSmem<HALO_BM, BN>::CTILE;
   static constexpr int BYTES = PIPE > CTILE ? PIPE : CTILE;
 };
 
-template <int BN, bool FLIP>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BN >= 128 ? 1 : 2)))
+template <int BN, bool FLIP, int RING = 3>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((BN >= 128 || RING > 3) ? 1 : 2)))
 conv_halo_kernel(const ConvParams p) {
   constexpr int BM = HALO_BM;
   constexpr int MI = BM / 32, NI = BN / 32;
   constexpr int BLOADS = (BN * 8 + 255) / 256;
-  constexpr int PATCH = HaloSmem<BN>::PATCH;
-  constexpr int BT = HaloSmem<BN>::BT;
+  constexpr int PATCH = HaloSmem<BN, RING>::PATCH;
+  constexpr int BT = HaloSmem<BN, RING>::BT;
 
-  __shared__ __attribute__((aligned(16))) char smem[HaloSmem<BN>::BYTES];
+  __shared__ __attribute__((aligned(16))) char smem[HaloSmem<BN, RING>::BYTES];
   typedef __attribute__((address_space(3))) char lds_char;
   const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_char*)smem;
 
@@ -894,22 +899,33 @@ conv_halo_kernel(const ConvParams p) {
   // prologue: patch of the first chunk, weight tiles of steps 0 and 1
 #pragma unroll
   for (int j = 0; j < HALO_PIECES; ++j) issue_piece(c_begin, 0, j);
-  issue_b(0, 0);
-  issue_b(1, 1);
+#pragma unroll
+  for (int s0 = 0; s0 < RING - 1; ++s0) issue_b(s0, s0);
   int pbuf = 0, bbuf = 0, step = 0;
   for (int cc = c_begin; cc < c_end; ++cc) {
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
-      // DMAs issued after B(step): [piece(tap-2) if 0<=tap-2<7] B(step+1) [piece(tap-1) if 0<=tap-1<7]
-      if (tap == 0) vm_wait_barrier<BLOADS>();
-      else if (tap == 1) vm_wait_barrier<BLOADS + 1>();
-      else if (tap <= 7) vm_wait_barrier<BLOADS + 2>();
-      else vm_wait_barrier<BLOADS + 1>();
-      const int nb = bbuf == 0 ? 2 : bbuf - 1;   // (step + 2) % 3
-      issue_b(step + 2, nb);
+      if (RING == 3) {
+        // DMAs issued after B(step): [piece(tap-2) if 0<=tap-2<7] B(step+1) [piece(tap-1) if 0<=tap-1<7]
+        if (tap == 0) vm_wait_barrier<BLOADS>();
+        else if (tap == 1) vm_wait_barrier<BLOADS + 1>();
+        else if (tap <= 7) vm_wait_barrier<BLOADS + 2>();
+        else vm_wait_barrier<BLOADS + 1>();
+      } else {
+        // B(step) is older than the RING-2 weight tiles issued after it, so
+        // vmcnt((RING-2)*BLOADS) has it landed (counting no patch piece keeps
+        // the count safe in the prologue steps too).  At tap 0 the patch of
+        // this chunk (last piece issued at tap 6 of the previous chunk, two
+        // weight tiles ago) must have landed as well.
+        if (tap == 0) vm_wait_barrier<2 * BLOADS>();
+        else vm_wait_barrier<(RING - 2) * BLOADS>();
+      }
+      int nb = bbuf + RING - 1;                  // (step + RING - 1) % RING
+      if (nb >= RING) nb -= RING;
+      issue_b(step + RING - 1, nb);
       if (tap < HALO_PIECES) issue_piece(cc + 1, pbuf ^ 1, tap);
       compute(pbuf, bbuf, tap);
-      bbuf = bbuf == 2 ? 0 : bbuf + 1;
+      bbuf = bbuf == RING - 1 ? 0 : bbuf + 1;
       ++step;
     }
     pbuf ^= 1;
@@ -1164,6 +1180,16 @@ bool use_par_dgrad() {
   return on;
 }
 
+// MDA_HALO_RING: 3 / 8 force the multi-chunk halo kernel's weight ring; unset
+// = 8 for grids of <= 320 blocks (about one per CU), else 3
+int halo_ring() {
+  static const int v = [] {
+    const char* e = getenv("MDA_HALO_RING");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 bool use_glds() {
   static const bool on = [] {
     const char* e = getenv("MDA_CONV_GLDS");
@@ -1251,12 +1277,26 @@ int dispatch(ConvParams& p, int mode, int64_t tile, int64_t splits, hipStream_t 
         if (halo == 2) hipLaunchKernelGGL((conv_halo1_kernel<64, true>), grid, dim3(256), 0, st, p);
         else hipLaunchKernelGGL((conv_halo1_kernel<64, false>), grid, dim3(256), 0, st, p);
       }
-    } else if (bn == 32) {
-      if (halo == 2) hipLaunchKernelGGL((conv_halo_kernel<32, true>), grid, dim3(256), 0, st, p);
-      else hipLaunchKernelGGL((conv_halo_kernel<32, false>), grid, dim3(256), 0, st, p);
     } else {
-      if (halo == 2) hipLaunchKernelGGL((conv_halo_kernel<64, true>), grid, dim3(256), 0, st, p);
-      else hipLaunchKernelGGL((conv_halo_kernel<64, false>), grid, dim3(256), 0, st, p);
+      const int64_t nblocks = (int64_t)grid.x * grid.y * grid.z;
+      const bool deep = halo_ring() == 8 || (halo_ring() == 0 && nblocks <= 320);
+      if (bn == 32) {
+        if (deep) {
+          if (halo == 2) hipLaunchKernelGGL((conv_halo_kernel<32, true, 8>), grid, dim3(256), 0, st, p);
+          else hipLaunchKernelGGL((conv_halo_kernel<32, false, 8>), grid, dim3(256), 0, st, p);
+        } else {
+          if (halo == 2) hipLaunchKernelGGL((conv_halo_kernel<32, true>), grid, dim3(256), 0, st, p);
+          else hipLaunchKernelGGL((conv_halo_kernel<32, false>), grid, dim3(256), 0, st, p);
+        }
+      } else {
+        if (deep) {
+          if (halo == 2) hipLaunchKernelGGL((conv_halo_kernel<64, true, 8>), grid, dim3(256), 0, st, p);
+          else hipLaunchKernelGGL((conv_halo_kernel<64, false, 8>), grid, dim3(256), 0, st, p);
+        } else {
+          if (halo == 2) hipLaunchKernelGGL((conv_halo_kernel<64, true>), grid, dim3(256), 0, st, p);
+          else hipLaunchKernelGGL((conv_halo_kernel<64, false>), grid, dim3(256), 0, st, p);
+        }
+      }
     }
     rc = (int)hipGetLastError();
   } else if (p.par > 1) {

@@ -293,7 +293,8 @@ pack_kernel(const float* __restrict__ w, bf16_t* __restrict__ wf, bf16_t* __rest
 // All layers of a network in one launch, as tiled transposes through LDS.
 // table[l] = {w, wf, wt (0 = none), Cout, Cin, KH, KW, Kp, KpT, tile0} (int64),
 // tile0 = first tile of layer l.  A tile is T co x T ci x all taps
-// (T = 64 for 1x1, 32 up to 3x3, 16 for larger kernels), loaded with
+// (T = 32 for 1x1, 16 up to 3x3, 8 for larger kernels: many small blocks, the
+// pack of a CIFAR student is only ~100 K weights), loaded with
 // coalesced reads of the OIHW fp32 rows (taps contiguous per (co, ci)) and
 // written as T-long contiguous runs of both packed layouts:
 //   wf[co][tap*Cin + ci]   and   wt[ci][tap*Cout + co].
@@ -306,7 +307,7 @@ constexpr int PACK_FIELDS = 10;
 constexpr int PACK_LDS_FLOATS = 13056;  // >= max over T of T*(T*KHKW + 1)
 
 __device__ __forceinline__ int pack_tile_dim(int khkw) {
-  return khkw == 1 ? 64 : (khkw <= 9 ? 32 : 16);
+  return khkw == 1 ? 32 : (khkw <= 9 ? 16 : 8);
 }
 
 __global__ void __launch_bounds__(256)
@@ -427,7 +428,7 @@ MDA_API int mda_pack_conv_weights_multi(const int64_t* table, int64_t L, int64_t
 // Tiles of one layer in mda_pack_conv_weights_multi.
 MDA_API int mda_pack_tiles(int64_t Cout, int64_t Cin, int64_t KH, int64_t KW, int64_t* tiles) {
   const int64_t khkw = KH * KW;
-  const int64_t T = khkw == 1 ? 64 : (khkw <= 9 ? 32 : 16);
+  const int64_t T = khkw == 1 ? 32 : (khkw <= 9 ? 16 : 8);
   if (khkw > 49) return (int)hipErrorInvalidValue;  // PACK_LDS_FLOATS sizing
   *tiles = ((Cout + T - 1) / T) * ((Cin + T - 1) / T);
   return 0;

@@ -184,25 +184,45 @@ struct ConvSmem {
 // row -> 16-byte residual loads and output stores, scale/bias loaded once
 // per thread.  Split-K blocks write fp32 partials instead.  The caller must
 // have finished every read of `smem` (barrier) before calling.
-template <int BM, int BN>
+// KS = 2: the block is two 256-thread K-groups with a partial accumulator
+// each (see conv_halo1_kernel); group 1 hands its tile to group 0 through
+// LDS, group 0 runs the epilogue.  Every barrier is reached by all threads.
+template <int BM, int BN, int KS = 1>
 __device__ __forceinline__ void conv_epilogue(const ConvParams& p, const f32x4 (&acc)[BM / 32][BN / 32],
                                               char* smem, int m0, int n0, int rows = BM,
                                               const ParClass* pc = nullptr) {
   constexpr int MI = BM / 32, NI = BN / 32;
   constexpr int CS = ConvSmem<BM, BN>::CS;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int grp = KS == 2 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8)) : 0;
+  const int tid = threadIdx.x & 255, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   float* const Cs = (float*)smem;
   {
     const int ecol = lane & 15;
     const int erow = (lane >> 4) * 4;
+    if (KS == 2) {
+      if (grp == 1) {
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < NI; ++j)
+          for (int j = 0; j < NI; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          Cs[(wm * (BM / 2) + i * 16 + erow + r) * CS + wn * (BN / 2) + j * 16 + ecol] = acc[i][j][r];
+            for (int r = 0; r < 4; ++r)
+              Cs[(wm * (BM / 2) + i * 16 + erow + r) * CS + wn * (BN / 2) + j * 16 + ecol] = acc[i][j][r];
+      }
+      __syncthreads();
+    }
+    if (grp == 0) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float* c = &Cs[(wm * (BM / 2) + i * 16 + erow + r) * CS + wn * (BN / 2) + j * 16 + ecol];
+            *c = KS == 2 ? *c + acc[i][j][r] : acc[i][j][r];
+          }
+    }
   }
   __syncthreads();
   constexpr int TPR = BN / 8;    // threads per row
@@ -217,7 +237,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, const f32x4 (
     // raw bf16 output + BN statistics partials of this block's rows.  No early
     // return before the barrier: threads past Cout just contribute zeros.
     float s1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, s2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    const bool cok = co < p.Cout;
+    const bool cok = co < p.Cout && grp == 0;
     for (int r0 = rr; r0 < rows; r0 += RPP) {
       const int m = m0 + r0;
       if (m >= mlim || !cok) break;
@@ -236,13 +256,15 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, const f32x4 (
     }
     __syncthreads();  // every read of the C tile is done: reuse it for the reduction
     float* red = Cs;  // [2][RPP][BN]
+    if (grp == 0) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      red[(0 * RPP + rr) * BN + c8 * 8 + e] = s1[e];
-      red[(1 * RPP + rr) * BN + c8 * 8 + e] = s2[e];
+      for (int e = 0; e < 8; ++e) {
+        red[(0 * RPP + rr) * BN + c8 * 8 + e] = s1[e];
+        red[(1 * RPP + rr) * BN + c8 * 8 + e] = s2[e];
+      }
     }
     __syncthreads();
-    if (tid < 2 * BN) {
+    if (grp == 0 && tid < 2 * BN) {
       const int q = tid / BN, c = tid - q * BN;
       float a0 = 0.f, a1 = 0.f;
       for (int r = 0; r < RPP; r += 2) {
@@ -254,6 +276,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, const f32x4 (
     }
     return;
   }
+  if (grp != 0) return;
   if ((p.Cout & 7) == 0) {
     if (co >= p.Cout) return;
     float sc[8], bi[8];
@@ -950,8 +973,13 @@ struct Halo1Smem {
   static constexpr int BYTES = PIPE > CTILE ? PIPE : CTILE;
 };
 
-template <int BN, bool FLIP>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+// KS = 2: 512 threads = two K-groups of four waves over the same patch and
+// weight tiles; group g multiplies the k-half g (channels 32g..32g+31) of
+// every tap, so each SIMD holds two waves whose LDS reads, waits and MFMAs
+// interleave (one wave per SIMD left the MFMA pipe ~85 % idle: PMC
+// SQ_VALU_MFMA_BUSY_CYCLES vs SQ_WAVE_CYCLES).  Only group 0 issues DMAs.
+template <int BN, bool FLIP, int KS = 1>
+__global__ void __launch_bounds__(256 * KS) __attribute__((amdgpu_waves_per_eu(2 * KS)))
 conv_halo1_kernel(const ConvParams p) {
   constexpr int BM = HALO_BM;
   constexpr int MI = BM / 32, NI = BN / 32;
@@ -964,7 +992,10 @@ conv_halo1_kernel(const ConvParams p) {
   typedef __attribute__((address_space(3))) char lds_char;
   const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_char*)smem;
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // wave-uniform K-group (readfirstlane: keeps the DMA branch and the LDS
+  // base on scalar registers)
+  const int grp = KS == 2 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8)) : 0;
+  const int tid = threadIdx.x & 255, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int PB = p.hpb;                       // output pixels of this block (<= BM)
   const int m0 = blockIdx.x * PB;
@@ -1062,7 +1093,7 @@ conv_halo1_kernel(const ConvParams p) {
     const int kh = tap / 3, kw = tap - (tap / 3) * 3;
     const int toff = kh * PW + kw;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    for (int kk = KS == 2 ? grp : 0; kk < (KS == 2 ? grp + 1 : 2); ++kk) {
       const int q = kk * 4 + g4;
       bf16x8 af[MI], bfr[NI];
 #pragma unroll
@@ -1082,20 +1113,23 @@ conv_halo1_kernel(const ConvParams p) {
   };
 
   // prologue: the (only) patch, then weight tiles of steps 0 .. RING-2
+  if (grp == 0) {
 #pragma unroll
-  for (int j = 0; j < HALO1_PIECES; ++j) issue_piece(c_begin, 0, j);
+    for (int j = 0; j < HALO1_PIECES; ++j) issue_piece(c_begin, 0, j);
 #pragma unroll
-  for (int s0 = 0; s0 < RING - 1; ++s0) issue_b(s0, s0);
+    for (int s0 = 0; s0 < RING - 1; ++s0) issue_b(s0, s0);
+  }
 #pragma unroll
   for (int tap = 0; tap < 9; ++tap) {
     // DMAs issued after B(tap): B(tap+1) .. B(tap+RING-2), always RING-2 tiles
-    // (tiles past the last step are zero-page dummies, so counts stay constant)
+    // (tiles past the last step are zero-page dummies, so counts stay constant);
+    // group 1 has no DMAs in flight and only joins the barrier
     vm_wait_barrier<(RING - 2) * BLOADS>();
-    issue_b(tap + RING - 1, (tap + RING - 1) % RING);
+    if (grp == 0) issue_b(tap + RING - 1, (tap + RING - 1) % RING);
     compute(0, tap % RING, tap);
   }
   vm_wait_barrier<0>();
-  conv_epilogue<BM, BN>(p, acc, smem, m0, n0, PB);
+  conv_epilogue<BM, BN, KS>(p, acc, smem, m0, n0, PB);
 }
 
 // Split-K combine: y = epilogue(sum_z partial[z]) in fixed z order.
@@ -1190,6 +1224,15 @@ int halo_ring() {
   return v;
 }
 
+// MDA_HALO1_KSPLIT=0 selects the 256-thread single-chunk halo kernel
+bool halo1_ksplit() {
+  static const bool on = [] {
+    const char* e = getenv("MDA_HALO1_KSPLIT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 bool use_glds() {
   static const bool on = [] {
     const char* e = getenv("MDA_CONV_GLDS");
@@ -1270,12 +1313,23 @@ int dispatch(ConvParams& p, int mode, int64_t tile, int64_t splits, hipStream_t 
     const int bn = p.Cout <= 32 ? 32 : 64;
     dim3 grid((p.M + p.hpb - 1) / p.hpb, (p.Cout + bn - 1) / bn, (int)splits);
     if (nchunks == 1 && splits == 1 && use_halo1()) {
+      const bool ks2 = halo1_ksplit();
       if (bn == 32) {
-        if (halo == 2) hipLaunchKernelGGL((conv_halo1_kernel<32, true>), grid, dim3(256), 0, st, p);
-        else hipLaunchKernelGGL((conv_halo1_kernel<32, false>), grid, dim3(256), 0, st, p);
+        if (ks2) {
+          if (halo == 2) hipLaunchKernelGGL((conv_halo1_kernel<32, true, 2>), grid, dim3(512), 0, st, p);
+          else hipLaunchKernelGGL((conv_halo1_kernel<32, false, 2>), grid, dim3(512), 0, st, p);
+        } else {
+          if (halo == 2) hipLaunchKernelGGL((conv_halo1_kernel<32, true>), grid, dim3(256), 0, st, p);
+          else hipLaunchKernelGGL((conv_halo1_kernel<32, false>), grid, dim3(256), 0, st, p);
+        }
       } else {
-        if (halo == 2) hipLaunchKernelGGL((conv_halo1_kernel<64, true>), grid, dim3(256), 0, st, p);
-        else hipLaunchKernelGGL((conv_halo1_kernel<64, false>), grid, dim3(256), 0, st, p);
+        if (ks2) {
+          if (halo == 2) hipLaunchKernelGGL((conv_halo1_kernel<64, true, 2>), grid, dim3(512), 0, st, p);
+          else hipLaunchKernelGGL((conv_halo1_kernel<64, false, 2>), grid, dim3(512), 0, st, p);
+        } else {
+          if (halo == 2) hipLaunchKernelGGL((conv_halo1_kernel<64, true>), grid, dim3(256), 0, st, p);
+          else hipLaunchKernelGGL((conv_halo1_kernel<64, false>), grid, dim3(256), 0, st, p);
+        }
       }
     } else {
       const int64_t nblocks = (int64_t)grid.x * grid.y * grid.z;

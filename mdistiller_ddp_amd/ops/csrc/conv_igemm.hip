@@ -184,49 +184,49 @@ struct ConvSmem {
 // row -> 16-byte residual loads and output stores, scale/bias loaded once
 // per thread.  Split-K blocks write fp32 partials instead.  The caller must
 // have finished every read of `smem` (barrier) before calling.
-// KS = 2: the block is two 256-thread K-groups with a partial accumulator
-// each (see conv_halo1_kernel); group 1 hands its tile to group 0 through
-// LDS, group 0 runs the epilogue.  Every barrier is reached by all threads.
-template <int BM, int BN, int KS = 1>
+// Phase 1 of the epilogue: one 4-wave group's MFMA accumulators (a BMg x BN
+// tile, 2x2 waves) into the fp32 C tile at row offset `row0`.
+template <int BMg, int BN>
+__device__ __forceinline__ void store_c_tile(float* Cs, int CS, const f32x4 (&acc)[BMg / 32][BN / 32],
+                                             int row0, int wid, int lane) {
+  constexpr int MI = BMg / 32, NI = BN / 32;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int ecol = lane & 15;
+  const int erow = (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Cs[(row0 + wm * (BMg / 2) + i * 16 + erow + r) * CS + wn * (BN / 2) + j * 16 + ecol] = acc[i][j][r];
+}
+
+template <int BM, int BN, int NT = 256>
+__device__ __forceinline__ void conv_epilogue_rows(const ConvParams& p, char* smem, int m0, int n0,
+                                                   int rows, const ParClass* pc);
+
+template <int BM, int BN>
 __device__ __forceinline__ void conv_epilogue(const ConvParams& p, const f32x4 (&acc)[BM / 32][BN / 32],
                                               char* smem, int m0, int n0, int rows = BM,
                                               const ParClass* pc = nullptr) {
-  constexpr int MI = BM / 32, NI = BN / 32;
-  constexpr int CS = ConvSmem<BM, BN>::CS;
-  const int grp = KS == 2 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8)) : 0;
-  const int tid = threadIdx.x & 255, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
-  float* const Cs = (float*)smem;
-  {
-    const int ecol = lane & 15;
-    const int erow = (lane >> 4) * 4;
-    if (KS == 2) {
-      if (grp == 1) {
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-          for (int j = 0; j < NI; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              Cs[(wm * (BM / 2) + i * 16 + erow + r) * CS + wn * (BN / 2) + j * 16 + ecol] = acc[i][j][r];
-      }
-      __syncthreads();
-    }
-    if (grp == 0) {
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float* c = &Cs[(wm * (BM / 2) + i * 16 + erow + r) * CS + wn * (BN / 2) + j * 16 + ecol];
-            *c = KS == 2 ? *c + acc[i][j][r] : acc[i][j][r];
-          }
-    }
-  }
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  store_c_tile<BM, BN>((float*)smem, ConvSmem<BM, BN>::CS, acc, 0, wid, lane);
   __syncthreads();
+  conv_epilogue_rows<BM, BN, 256>(p, smem, m0, n0, rows, pc);
+}
+
+// Phase 2: NT threads own 8 channels x rows of the C tile: bias / BN affine,
+// residual, activation, preact and bf16 stores, split-K partials, or the raw
+// output + BN statistics partials.  Every barrier is reached by all threads.
+template <int BM, int BN, int NT>
+__device__ __forceinline__ void conv_epilogue_rows(const ConvParams& p, char* smem, int m0, int n0,
+                                                   int rows, const ParClass* pc) {
+  constexpr int CS = ConvSmem<BM, BN>::CS;
+  const int tid = threadIdx.x;
+  float* const Cs = (float*)smem;
   constexpr int TPR = BN / 8;    // threads per row
-  constexpr int RPP = 256 / TPR; // rows per pass
+  constexpr int RPP = NT / TPR;  // rows per pass
   const int c8 = tid % TPR;
   const int rr = tid / TPR;
   const int co = n0 + c8 * 8;
@@ -237,7 +237,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, const f32x4 (
     // raw bf16 output + BN statistics partials of this block's rows.  No early
     // return before the barrier: threads past Cout just contribute zeros.
     float s1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, s2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    const bool cok = co < p.Cout && grp == 0;
+    const bool cok = co < p.Cout;
     for (int r0 = rr; r0 < rows; r0 += RPP) {
       const int m = m0 + r0;
       if (m >= mlim || !cok) break;
@@ -256,15 +256,13 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, const f32x4 (
     }
     __syncthreads();  // every read of the C tile is done: reuse it for the reduction
     float* red = Cs;  // [2][RPP][BN]
-    if (grp == 0) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        red[(0 * RPP + rr) * BN + c8 * 8 + e] = s1[e];
-        red[(1 * RPP + rr) * BN + c8 * 8 + e] = s2[e];
-      }
+    for (int e = 0; e < 8; ++e) {
+      red[(0 * RPP + rr) * BN + c8 * 8 + e] = s1[e];
+      red[(1 * RPP + rr) * BN + c8 * 8 + e] = s2[e];
     }
     __syncthreads();
-    if (grp == 0 && tid < 2 * BN) {
+    if (tid < 2 * BN) {
       const int q = tid / BN, c = tid - q * BN;
       float a0 = 0.f, a1 = 0.f;
       for (int r = 0; r < RPP; r += 2) {
@@ -276,7 +274,6 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, const f32x4 (
     }
     return;
   }
-  if (grp != 0) return;
   if ((p.Cout & 7) == 0) {
     if (co >= p.Cout) return;
     float sc[8], bi[8];
@@ -973,13 +970,8 @@ struct Halo1Smem {
   static constexpr int BYTES = PIPE > CTILE ? PIPE : CTILE;
 };
 
-// KS = 2: 512 threads = two K-groups of four waves over the same patch and
-// weight tiles; group g multiplies the k-half g (channels 32g..32g+31) of
-// every tap, so each SIMD holds two waves whose LDS reads, waits and MFMAs
-// interleave (one wave per SIMD left the MFMA pipe ~85 % idle: PMC
-// SQ_VALU_MFMA_BUSY_CYCLES vs SQ_WAVE_CYCLES).  Only group 0 issues DMAs.
-template <int BN, bool FLIP, int KS = 1>
-__global__ void __launch_bounds__(256 * KS) __attribute__((amdgpu_waves_per_eu(2 * KS)))
+template <int BN, bool FLIP>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 conv_halo1_kernel(const ConvParams p) {
   constexpr int BM = HALO_BM;
   constexpr int MI = BM / 32, NI = BN / 32;
@@ -992,10 +984,7 @@ conv_halo1_kernel(const ConvParams p) {
   typedef __attribute__((address_space(3))) char lds_char;
   const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_char*)smem;
 
-  // wave-uniform K-group (readfirstlane: keeps the DMA branch and the LDS
-  // base on scalar registers)
-  const int grp = KS == 2 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8)) : 0;
-  const int tid = threadIdx.x & 255, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int PB = p.hpb;                       // output pixels of this block (<= BM)
   const int m0 = blockIdx.x * PB;
@@ -1093,7 +1082,7 @@ conv_halo1_kernel(const ConvParams p) {
     const int kh = tap / 3, kw = tap - (tap / 3) * 3;
     const int toff = kh * PW + kw;
 #pragma unroll
-    for (int kk = KS == 2 ? grp : 0; kk < (KS == 2 ? grp + 1 : 2); ++kk) {
+    for (int kk = 0; kk < 2; ++kk) {
       const int q = kk * 4 + g4;
       bf16x8 af[MI], bfr[NI];
 #pragma unroll
@@ -1113,23 +1102,171 @@ conv_halo1_kernel(const ConvParams p) {
   };
 
   // prologue: the (only) patch, then weight tiles of steps 0 .. RING-2
-  if (grp == 0) {
 #pragma unroll
-    for (int j = 0; j < HALO1_PIECES; ++j) issue_piece(c_begin, 0, j);
+  for (int j = 0; j < HALO1_PIECES; ++j) issue_piece(c_begin, 0, j);
 #pragma unroll
-    for (int s0 = 0; s0 < RING - 1; ++s0) issue_b(s0, s0);
-  }
+  for (int s0 = 0; s0 < RING - 1; ++s0) issue_b(s0, s0);
 #pragma unroll
   for (int tap = 0; tap < 9; ++tap) {
     // DMAs issued after B(tap): B(tap+1) .. B(tap+RING-2), always RING-2 tiles
-    // (tiles past the last step are zero-page dummies, so counts stay constant);
-    // group 1 has no DMAs in flight and only joins the barrier
+    // (tiles past the last step are zero-page dummies, so counts stay constant)
     vm_wait_barrier<(RING - 2) * BLOADS>();
-    if (grp == 0) issue_b(tap + RING - 1, (tap + RING - 1) % RING);
+    issue_b(tap + RING - 1, (tap + RING - 1) % RING);
     compute(0, tap % RING, tap);
   }
   vm_wait_barrier<0>();
-  conv_epilogue<BM, BN, KS>(p, acc, smem, m0, n0, PB);
+  conv_epilogue<BM, BN>(p, acc, smem, m0, n0, PB);
+}
+
+// Single-chunk (Cin == 64) halo conv with a 256-pixel block: two groups of
+// four waves (512 threads) own 128 output pixels each and share ONE patch
+// and ONE copy of all nine weight tiles, resident in LDS for the whole
+// block.  The 128-pixel kernels spent most of their time streaming the same
+// 72 KB of weights into every block (512 blocks x 72 KB = 37 MB of L2->LDS
+// traffic per 4.8 GFLOP conv, vs 13 MB of activations); a 256-pixel block
+// halves that, and with every load issued up front each tap waits only for
+// its own tile.  DMA layout: 64-row slabs (8 waves x 8 rows); weight tiles
+// use 64-row slots whatever BN is (rows >= BN read the zero page).
+constexpr int HALO2_CAP = 256;
+constexpr int HALO2_PIECES = 6;                        // 6 x 64 = 384 patch rows
+constexpr int HALO2_PROWS = HALO2_PIECES * 64;
+
+template <int BN>
+struct Halo2Smem {
+  static constexpr int PATCH = HALO2_PROWS * 128;      // 48 KB
+  static constexpr int BT = 64 * 128;                  // one tap's weight slot
+  static constexpr int PIPE = PATCH + 9 * BT;          // 120 KB
+  static constexpr int CTILE = ConvSmem<HALO2_CAP, BN>::CTILE;
+  static constexpr int BYTES = PIPE > CTILE ? PIPE : CTILE;
+};
+
+template <int BN, bool FLIP>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
+conv_halo2_kernel(const ConvParams p) {
+  constexpr int BMG = 128;                    // pixels per group
+  constexpr int MI = BMG / 32, NI = BN / 32;
+  constexpr int PATCH = Halo2Smem<BN>::PATCH;
+  constexpr int BT = Halo2Smem<BN>::BT;
+
+  __shared__ __attribute__((aligned(16))) char smem[Halo2Smem<BN>::BYTES];
+  typedef __attribute__((address_space(3))) char lds_char;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_char*)smem;
+
+  const int gtid = threadIdx.x;                                   // 0..511
+  const int grp = __builtin_amdgcn_readfirstlane(gtid >> 8);     // pixel group
+  const int tid = gtid & 255, lane = tid & 63, wid = tid >> 6;   // within the group
+  const int wm = wid >> 1, wn = wid & 1;
+  const int PB = p.hpb;
+  const int m0 = blockIdx.x * PB;
+  const int n0 = blockIdx.y * BN;
+  const uint32_t wave_off = (uint32_t)__builtin_amdgcn_readfirstlane(gtid >> 6) * 1024u;
+  const bf16_t* const zero = (const bf16_t*)g_zero16;
+
+  const int W = p.W, H = p.H;
+  const int IMGS = p.himgs, RH = p.hrows;
+  const int PW = W + 2, PH = RH + 2;
+  const int grow0 = m0 / W;
+  const int img0 = grow0 / H;
+  const int oh0 = grow0 - img0 * H;
+
+  // DMA lanes: 64 rows (8 per wave) x 8 sixteen-byte chunks, XOR-swizzled
+  const int trow = gtid >> 3;
+  const int chunk = (gtid & 7) ^ ((trow >> 1) & 7);
+  int p_src[HALO2_PIECES];
+  {
+    const int P = IMGS * PH * PW;
+#pragma unroll
+    for (int j = 0; j < HALO2_PIECES; ++j) {
+      const int pr = 64 * j + trow;
+      int off = -1;
+      if (pr < P) {
+        const int img = pr / (PH * PW);
+        const int rem = pr - img * PH * PW;
+        const int ir = rem / PW, ic = rem - (rem / PW) * PW;
+        const int n = img0 + img;
+        const int ih = oh0 + ir - 1, iw = ic - 1;
+        if (n < p.N && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
+          off = ((n * H + ih) * W + iw) * p.Cin;
+      }
+      p_src[j] = off;
+    }
+  }
+  const int co = n0 + trow;
+  const bool b_ok = trow < BN && co < p.Cout;
+  const bf16_t* const b_row = p.w + (int64_t)(b_ok ? co : 0) * p.Kp + chunk * 8;
+
+  // every DMA up front: the patch, then the nine weight taps in order
+#pragma unroll
+  for (int j = 0; j < HALO2_PIECES; ++j) {
+    const bf16_t* src = p_src[j] >= 0 ? p.x + p_src[j] + chunk * 8 : zero;
+    glds16(src, lds0 + (uint32_t)(j * 64 * 128) + wave_off);
+  }
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int wtap = FLIP ? 8 - t : t;
+    glds16(b_ok ? b_row + wtap * p.Cin : zero, lds0 + PATCH + (uint32_t)(t * BT) + wave_off);
+  }
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int frow = lane & 15;
+  const int g4 = lane >> 4;
+  int a_prow[MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    int ml = grp * BMG + wm * (BMG / 2) + i * 16 + frow;
+    if (ml >= PB) ml = 0;                       // idle MFMA row (masked at the store)
+    const int lr = ml / W, c = ml - (ml / W) * W;
+    const int img = lr / RH, r = lr - img * RH;
+    a_prow[i] = (img * PH + r) * PW + c;
+  }
+  const int bswz = (frow >> 1) & 7;
+
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    // the patch and weight taps 0..tap have landed: 8 - tap younger DMAs
+    switch (tap) {  // (the loop is unrolled: each case folds to one wait)
+      case 0: vm_wait_barrier<8>(); break;
+      case 1: vm_wait_barrier<7>(); break;
+      case 2: vm_wait_barrier<6>(); break;
+      case 3: vm_wait_barrier<5>(); break;
+      case 4: vm_wait_barrier<4>(); break;
+      case 5: vm_wait_barrier<3>(); break;
+      case 6: vm_wait_barrier<2>(); break;
+      case 7: vm_wait_barrier<1>(); break;
+      default: vm_wait_barrier<0>(); break;
+    }
+    const char* Ps = smem;
+    const char* Bs = smem + PATCH + tap * BT;
+    const int kh = tap / 3, kw = tap - (tap / 3) * 3;
+    const int toff = kh * PW + kw;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int q = kk * 4 + g4;
+      bf16x8 af[MI], bfr[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int pr = a_prow[i] + toff;
+        af[i] = *(const bf16x8*)(Ps + pr * 128 + ((q ^ ((pr >> 1) & 7)) * 16));
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+        bfr[j] = *(const bf16x8*)(Bs + (wn * (BN / 2) + j * 16 + frow) * 128 + ((q ^ bswz) * 16));
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  __syncthreads();  // every LDS read of the patch / weights done: the C tile aliases them
+  store_c_tile<BMG, BN>((float*)smem, ConvSmem<HALO2_CAP, BN>::CS, acc, grp * BMG, wid, lane);
+  __syncthreads();
+  conv_epilogue_rows<HALO2_CAP, BN, 512>(p, smem, m0, n0, PB, nullptr);
 }
 
 // Split-K combine: y = epilogue(sum_z partial[z]) in fixed z order.
@@ -1168,21 +1305,22 @@ __global__ void __launch_bounds__(256) conv_splitk_epilogue(const ConvParams p, 
 // 3x3 / stride 1 / pad 1 "same" conv with Cin % 64 == 0 whose block
 // geometry (see HALO_BM) has a patch of at most `max_rows` rows; fills
 // p.hrows / p.himgs / p.hpb.
-bool halo_geometry(ConvParams& p, int max_rows) {
+bool halo_geometry(ConvParams& p, int max_rows, int cap = HALO_BM) {
   if (p.KH != 3 || p.KW != 3 || p.stride != 1 || p.pad != 1) return false;
   if (p.Ho != p.H || p.Wo != p.W || p.Cin % BK || p.Kp != 9 * p.Cin) return false;
   if (p.W > HALO_BM) return false;
   int imgs = 1, rows = 0;
-  if (p.H * p.W <= HALO_BM) {
-    imgs = HALO_BM / (p.H * p.W);
+  if (p.H * p.W <= cap) {
+    imgs = cap / (p.H * p.W);
+    while (imgs > 1 && imgs * (p.H + 2) * (p.W + 2) > max_rows) --imgs;
     rows = p.H;
   } else {
-    for (int r = HALO_BM / p.W; r >= 1; --r)
-      if (p.H % r == 0) { rows = r; break; }
+    for (int r = cap / p.W; r >= 1; --r)
+      if (p.H % r == 0 && (r + 2) * (p.W + 2) <= max_rows) { rows = r; break; }
   }
   if (rows <= 0 || imgs * (rows + 2) * (p.W + 2) > max_rows) return false;
   const int pb = imgs * rows * p.W;
-  if (4 * pb < 3 * HALO_BM && !(p.H * p.W <= HALO_BM)) return false;  // < 75 % rows busy
+  if (4 * pb < 3 * cap && !(p.H * p.W <= HALO_BM)) return false;  // < 75 % rows busy
   p.hrows = rows;
   p.himgs = imgs;
   p.hpb = pb;
@@ -1196,6 +1334,15 @@ bool halo_eligible(ConvParams& p) {
   }();
   if (!on) return false;
   return halo_geometry(p, p.Cin == BK ? HALO1_PROWS : HALO_PROWS);
+}
+
+// MDA_CONV_HALO2=0: single-chunk convs on the 128-pixel kernel
+bool use_halo2() {
+  static const bool on = [] {
+    const char* e = getenv("MDA_CONV_HALO2");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 
 bool use_halo1() {
@@ -1222,15 +1369,6 @@ int halo_ring() {
     return e ? atoi(e) : 3;
   }();
   return v;
-}
-
-// MDA_HALO1_KSPLIT=0 selects the 256-thread single-chunk halo kernel
-bool halo1_ksplit() {
-  static const bool on = [] {
-    const char* e = getenv("MDA_HALO1_KSPLIT");
-    return !(e && e[0] == '0');
-  }();
-  return on;
 }
 
 bool use_glds() {
@@ -1307,29 +1445,33 @@ int dispatch(ConvParams& p, int mode, int64_t tile, int64_t splits, hipStream_t 
         p.himgs * (p.hrows + 2) * (p.W + 2) > HALO_PROWS)
       halo = 0;
   }
+  if (halo && p.Cin == BK && splits == 1 && use_halo2()) {
+    ConvParams q = p;
+    if (halo_geometry(q, HALO2_PROWS, HALO2_CAP)) {
+      const int bn = q.Cout <= 32 ? 32 : 64;
+      dim3 grid((q.M + q.hpb - 1) / q.hpb, (q.Cout + bn - 1) / bn, 1);
+      if (bn == 32) {
+        if (halo == 2) hipLaunchKernelGGL((conv_halo2_kernel<32, true>), grid, dim3(512), 0, st, q);
+        else hipLaunchKernelGGL((conv_halo2_kernel<32, false>), grid, dim3(512), 0, st, q);
+      } else {
+        if (halo == 2) hipLaunchKernelGGL((conv_halo2_kernel<64, true>), grid, dim3(512), 0, st, q);
+        else hipLaunchKernelGGL((conv_halo2_kernel<64, false>), grid, dim3(512), 0, st, q);
+      }
+      return (int)hipGetLastError();  // single chunk: no split-K combine
+    }
+  }
   if (halo) {  // halo kernel: split over 64-channel chunks, hpb pixels per block
     const int nchunks = p.Cin / BK;
     p.steps_per_split = (int)((nchunks + splits - 1) / splits);
     const int bn = p.Cout <= 32 ? 32 : 64;
     dim3 grid((p.M + p.hpb - 1) / p.hpb, (p.Cout + bn - 1) / bn, (int)splits);
     if (nchunks == 1 && splits == 1 && use_halo1()) {
-      const bool ks2 = halo1_ksplit();
       if (bn == 32) {
-        if (ks2) {
-          if (halo == 2) hipLaunchKernelGGL((conv_halo1_kernel<32, true, 2>), grid, dim3(512), 0, st, p);
-          else hipLaunchKernelGGL((conv_halo1_kernel<32, false, 2>), grid, dim3(512), 0, st, p);
-        } else {
-          if (halo == 2) hipLaunchKernelGGL((conv_halo1_kernel<32, true>), grid, dim3(256), 0, st, p);
-          else hipLaunchKernelGGL((conv_halo1_kernel<32, false>), grid, dim3(256), 0, st, p);
-        }
+        if (halo == 2) hipLaunchKernelGGL((conv_halo1_kernel<32, true>), grid, dim3(256), 0, st, p);
+        else hipLaunchKernelGGL((conv_halo1_kernel<32, false>), grid, dim3(256), 0, st, p);
       } else {
-        if (ks2) {
-          if (halo == 2) hipLaunchKernelGGL((conv_halo1_kernel<64, true, 2>), grid, dim3(512), 0, st, p);
-          else hipLaunchKernelGGL((conv_halo1_kernel<64, false, 2>), grid, dim3(512), 0, st, p);
-        } else {
-          if (halo == 2) hipLaunchKernelGGL((conv_halo1_kernel<64, true>), grid, dim3(256), 0, st, p);
-          else hipLaunchKernelGGL((conv_halo1_kernel<64, false>), grid, dim3(256), 0, st, p);
-        }
+        if (halo == 2) hipLaunchKernelGGL((conv_halo1_kernel<64, true>), grid, dim3(256), 0, st, p);
+        else hipLaunchKernelGGL((conv_halo1_kernel<64, false>), grid, dim3(256), 0, st, p);
       }
     } else {
       const int64_t nblocks = (int64_t)grid.x * grid.y * grid.z;
@@ -1482,8 +1624,11 @@ MDA_API int mda_conv_fwd_bnstats(const void* x, const void* w, void* y, float* p
   const int halo = halo_eligible(p) ? 1 : 0;
   // M-blocks of the launch that will run (see dispatch)
   int64_t nblk;
-  if (halo && !(!((Cin / BK) == 1 && splits == 1 && use_halo1()) &&
-                p.himgs * (p.hrows + 2) * (p.W + 2) > HALO_PROWS))
+  ConvParams q2 = p;
+  if (halo && p.Cin == BK && splits == 1 && use_halo2() && halo_geometry(q2, HALO2_PROWS, HALO2_CAP))
+    nblk = (p.M + q2.hpb - 1) / q2.hpb;
+  else if (halo && !(!((Cin / BK) == 1 && splits == 1 && use_halo1()) &&
+                     p.himgs * (p.hrows + 2) * (p.W + 2) > HALO_PROWS))
     nblk = (p.M + p.hpb - 1) / p.hpb;
   else
     nblk = (p.M + tile / 1000 - 1) / (tile / 1000);

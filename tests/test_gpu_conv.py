@@ -79,6 +79,8 @@ DGRAD_SHAPES = [
     (2, 64, 32, 128, 1, 2, 0),    # 1x1 / s2: three classes have no taps
     (2, 8, 30, 64, 7, 2, 3),      # 7x7 / s2 (stem-like)
     (2, 64, 16, 64, 3, 1, 1),     # stride 1 (halo)
+    (8, 64, 8, 64, 3, 1, 1),      # 8x8 maps: 3 images per 256-pixel block, partial last block
+    (4, 32, 32, 64, 3, 1, 1),     # dgrad with 32 output channels (BN = 32 tiles)
     (2, 64, 56, 64, 3, 1, 1),     # stride 1, width 56 (halo, 112-pixel blocks)
     (2, 128, 28, 128, 3, 1, 1),   # width 28, two channel chunks
     (2, 128, 14, 128, 3, 1, 1),   # width 14 (98-pixel blocks)
@@ -100,7 +102,8 @@ def test_conv_dgrad_matches_autograd(shape):
     torch.testing.assert_close(dx.float(), x.grad, atol=3e-2, rtol=3e-2)
 
 
-@pytest.mark.parametrize("shape", [(2, 64, 56, 64, 3, 1, 1), (2, 128, 28, 128, 3, 1, 1),
+@pytest.mark.parametrize("shape", [(2, 64, 56, 64, 3, 1, 1), (4, 64, 32, 32, 3, 1, 1),
+                                   (5, 64, 8, 64, 3, 1, 1), (2, 128, 28, 128, 3, 1, 1),
                                    (2, 256, 14, 256, 3, 1, 1), (4, 512, 7, 512, 3, 1, 1)])
 def test_conv_forward_imagenet_widths(shape):
     """Halo kernel with blocks of whole rows that do not fill 128 pixels."""

@@ -36,6 +36,7 @@ SIGNATURES = {
     # convolution (csrc/conv_igemm.hip)
     "mda_conv_fwd": "pppppppp" + "i" * 15 + "s",
     "mda_conv_plan": "iiipp",
+    "mda_conv_set_stamps": "p",
     "mda_conv_fwd_bnstats": "ppppp" + "i" * 15 + "p" * 8 + "ff" + "ps",
     "mda_conv_dgrad": "pppp" + "i" * 14 + "s",
     "mda_conv_wgrad": "pppp" + "i" * 13 + "fiis",

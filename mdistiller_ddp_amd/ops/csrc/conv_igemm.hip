@@ -68,7 +68,17 @@ struct ConvParams {
   // (bf16-rounded) output, stats_part[blockIdx.x][2][Cout] (raw output only:
   // no scale/bias/residual/activation, no split-K)
   float* stats_part;
+  // diagnostics: per-block phase timestamps (s_memrealtime, 100 MHz), null in
+  // normal runs (mda_conv_set_stamps)
+  uint64_t* stamps;
 };
+
+__device__ __forceinline__ void stamp(const ConvParams& p, int k) {
+  if (p.stamps != nullptr && threadIdx.x == 0) {
+    const int b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    p.stamps[(int64_t)b * 8 + k] = __builtin_amdgcn_s_memrealtime();
+  }
+}
 
 // Parity class of the strided-dgrad decomposition.
 struct ParClass {
@@ -1152,6 +1162,7 @@ conv_halo2_kernel(const ConvParams p) {
   typedef __attribute__((address_space(3))) char lds_char;
   const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_char*)smem;
 
+  stamp(p, 0);
   const int gtid = threadIdx.x;                                   // 0..511
   const int grp = __builtin_amdgcn_readfirstlane(gtid >> 8);     // pixel group
   const int tid = gtid & 255, lane = tid & 63, wid = tid >> 6;   // within the group
@@ -1206,6 +1217,7 @@ conv_halo2_kernel(const ConvParams p) {
     const int wtap = FLIP ? 8 - t : t;
     glds16(b_ok ? b_row + wtap * p.Cin : zero, lds0 + PATCH + (uint32_t)(t * BT) + wave_off);
   }
+  stamp(p, 1);
 
   f32x4 acc[MI][NI];
 #pragma unroll
@@ -1240,6 +1252,7 @@ conv_halo2_kernel(const ConvParams p) {
       case 7: vm_wait_barrier<1>(); break;
       default: vm_wait_barrier<0>(); break;
     }
+    if (tap == 0) stamp(p, 2);
     const char* Ps = smem;
     const char* Bs = smem + PATCH + tap * BT;
     const int kh = tap / 3, kw = tap - (tap / 3) * 3;
@@ -1264,9 +1277,14 @@ conv_halo2_kernel(const ConvParams p) {
     }
   }
   __syncthreads();  // every LDS read of the patch / weights done: the C tile aliases them
+  stamp(p, 3);
   store_c_tile<BMG, BN>((float*)smem, ConvSmem<HALO2_CAP, BN>::CS, acc, grp * BMG, wid, lane);
   __syncthreads();
   conv_epilogue_rows<HALO2_CAP, BN, 512>(p, smem, m0, n0, PB, nullptr);
+  if (p.stamps != nullptr) {
+    __syncthreads();
+    stamp(p, 4);
+  }
 }
 
 // Split-K combine: y = epilogue(sum_z partial[z]) in fixed z order.
@@ -1407,6 +1425,15 @@ int launch_tile(const ConvParams& p, int mode, int splits, hipStream_t st) {
 }
 
 }  // namespace
+
+uint64_t* g_stamps = nullptr;  // diagnostics (mda_conv_set_stamps)
+
+// Diagnostics: subsequent conv launches write per-block phase timestamps into
+// buf (8 x uint64 per block; instrumented kernels only); null turns it off.
+MDA_API int mda_conv_set_stamps(void* buf) {
+  g_stamps = (uint64_t*)buf;
+  return 0;
+}
 
 // Host-side tile / split-K choice (also used by Python to size the workspace).
 // Returns tile code BM*1000+BN in *tile and the split count in *splits.
@@ -1553,6 +1580,7 @@ MDA_API int mda_conv_fwd(const void* x, const void* w, const float* scale, const
   p.par = 0;
   p.zsplits = 1;
   p.stats_part = nullptr;
+  p.stamps = g_stamps;
   int mode = (Cin % BK == 0) ? LOAD_FAST : (Cin % 8 == 0 ? LOAD_VEC8 : LOAD_SCALAR);
   return dispatch(p, mode, tile, splits, st, halo_eligible(p) ? 1 : 0);
 }
@@ -1577,6 +1605,7 @@ MDA_API int mda_conv_dgrad(const void* dy, const void* wt, void* dx, float* part
   p.par = 0;
   p.zsplits = 1;
   p.stats_part = nullptr;
+  p.stamps = g_stamps;
   // strided dgrad: one GEMM per output-parity class with only its taps
   if (stride > 1 && mode == LOAD_DGRAD_FAST && use_glds() && use_par_dgrad()) p.par = (int)stride;
   // stride-1 3x3 pad-1 dgrad is a "same" conv of dy with the mirrored taps
@@ -1618,6 +1647,7 @@ MDA_API int mda_conv_fwd_bnstats(const void* x, const void* w, void* y, float* p
   p.par = 0;
   p.zsplits = 1;
   p.stats_part = nullptr;
+  p.stamps = g_stamps;
   if (Cout % 8 || Cout > 2048) return (int)hipErrorInvalidValue;
   int mode = (Cin % BK == 0) ? LOAD_FAST : (Cin % 8 == 0 ? LOAD_VEC8 : LOAD_SCALAR);
   if (tile == 0 || splits == 0) mda_conv_plan(p.M, p.Cout, p.Kp, &tile, &splits);

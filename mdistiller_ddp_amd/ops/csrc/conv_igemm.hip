@@ -150,13 +150,15 @@ __device__ __forceinline__ void epilogue_store(const ConvParams& p, int m, int c
 // residual load, preact and output stores; sc/bi already hold the channels'
 // scale and bias.
 __device__ __forceinline__ void epilogue_store8(const ConvParams& p, int m, int co, const float* v,
-                                                const float* sc, const float* bi) {
+                                                const float* sc, const float* bi,
+                                                uint4 res_reg = make_uint4(0u, 0u, 0u, 0u),
+                                                bool use_reg = false) {
   const int64_t o = (int64_t)m * p.Cout + co;
   float t[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) t[e] = v[e] * sc[e] + bi[e];
   if (p.res) {
-    const uint4 r = *(const uint4*)(p.res + o);
+    const uint4 r = use_reg ? res_reg : *(const uint4*)(p.res + o);
     const uint32_t rr[4] = {r.x, r.y, r.z, r.w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -212,18 +214,62 @@ __device__ __forceinline__ void store_c_tile(float* Cs, int CS, const f32x4 (&ac
         Cs[(row0 + wm * (BMg / 2) + i * 16 + erow + r) * CS + wn * (BN / 2) + j * 16 + ecol] = acc[i][j][r];
 }
 
+// Epilogue operands of one thread (its 8 channels' scale / bias and, when the
+// row count is small, its residual rows), loaded at kernel start, BEFORE the
+// first LDS-DMA is issued (older than every DMA, so the vmcnt-counted waits
+// of the main loop stay exact).  Loaded after the main loop instead, their
+// global latency serialises with the stores: in-kernel stamps put the halo
+// conv epilogue at ~3.7 of ~11.4 us, one round trip of it being these loads.
+template <int BM, int BN, int NT>
+struct EpiPre {
+  static constexpr int TPR = BN / 8;                  // threads per row
+  static constexpr int RPP = NT / TPR;                // rows per pass
+  static constexpr int RPT = (BM + RPP - 1) / RPP;    // passes
+  static constexpr bool RES = RPT <= 4;               // residual rows held in registers
+  float sc[8], bi[8];
+  uint4 res[RES ? RPT : 1];
+  bool have;                                          // sc / bi valid
+  bool have_res;                                      // res valid
+};
+
+template <int BM, int BN, int NT>
+__device__ __forceinline__ void epi_prefetch(const ConvParams& p, EpiPre<BM, BN, NT>& e, int m0, int n0,
+                                             int rows, bool par) {
+  using E = EpiPre<BM, BN, NT>;
+  const int tid = threadIdx.x;
+  const int c8 = tid % E::TPR, rr = tid / E::TPR;
+  const int co = n0 + c8 * 8;
+  const bool split = par ? p.zsplits > 1 : gridDim.z > 1;
+  e.have = !split && p.stats_part == nullptr && (p.Cout & 7) == 0 && co < p.Cout;
+  e.have_res = false;
+  if (!e.have) return;
+  load_scale_bias8(p, co, e.sc, e.bi);
+  if (E::RES && p.res != nullptr && !par) {
+    e.have_res = true;
+#pragma unroll
+    for (int k = 0; k < (E::RES ? E::RPT : 1); ++k) {
+      const int r0 = rr + k * E::RPP;
+      const int m = m0 + r0;
+      e.res[k] = (r0 < rows && m < p.M) ? *(const uint4*)(p.res + (int64_t)m * p.Cout + co)
+                                        : make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
+}
+
 template <int BM, int BN, int NT = 256>
 __device__ __forceinline__ void conv_epilogue_rows(const ConvParams& p, char* smem, int m0, int n0,
-                                                   int rows, const ParClass* pc);
+                                                   int rows, const ParClass& pc, bool has_pc,
+                                                   const EpiPre<BM, BN, NT>& pre);
 
 template <int BM, int BN>
 __device__ __forceinline__ void conv_epilogue(const ConvParams& p, const f32x4 (&acc)[BM / 32][BN / 32],
-                                              char* smem, int m0, int n0, int rows = BM,
-                                              const ParClass* pc = nullptr) {
+                                              char* smem, int m0, int n0, int rows,
+                                              const ParClass& pc, bool has_pc,
+                                              const EpiPre<BM, BN, 256>& pre) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   store_c_tile<BM, BN>((float*)smem, ConvSmem<BM, BN>::CS, acc, 0, wid, lane);
   __syncthreads();
-  conv_epilogue_rows<BM, BN, 256>(p, smem, m0, n0, rows, pc);
+  conv_epilogue_rows<BM, BN, 256>(p, smem, m0, n0, rows, pc, has_pc, pre);
 }
 
 // Phase 2: NT threads own 8 channels x rows of the C tile: bias / BN affine,
@@ -231,7 +277,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, const f32x4 (
 // output + BN statistics partials.  Every barrier is reached by all threads.
 template <int BM, int BN, int NT>
 __device__ __forceinline__ void conv_epilogue_rows(const ConvParams& p, char* smem, int m0, int n0,
-                                                   int rows, const ParClass* pc) {
+                                                   int rows, const ParClass& pc, bool has_pc,
+                                                   const EpiPre<BM, BN, NT>& pre) {
   constexpr int CS = ConvSmem<BM, BN>::CS;
   const int tid = threadIdx.x;
   float* const Cs = (float*)smem;
@@ -240,9 +287,9 @@ __device__ __forceinline__ void conv_epilogue_rows(const ConvParams& p, char* sm
   const int c8 = tid % TPR;
   const int rr = tid / TPR;
   const int co = n0 + c8 * 8;
-  const int zsplit = pc ? (int)blockIdx.z % p.zsplits : (int)blockIdx.z;
-  const bool split = pc ? p.zsplits > 1 : gridDim.z > 1;
-  const int mlim = pc ? pc->Mc : p.M;
+  const int zsplit = has_pc ? (int)blockIdx.z % p.zsplits : (int)blockIdx.z;
+  const bool split = has_pc ? p.zsplits > 1 : gridDim.z > 1;
+  const int mlim = has_pc ? pc.Mc : p.M;
   if (p.stats_part != nullptr) {
     // raw bf16 output + BN statistics partials of this block's rows.  No early
     // return before the barrier: threads past Cout just contribute zeros.
@@ -286,13 +333,31 @@ __device__ __forceinline__ void conv_epilogue_rows(const ConvParams& p, char* sm
   }
   if ((p.Cout & 7) == 0) {
     if (co >= p.Cout) return;
+    using E = EpiPre<BM, BN, NT>;
+    if (pre.have) {
+      // operands already in registers (epi_prefetch); fully unrolled so the
+      // residual array stays in VGPRs
+#pragma unroll
+      for (int k = 0; k < E::RPT; ++k) {
+        const int r0 = rr + k * RPP;
+        int m = m0 + r0;
+        if (r0 < rows && m < mlim) {  // (no break: keeps the loop fully unrolled)
+          if (has_pc) m = par_row(p, pc, m);
+          const float4 lo = *(const float4*)&Cs[r0 * CS + c8 * 8];
+          const float4 hi = *(const float4*)&Cs[r0 * CS + c8 * 8 + 4];
+          const float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+          epilogue_store8(p, m, co, v, pre.sc, pre.bi, pre.res[E::RES ? k : 0], pre.have_res);
+        }
+      }
+      return;
+    }
     float sc[8], bi[8];
     if (!split) load_scale_bias8(p, co, sc, bi);
 #pragma unroll 2
     for (int r0 = rr; r0 < rows; r0 += RPP) {
       int m = m0 + r0;
       if (m >= mlim) break;
-      if (pc) m = par_row(p, *pc, m);
+      if (has_pc) m = par_row(p, pc, m);
       const float4 lo = *(const float4*)&Cs[r0 * CS + c8 * 8];
       const float4 hi = *(const float4*)&Cs[r0 * CS + c8 * 8 + 4];
       if (split) {
@@ -308,7 +373,7 @@ __device__ __forceinline__ void conv_epilogue_rows(const ConvParams& p, char* sm
     for (int r0 = rr; r0 < rows; r0 += RPP) {
       int m = m0 + r0;
       if (m >= mlim) break;
-      if (pc) m = par_row(p, *pc, m);
+      if (has_pc) m = par_row(p, pc, m);
       for (int e = 0; e < 8; ++e) {
         if (co + e >= p.Cout) break;
         const float a = Cs[r0 * CS + c8 * 8 + e];
@@ -346,6 +411,8 @@ conv_fwd_kernel(const ConvParams p) {
   const int wm = wid >> 1, wn = wid & 1;
   const int m0 = blockIdx.x * BM;
   const int n0 = blockIdx.y * BN;
+  EpiPre<BM, BN, 256> pre;
+  epi_prefetch(p, pre, m0, n0, BM, false);
   const int chunk = tid & 7;
   const int arow = tid >> 3;
   const int HoWo = p.Ho * p.Wo;
@@ -533,7 +600,7 @@ conv_fwd_kernel(const ConvParams p) {
   }
 
   __syncthreads();  // (loop ended with a barrier; keeps the C tile write safe either way)
-  conv_epilogue<BM, BN>(p, acc, smem, m0, n0);
+  conv_epilogue<BM, BN>(p, acc, smem, m0, n0, BM, ParClass{}, false, pre);
 }
 
 // ---------------------------------------------------------------------------
@@ -611,14 +678,16 @@ conv_glds_kernel(const ConvParams p) {
   const uint32_t wave_off = (uint32_t)__builtin_amdgcn_readfirstlane(wid) * 1024u;
   const int HoWo = p.Ho * p.Wo;
   const bf16_t* const zero = (const bf16_t*)g_zero16;
-  // strided-dgrad parity class (see ConvParams::par); pc == nullptr otherwise
+  // strided-dgrad parity class (see ConvParams::par); unused otherwise
   const bool PAR = DGRAD && FASTK && p.par > 1;
-  ParClass pcv;
+  ParClass pcv{};
   if (PAR) {
     pcv = par_class(p, (int)blockIdx.z / p.zsplits);
     if (m0 >= pcv.Mc) return;                             // whole block past this class
   }
   const int mlim = PAR ? pcv.Mc : p.M;
+  EpiPre<BM, BN, 256> pre;
+  epi_prefetch(p, pre, m0, n0, BM, PAR);
 
   int a_img[AROWS], a_ih0[AROWS], a_iw0[AROWS];
 #pragma unroll
@@ -752,7 +821,7 @@ conv_glds_kernel(const ConvParams p) {
     cbuf = cbuf == 2 ? 0 : cbuf + 1;
   }
   vm_wait_barrier<0>();  // drain the zero-page prefetches; all reads done before the C tile
-  conv_epilogue<BM, BN>(p, acc, smem, m0, n0, BM, PAR ? &pcv : nullptr);
+  conv_epilogue<BM, BN>(p, acc, smem, m0, n0, BM, pcv, PAR, pre);
 }
 
 // ---------------------------------------------------------------------------
@@ -824,6 +893,8 @@ conv_halo_kernel(const ConvParams p) {
   const int grow0 = m0 / W;                   // first global output row (n*H + oh)
   const int img0 = grow0 / H;
   const int oh0 = grow0 - img0 * H;
+  EpiPre<BM, BN, 256> pre;
+  epi_prefetch(p, pre, m0, n0, PB, false);
 
   // patch DMA: piece j covers patch rows 32j..32j+31; this thread's row/chunk
   const int trow = tid >> 3;
@@ -961,7 +1032,7 @@ conv_halo_kernel(const ConvParams p) {
     pbuf ^= 1;
   }
   vm_wait_barrier<0>();
-  conv_epilogue<BM, BN>(p, acc, smem, m0, n0, PB);
+  conv_epilogue<BM, BN>(p, acc, smem, m0, n0, PB, ParClass{}, false, pre);
 }
 
 // Single-chunk (Cin == 64) halo variant: the block's one patch is staged
@@ -1011,6 +1082,8 @@ conv_halo1_kernel(const ConvParams p) {
   const int grow0 = m0 / W;                   // first global output row (n*H + oh)
   const int img0 = grow0 / H;
   const int oh0 = grow0 - img0 * H;
+  EpiPre<BM, BN, 256> pre;
+  epi_prefetch(p, pre, m0, n0, PB, false);
 
   // patch DMA: piece j covers patch rows 32j..32j+31; this thread's row/chunk
   const int trow = tid >> 3;
@@ -1125,7 +1198,7 @@ conv_halo1_kernel(const ConvParams p) {
     compute(0, tap % RING, tap);
   }
   vm_wait_barrier<0>();
-  conv_epilogue<BM, BN>(p, acc, smem, m0, n0, PB);
+  conv_epilogue<BM, BN>(p, acc, smem, m0, n0, PB, ParClass{}, false, pre);
 }
 
 // Single-chunk (Cin == 64) halo conv with a 256-pixel block: two groups of
@@ -1179,6 +1252,8 @@ conv_halo2_kernel(const ConvParams p) {
   const int grow0 = m0 / W;
   const int img0 = grow0 / H;
   const int oh0 = grow0 - img0 * H;
+  EpiPre<HALO2_CAP, BN, 512> pre;
+  epi_prefetch(p, pre, m0, n0, PB, false);
 
   // DMA lanes: 64 rows (8 per wave) x 8 sixteen-byte chunks, XOR-swizzled
   const int trow = gtid >> 3;
@@ -1280,7 +1355,7 @@ conv_halo2_kernel(const ConvParams p) {
   stamp(p, 3);
   store_c_tile<BMG, BN>((float*)smem, ConvSmem<HALO2_CAP, BN>::CS, acc, grp * BMG, wid, lane);
   __syncthreads();
-  conv_epilogue_rows<HALO2_CAP, BN, 512>(p, smem, m0, n0, PB, nullptr);
+  conv_epilogue_rows<HALO2_CAP, BN, 512>(p, smem, m0, n0, PB, ParClass{}, false, pre);
   if (p.stamps != nullptr) {
     __syncthreads();
     stamp(p, 4);

@@ -622,10 +622,17 @@ __device__ __attribute__((aligned(16))) uint32_t g_zero16[4] = {0u, 0u, 0u, 0u};
 
 constexpr int GLDS_NBUF = 3;
 
-template <int BM, int BN>
+// RING = 1: single-stage blocks (K <= 64, e.g. the 1x1 expand convs of a
+// bottleneck): one LDS buffer, no dead prefetch stages, and a footprint of
+// max(stage, C tile) so 2-4 blocks share a CU and one block's DMA wait / MFMA
+// / epilogue overlap another's.  With three buffers a K = 64 block issued three
+// stages of DMAs (two of them zero-page dummies) and held 74-98 KB of LDS, one
+// block per CU, every phase serialised: 97 us for a 6.6 GFLOP 64->256 1x1 conv
+// at 56x56 x 64 that moves 128 MB (MIOpen: 23 us).
+template <int BM, int BN, int RING = GLDS_NBUF>
 struct GldsSmem {
   static constexpr int STAGE = (BM + BN) * 128;  // bytes per stage: A rows then B rows
-  static constexpr int PIPE = GLDS_NBUF * STAGE;
+  static constexpr int PIPE = RING * STAGE;
   static constexpr int CTILE = ConvSmem<BM, BN>::CTILE;
   static constexpr int BYTES = PIPE > CTILE ? PIPE : CTILE;
 };
@@ -648,22 +655,25 @@ __device__ __forceinline__ void vm_wait_barrier() {
   asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(N) : "memory");
 }
 
-template <int BM, int BN>
-struct GldsOcc { static constexpr int W = (BM * BN >= 16384) ? 1 : 2; };
+template <int BM, int BN, int RING = GLDS_NBUF>
+struct GldsOcc {
+  static constexpr int W = RING == 1 ? (BM * BN >= 16384 ? 2 : 4) : ((BM * BN >= 16384) ? 1 : 2);
+};
 
-template <int BM, int BN, int MODE>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GldsOcc<BM, BN>::W)))
+template <int BM, int BN, int MODE, int RING = GLDS_NBUF>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GldsOcc<BM, BN, RING>::W)))
 conv_glds_kernel(const ConvParams p) {
   constexpr int MI = BM / 32, NI = BN / 32;
   constexpr int AROWS = BM / 32;
   constexpr int BLOADS = (BN * 8 + 255) / 256;
   constexpr int NL = AROWS + BLOADS;  // DMA instructions per stage per wave
-  constexpr int STAGE = GldsSmem<BM, BN>::STAGE;
+  constexpr int STAGE = GldsSmem<BM, BN, RING>::STAGE;
   constexpr bool DGRAD = (MODE == LOAD_DGRAD_FAST || MODE == LOAD_DGRAD_VEC8);
   constexpr bool FASTK = (MODE == LOAD_FAST || MODE == LOAD_DGRAD_FAST);
   static_assert(MODE != LOAD_SCALAR, "SCALAR gathers use conv_fwd_kernel");
+  static_assert(RING == 1 || RING == GLDS_NBUF, "ring depth");
 
-  __shared__ __attribute__((aligned(16))) char smem[GldsSmem<BM, BN>::BYTES];
+  __shared__ __attribute__((aligned(16))) char smem[GldsSmem<BM, BN, RING>::BYTES];
   typedef __attribute__((address_space(3))) char lds_char;
   const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_char*)smem;
 
@@ -810,15 +820,24 @@ conv_glds_kernel(const ConvParams p) {
   };
 
   const int n = s_end - s_begin;
-  issue(s_begin, 0);
-  issue(s_begin + 1, 1);
-  int cbuf = 0;
-  for (int t = 0; t < n; ++t) {
-    vm_wait_barrier<NL>();  // stage t landed everywhere; stage t-1 reads retired everywhere
-    const int ibuf = cbuf == 0 ? 2 : cbuf - 1;  // (t + 2) % 3
-    issue(s_begin + t + 2, ibuf);
-    compute(cbuf);
-    cbuf = cbuf == 2 ? 0 : cbuf + 1;
+  if constexpr (RING == 1) {
+    for (int t = 0; t < n; ++t) {
+      if (t) __syncthreads();  // every read of the previous stage retired
+      issue(s_begin + t, 0);
+      vm_wait_barrier<0>();    // landed everywhere
+      compute(0);
+    }
+  } else {
+    issue(s_begin, 0);
+    issue(s_begin + 1, 1);
+    int cbuf = 0;
+    for (int t = 0; t < n; ++t) {
+      vm_wait_barrier<NL>();  // stage t landed everywhere; stage t-1 reads retired everywhere
+      const int ibuf = cbuf == 0 ? 2 : cbuf - 1;  // (t + 2) % 3
+      issue(s_begin + t + 2, ibuf);
+      compute(cbuf);
+      cbuf = cbuf == 2 ? 0 : cbuf + 1;
+    }
   }
   vm_wait_barrier<0>();  // drain the zero-page prefetches; all reads done before the C tile
   conv_epilogue<BM, BN>(p, acc, smem, m0, n0, BM, pcv, PAR, pre);
@@ -1464,6 +1483,15 @@ int halo_ring() {
   return v;
 }
 
+// largest per-block K-step count that takes the single-stage glds variant
+int ring1_max() {
+  static const int v = [] {
+    const char* e = getenv("MDA_GLDS_RING1_MAX");
+    return e ? atoi(e) : 4;
+  }();
+  return v;
+}
+
 bool use_glds() {
   static const bool on = [] {
     const char* e = getenv("MDA_CONV_GLDS");
@@ -1475,6 +1503,17 @@ bool use_glds() {
 template <int BM, int BN>
 int launch_tile(const ConvParams& p, int mode, int splits, hipStream_t st) {
   dim3 grid((p.M + BM - 1) / BM, (p.Cout + BN - 1) / BN, splits);
+  if (mode != LOAD_SCALAR && use_glds() && p.steps_per_split <= ring1_max()) {  // short-K blocks
+    if (mode == LOAD_FAST)
+      hipLaunchKernelGGL((conv_glds_kernel<BM, BN, LOAD_FAST, 1>), grid, dim3(256), 0, st, p);
+    else if (mode == LOAD_VEC8)
+      hipLaunchKernelGGL((conv_glds_kernel<BM, BN, LOAD_VEC8, 1>), grid, dim3(256), 0, st, p);
+    else if (mode == LOAD_DGRAD_FAST)
+      hipLaunchKernelGGL((conv_glds_kernel<BM, BN, LOAD_DGRAD_FAST, 1>), grid, dim3(256), 0, st, p);
+    else
+      hipLaunchKernelGGL((conv_glds_kernel<BM, BN, LOAD_DGRAD_VEC8, 1>), grid, dim3(256), 0, st, p);
+    return (int)hipGetLastError();
+  }
   if (mode != LOAD_SCALAR && use_glds()) {
     if (mode == LOAD_FAST)
       hipLaunchKernelGGL((conv_glds_kernel<BM, BN, LOAD_FAST>), grid, dim3(256), 0, st, p);
@@ -1517,10 +1556,11 @@ MDA_API int mda_conv_plan(int64_t M, int64_t Cout, int64_t Kp, int64_t* tile, in
   int bn = Cout <= 32 ? 32 : (Cout <= 64 ? 64 : 128);
   int bm = 128;
   auto blocks = [&](int bm_, int bn_) { return ((M + bm_ - 1) / bm_) * ((Cout + bn_ - 1) / bn_); };
+  int64_t steps = Kp / BK;
+  if (steps <= ring1_max() && bn == 128) bn = 64;  // short K: 4 blocks per CU (see GldsSmem)
   if (blocks(bm, bn) < target && bn == 128) bn = 64;
   if (blocks(bm, bn) < target) bm = 64;
   int64_t nb = blocks(bm, bn);
-  int64_t steps = Kp / BK;
   int64_t sp = 1;
   while (nb * sp < target && steps / (sp * 2) >= 4 && sp < 8) sp *= 2;
   *tile = bm * 1000 + bn;

@@ -30,6 +30,24 @@ SHAPES = [  # N, Cin, H, Cout, k, s, p
     (64, 256, 8, 256, 3, 1, 1),
     (64, 64, 32, 128, 1, 2, 0),
 ]
+IMAGENET = [  # ResNet-50 teacher at batch 64, ResNet-18 student at batch 32
+    (64, 64, 56, 64, 1, 1, 0),
+    (64, 64, 56, 256, 1, 1, 0),
+    (64, 256, 56, 64, 1, 1, 0),
+    (64, 64, 56, 64, 3, 1, 1),
+    (64, 256, 56, 512, 1, 2, 0),
+    (64, 128, 28, 512, 1, 1, 0),
+    (64, 512, 28, 128, 1, 1, 0),
+    (64, 128, 28, 128, 3, 1, 1),
+    (64, 1024, 14, 256, 1, 1, 0),
+    (64, 256, 14, 1024, 1, 1, 0),
+    (64, 512, 7, 2048, 1, 1, 0),
+    (64, 2048, 7, 512, 1, 1, 0),
+    (32, 64, 56, 64, 3, 1, 1),
+    (32, 128, 28, 128, 3, 1, 1),
+    (32, 256, 14, 256, 3, 1, 1),
+    (32, 512, 7, 512, 3, 1, 1),
+]
 
 
 def timeit(fn, iters):
@@ -51,12 +69,14 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--shape", type=int, default=-1, help="index into SHAPES (-1 = all)")
     ap.add_argument("--ops", default="fwd,mio,wgrad,dgrad")
+    ap.add_argument("--set", default="cifar", choices=["cifar", "imagenet"])
     args = ap.parse_args()
     ops = set(args.ops.split(","))
     from mdistiller_ddp_amd.ops import hip_layers, hip_train
     torch.backends.cudnn.benchmark = True
     rows = []
-    shapes = SHAPES if args.shape < 0 else [SHAPES[args.shape]]
+    table = SHAPES if args.set == "cifar" else IMAGENET
+    shapes = table if args.shape < 0 else [table[args.shape]]
     nan = float("nan")
     for (N, Cin, H, Cout, k, s, p) in shapes:
         conv = nn.Conv2d(Cin, Cout, k, s, p, bias=False).cuda()
@@ -75,7 +95,8 @@ def main():
                 t_dg = timeit(lambda: hip_train.conv_dgrad(dy, conv.weight, tuple(x.shape), s, p), args.iters)
         row = dict(shape=[N, Cin, H, Cout, k, s, p], gflop=flop / 1e9, fwd_us=t_fwd,
                    fwd_tflops=flop / t_fwd / 1e6, miopen_fwd_us=t_mio, dgrad_us=t_dg,
-                   wgrad_us=t_wg, wgrad_tflops=flop / t_wg / 1e6)
+                   wgrad_us=t_wg, wgrad_tflops=flop / t_wg / 1e6, dgrad_tflops=flop / t_dg / 1e6,
+                   miopen_tflops=flop / t_mio / 1e6)
         rows.append(row)
         print(json.dumps({k_: (round(v, 2) if isinstance(v, float) else v) for k_, v in row.items()}),
               flush=True)

@@ -45,7 +45,7 @@ SIGNATURES = {
     "mda_maxpool_fwd": "ppp" + "i" * 9 + "s",
     "mda_maxpool_bwd": "ppp" + "i" * 9 + "s",
     "mda_pack_conv_weights_pad": "pp" + "i" * 6 + "s",
-    "mda_wgrad_plan": "iiip",
+    "mda_wgrad_plan": "iiiiiip",
     "mda_pack_conv_weights": "ppp" + "i" * 6 + "s",
     "mda_pack_conv_weights_multi": "piis",
     "mda_pack_tiles": "iiiip",

@@ -634,7 +634,11 @@ struct GldsSmem {
   static constexpr int STAGE = (BM + BN) * 128;  // bytes per stage: A rows then B rows
   static constexpr int PIPE = RING * STAGE;
   static constexpr int CTILE = ConvSmem<BM, BN>::CTILE;
-  static constexpr int BYTES = PIPE > CTILE ? PIPE : CTILE;
+  // the BN-statistics reduction of conv_epilogue_rows: [2][RPP][BN] floats
+  // (256 threads: RPP * BN = 2048) -- larger than a small tile's single stage
+  static constexpr int RED = 2 * 2048 * 4;
+  static constexpr int BYTES0 = PIPE > CTILE ? PIPE : CTILE;
+  static constexpr int BYTES = BYTES0 > RED ? BYTES0 : RED;
 };
 
 __device__ __forceinline__ void glds16(const void* src, uint32_t lds_wave_base) {

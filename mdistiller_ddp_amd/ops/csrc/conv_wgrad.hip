@@ -227,36 +227,256 @@ conv_wgrad_kernel(const WgParams p) {
       }
 }
 
+// ---------------------------------------------------------------------------
+// LDS-DMA wgrad (FAST / VEC8 modes).  The register-staged kernel above held
+// one stage in flight per block and one block per CU for the ImageNet layers
+// (M = 100-200 K pixels, 9-64 (co, k) tiles -> ~300 blocks): every 64-pixel
+// stage paid a global-load round trip, ~56 TFLOP/s on a ResNet-18 at batch
+// 32.  Here both operands go global -> LDS with global_load_lds_dwordx4
+// through a 3-buffer ring (two stages in flight, one barrier per stage, as
+// conv_glds_kernel), the block tile grows to 128 x 128 where the layer allows
+// (64 x 64 per wave: LDS reads at half the MFMA time), and the split count
+// targets several blocks per CU.
+//
+// Stage layout: [64 px][64 ch] bf16 subtiles of 128-B rows, TCo/64 of dy then
+// TKk/64 of im2col(x).  A DMA instruction of wave w writes rows
+// 32 d + 8 w + (lane >> 3), slot lane & 7, which holds the global 16-B chunk
+// slot ^ wg_swz(row).  The fragment reads are ds_read_b64_tr_b16: in each 32-
+// lane group they touch rows {q, 8 + q} (+ 4) x a 32-B chunk pair; rows of
+// one parity share a bank half, so the XOR (even, keeps the pair) separates
+// rows whose bits 1 and 3 differ -> conflict-free.
+constexpr int WG_NBUF = 3;
+__device__ __attribute__((aligned(16))) uint32_t g_wg_zero16[4] = {0u, 0u, 0u, 0u};
+
+__device__ __forceinline__ int wg_swz(int r) { return (((r >> 1) & 1) | (((r >> 3) & 1) << 1)) << 1; }
+
+__device__ __forceinline__ void wg_glds16(const void* src, uint32_t lds_wave_base) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds_wave_base)
+      : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wg_wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(N) : "memory");
+}
+
+template <int TCo, int TKk>
+struct WgOcc { static constexpr int W = (TCo * TKk >= 16384) ? 1 : 3; };
+
+template <int TCo, int TKk>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WgOcc<TCo, TKk>::W)))
+conv_wgrad_glds_kernel(const WgParams p) {
+  constexpr int SC = TCo / 64, SK = TKk / 64;  // 64-wide subtiles of dy / im2col(x)
+  constexpr int SUB = 64 * 128;                // bytes per [64 px][64 ch] subtile
+  constexpr int STAGE = (SC + SK) * SUB;
+  constexpr int NL = 2 * (SC + SK);            // DMA instructions per wave per stage
+  constexpr int MI = TCo / 32, NI = TKk / 32;  // 16x16 tiles per wave (wave tile TCo/2 x TKk/2)
+  __shared__ __attribute__((aligned(16))) char smem[WG_NBUF * STAGE];
+  typedef __attribute__((address_space(3))) char lds_char;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_char*)smem;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int co0 = blockIdx.x * TCo;
+  const int k0 = blockIdx.y * TKk;
+  const int m_begin = blockIdx.z * p.m_per_split;
+  const int m_end = min(p.M, m_begin + p.m_per_split);
+  const uint32_t wave_off = (uint32_t)__builtin_amdgcn_readfirstlane(wid) * 1024u;
+  const bf16_t* const zero = (const bf16_t*)g_wg_zero16;
+
+  // per-lane DMA geometry (fixed for the block): rows and swizzled chunks
+  int drow[2], dch[2];
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {
+    drow[d] = 32 * d + 8 * wid + (lane >> 3);
+    dch[d] = (lane & 7) ^ wg_swz(drow[d]);
+  }
+  int dy_col[SC][2];
+  bool dy_ok[SC][2];
+  int x_kh[SK][2], x_kw[SK][2], x_c[SK][2];
+  bool x_ok[SK][2];
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {
+#pragma unroll
+    for (int sc = 0; sc < SC; ++sc) {
+      const int col = co0 + 64 * sc + dch[d] * 8;
+      dy_ok[sc][d] = col < p.Cout;
+      dy_col[sc][d] = dy_ok[sc][d] ? col : 0;
+    }
+#pragma unroll
+    for (int sk = 0; sk < SK; ++sk) {
+      const int k = k0 + 64 * sk + dch[d] * 8;
+      x_ok[sk][d] = k < p.K;
+      const int kk = x_ok[sk][d] ? k : 0;
+      const int tap = kk / p.Cin;
+      x_c[sk][d] = kk - tap * p.Cin;
+      x_kh[sk][d] = tap / p.KW;
+      x_kw[sk][d] = tap - x_kh[sk][d] * p.KW;
+    }
+  }
+
+  // every copy of the 64-pixel stage starting at mb into buffer buf (always NL per wave)
+  auto issue = [&](int mb, int buf) {
+    const uint32_t base = lds0 + (uint32_t)(buf * STAGE) + wave_off;
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      const int m = mb + drow[d];
+      const bool mok = m < m_end;
+      const int mm = mok ? m : 0;
+      const int n = fdiv(mm, p.div_howo);
+      const int rr = mm - n * p.Ho * p.Wo;
+      const int oh = fdiv(rr, p.div_wo);
+      const int ow = rr - oh * p.Wo;
+#pragma unroll
+      for (int sc = 0; sc < SC; ++sc) {
+        const bf16_t* src = (mok && dy_ok[sc][d]) ? p.dy + ((int64_t)mm * p.Cout + dy_col[sc][d]) : zero;
+        wg_glds16(src, base + (uint32_t)(sc * SUB + d * 4096));
+      }
+#pragma unroll
+      for (int sk = 0; sk < SK; ++sk) {
+        const int ih = oh * p.stride - p.pad + x_kh[sk][d];
+        const int iw = ow * p.stride - p.pad + x_kw[sk][d];
+        const bool ok = mok && x_ok[sk][d] && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+        const bf16_t* src = ok ? p.x + ((int64_t)((n * p.H + ih) * p.W + iw) * p.Cin + x_c[sk][d]) : zero;
+        wg_glds16(src, base + (uint32_t)((SC + sk) * SUB + d * 4096));
+      }
+    }
+  };
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // transposing fragment reads: lane 16g + 4q + p reads rows r0 + 8g + q (+4),
+  // bf16 columns c0 + 4p .. +3 and receives column (lane & 15), rows r0 + 8g .. +7.
+  // The swizzle depends on row bits 1 and 3 only (= q >> 1, g & 1): fixed per lane.
+  const int fg = lane >> 4, fq = (lane >> 2) & 3, fp = lane & 3;
+  const int fswz = ((fq >> 1) | ((fg & 1) << 1)) << 1;
+  const int frow_off = (8 * fg + fq) * 128 + (fp & 1) * 8;
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  auto frag = [&](const char* tile, int r0, int c0) {
+    const char* a = tile + r0 * 128 + frow_off + ((((c0 >> 3) + (fp >> 1)) ^ fswz) << 4);
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a + 4 * 128));
+    bf16x8 out;
+    short* o = (short*)&out;
+    o[0] = lo[0]; o[1] = lo[1]; o[2] = lo[2]; o[3] = lo[3];
+    o[4] = hi[0]; o[5] = hi[1]; o[6] = hi[2]; o[7] = hi[3];
+    return out;
+  };
+  auto compute = [&](int buf) {
+    const char* Ds = smem + buf * STAGE;
+    const char* Xs = Ds + SC * SUB;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[MI], bfr[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int c = wm * (TCo / 2) + i * 16;  // local co
+        af[i] = frag(Ds + (c >> 6) * SUB, kk * 32, c & 63);
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int c = wn * (TKk / 2) + j * 16;  // local k
+        bfr[j] = frag(Xs + (c >> 6) * SUB, kk * 32, c & 63);
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  const int n = (m_end - m_begin + 63) / 64;
+  issue(m_begin, 0);
+  issue(m_begin + 64, 1);
+  int cbuf = 0;
+  for (int t = 0; t < n; ++t) {
+    wg_wait_barrier<NL>();  // stage t landed everywhere; stage t-1 reads retired everywhere
+    const int ibuf = cbuf == 0 ? 2 : cbuf - 1;
+    issue(m_begin + (t + 2) * 64, ibuf);
+    compute(cbuf);
+    cbuf = cbuf == 2 ? 0 : cbuf + 1;
+  }
+  wg_wait_barrier<0>();  // drain the zero-page prefetches before the block retires
+
+  const int ecol = lane & 15, erow = (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int oc = co0 + wm * (TCo / 2) + i * 16 + erow + r;
+        const int k = k0 + wn * (TKk / 2) + j * 16 + ecol;
+        if (oc < p.Cout && k < p.Kp)
+          p.partial[((int64_t)blockIdx.z * p.Cout + oc) * p.Kp + k] = acc[i][j][r];
+      }
+}
+
 // grad[co][ci][kh][kw] (+)= scale * sum_s partial[s][co][(kh*KW+kw)*Cin+ci]
-// Threads walk the packed (co, k) order so the split partials are read
-// coalesced; the OIHW write is the only scattered access.
+// Block = 4 waves x 64 lanes; a lane owns 4 consecutive packed (co, k)
+// elements (one float4 per partial set), wave w sums the sets s = w (mod 4)
+// with four loads in flight, and wave 0 combines the four in a fixed order
+// (deterministic).  The element-per-thread version walked all the sets
+// serially per thread (~9 us for a 64-set ResNet layer).
 __global__ void __launch_bounds__(256)
 wgrad_reduce_kernel(const float* __restrict__ partial, float* __restrict__ grad, int splits,
                     int Cout, int Cin, int KH, int KW, int Kp, float scale, int accumulate,
                     int cin_keep) {
-  const int K = Cin * KH * KW;
-  const int64_t total = (int64_t)Cout * K;
-  const int64_t sstride = (int64_t)Cout * Kp;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int co = (int)(i / K);
-    const int k = (int)(i - (int64_t)co * K);        // packed order: (kh*KW + kw)*Cin + ci
-    const int tap = k / Cin, ci = k - tap * Cin;
-    const int64_t src = (int64_t)co * Kp + k;
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    int s = 0;
-    for (; s + 4 <= splits; s += 4) {
-      a0 += partial[src + (s + 0) * sstride];
-      a1 += partial[src + (s + 1) * sstride];
-      a2 += partial[src + (s + 2) * sstride];
-      a3 += partial[src + (s + 3) * sstride];
+  __shared__ float4 red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t total4 = (int64_t)Cout * Kp / 4;
+  const int64_t e4 = (int64_t)blockIdx.x * 64 + lane;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e4 < total4) {
+    const float4* src = (const float4*)partial + e4;
+    float4 b = a, c = a, d = a;
+    int s = w;
+    for (; s + 12 < splits; s += 16) {
+      const float4 u0 = src[(int64_t)s * total4], u1 = src[(int64_t)(s + 4) * total4];
+      const float4 u2 = src[(int64_t)(s + 8) * total4], u3 = src[(int64_t)(s + 12) * total4];
+      a.x += u0.x; a.y += u0.y; a.z += u0.z; a.w += u0.w;
+      b.x += u1.x; b.y += u1.y; b.z += u1.z; b.w += u1.w;
+      c.x += u2.x; c.y += u2.y; c.z += u2.z; c.w += u2.w;
+      d.x += u3.x; d.y += u3.y; d.z += u3.z; d.w += u3.w;
     }
-    for (; s < splits; ++s) a0 += partial[src + s * sstride];
-    const float a = (a0 + a1) + (a2 + a3);
+    for (; s < splits; s += 4) {
+      const float4 u = src[(int64_t)s * total4];
+      a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+    }
+    a.x += b.x + (c.x + d.x); a.y += b.y + (c.y + d.y);
+    a.z += b.z + (c.z + d.z); a.w += b.w + (c.w + d.w);
+  }
+  red[w][lane] = a;
+  __syncthreads();
+  if (w != 0 || e4 >= total4) return;
+  const float4 r0 = red[0][lane], r1 = red[1][lane], r2 = red[2][lane], r3 = red[3][lane];
+  const float v[4] = {(r0.x + r1.x) + (r2.x + r3.x), (r0.y + r1.y) + (r2.y + r3.y),
+                      (r0.z + r1.z) + (r2.z + r3.z), (r0.w + r1.w) + (r2.w + r3.w)};
+  const int K = Cin * KH * KW;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int64_t e = e4 * 4 + q;
+    const int co = (int)(e / Kp);
+    const int k = (int)(e - (int64_t)co * Kp);   // packed order: (kh*KW + kw)*Cin + ci
+    if (k >= K) continue;                        // padding columns
+    const int tap = k / Cin, ci = k - tap * Cin;
     // channel-padded stems (Cin 3 -> 8): only the real input channels exist in grad
     if (ci >= cin_keep) continue;
     const int64_t dst = ((int64_t)co * cin_keep + ci) * KH * KW + tap;
-    grad[dst] = (accumulate ? grad[dst] : 0.f) + scale * a;
+    grad[dst] = (accumulate ? grad[dst] : 0.f) + scale * v[q];
   }
 }
 
@@ -434,11 +654,45 @@ MDA_API int mda_pack_tiles(int64_t Cout, int64_t Cin, int64_t KH, int64_t KW, in
   return 0;
 }
 
-MDA_API int mda_wgrad_plan(int64_t M, int64_t Cout, int64_t Kp, int64_t* splits) {
-  int64_t tiles = ((Cout + TC - 1) / TC) * ((Kp + TK - 1) / TK);
+// Kernel / block tile of a wgrad, from the kernel-level A/B on the ResNet
+// CIFAR and ImageNet shapes (profiles/r2_wgrad_ab.md): the LDS-DMA kernel with
+// 128 x 128 tiles for wide 1x1 layers (64 x 64 for narrow ones), 64 x 128 for
+// 3x3 layers with >= 20 K pixels; the register-staged kernel (0) for small-M
+// 3x3 layers and the scalar stem gather.  MDA_WG_TILE=<code> forces a tile,
+// MDA_WG_GLDS=0 the register-staged kernel.
+static int wg_tile(int64_t M, int64_t Cout, int64_t Cin, int64_t KH, int64_t KW, int64_t Kp) {
+  static const int forced = [] {
+    const char* e = getenv("MDA_WG_TILE");
+    return e ? atoi(e) : -1;
+  }();
+  static const bool glds = [] {
+    const char* e = getenv("MDA_WG_GLDS");
+    return !(e && e[0] == '0');
+  }();
+  if (Cin % 8 || !glds) return 0;
+  if (forced == 0 || forced == 64064 || forced == 64128 || forced == 128064 || forced == 128128) return forced;
+  if (KH * KW == 1) return (Cout >= 128 && Kp >= 128) ? 128128 : 64064;
+  return M >= 20000 ? 64128 : 0;
+}
+
+MDA_API int mda_wgrad_plan(int64_t M, int64_t Cout, int64_t Cin, int64_t KH, int64_t KW, int64_t Kp,
+                           int64_t* splits) {
+  const int tile = wg_tile(M, Cout, Cin, KH, KW, Kp);
   int64_t sp = 1;
-  // aim for >= 512 workgroups, keep >= 4 stages (256 pixels) per split
-  while (tiles * sp < 256 && (M / (sp * 2)) >= 4 * TM && sp < 64) sp *= 2;
+  if (tile == 0) {
+    // register-staged kernel: >= 256 workgroups, >= 4 stages (256 pixels) per split
+    const int64_t tiles = ((Cout + TC - 1) / TC) * ((Kp + TK - 1) / TK);
+    while (tiles * sp < 256 && (M / (sp * 2)) >= 4 * TM && sp < 64) sp *= 2;
+  } else {
+    const int tc = tile / 1000, tk = tile % 1000;
+    const int64_t tiles = ((Cout + tc - 1) / tc) * ((Kp + tk - 1) / tk);
+    // one round of blocks over the CU slots (LDS-limited blocks per CU), each
+    // split >= 8 stages of 64 pixels, at most 128 partial sets
+    const int64_t occ = tile == 128128 ? 1 : (tile == 64064 ? 3 : 2);
+    sp = (256 * occ + tiles - 1) / tiles;
+    sp = std::min<int64_t>(sp, std::max<int64_t>(1, M / (8 * TM)));
+    sp = std::max<int64_t>(1, std::min<int64_t>(sp, 128));
+  }
   *splits = sp;
   return 0;
 }
@@ -461,11 +715,21 @@ MDA_API int mda_conv_wgrad(const void* x, const void* dy, float* partial, float*
   p.dy_bytes = (int)db;
   p.div_howo = make_fastdiv((uint32_t)(Ho * Wo));
   p.div_wo = make_fastdiv((uint32_t)Wo);
-  if (splits <= 0) mda_wgrad_plan(p.M, Cout, Kp, &splits);
+  if (splits <= 0) mda_wgrad_plan(p.M, Cout, Cin, KH, KW, Kp, &splits);
   p.m_per_split = (int)(((p.M + splits - 1) / splits + TM - 1) / TM * TM);
-  dim3 grid((int)((Cout + TC - 1) / TC), (int)(Kp / TK), (int)splits);
   const int mode = (Cin % TK == 0) ? WG_FAST : (Cin % 8 == 0 ? WG_VEC8 : WG_SCALAR);
-  if (mode == WG_FAST)
+  dim3 grid((int)((Cout + TC - 1) / TC), (int)(Kp / TK), (int)splits);
+  const int tile = mode == WG_SCALAR ? 0 : wg_tile(p.M, Cout, Cin, KH, KW, Kp);
+  if (tile != 0) {
+    const int tc = tile / 1000, tk = tile % 1000;
+    dim3 g2((int)((Cout + tc - 1) / tc), (int)((Kp + tk - 1) / tk), (int)splits);
+    switch (tile) {
+      case 128128: hipLaunchKernelGGL((conv_wgrad_glds_kernel<128, 128>), g2, dim3(256), 0, st, p); break;
+      case 128064: hipLaunchKernelGGL((conv_wgrad_glds_kernel<128, 64>), g2, dim3(256), 0, st, p); break;
+      case 64128: hipLaunchKernelGGL((conv_wgrad_glds_kernel<64, 128>), g2, dim3(256), 0, st, p); break;
+      default: hipLaunchKernelGGL((conv_wgrad_glds_kernel<64, 64>), g2, dim3(256), 0, st, p); break;
+    }
+  } else if (mode == WG_FAST)
     hipLaunchKernelGGL(conv_wgrad_kernel<WG_FAST>, grid, dim3(256), 0, st, p);
   else if (mode == WG_VEC8)
     hipLaunchKernelGGL(conv_wgrad_kernel<WG_VEC8>, grid, dim3(256), 0, st, p);
@@ -473,8 +737,8 @@ MDA_API int mda_conv_wgrad(const void* x, const void* dy, float* partial, float*
     hipLaunchKernelGGL(conv_wgrad_kernel<WG_SCALAR>, grid, dim3(256), 0, st, p);
   int rc = (int)hipGetLastError();
   if (rc) return rc;
-  int64_t total = Cout * KH * KW * Cin;
-  int blocks = (int)std::min<int64_t>((total + 255) / 256, 1024);
+  const int64_t total4 = Cout * Kp / 4;  // Kp % 64 == 0
+  const int blocks = (int)((total4 + 63) / 64);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, partial, grad,
                      (int)splits, (int)Cout, (int)Cin, (int)KH, (int)KW, (int)Kp, scale,
                      (int)accumulate, (int)cin_keep);

@@ -57,12 +57,12 @@ def _ws(device):
 _WG_PLANS: dict = {}
 
 
-def _wgrad_splits(M, Cout, Kp):
-    key = (M, Cout, Kp)
+def _wgrad_splits(M, Cout, Cin, KH, KW, Kp):
+    key = (M, Cout, Cin, KH, KW, Kp)
     v = _WG_PLANS.get(key)
     if v is None:
         s = ctypes.c_int64(0)
-        _ext.call("mda_wgrad_plan", M, Cout, Kp, s)
+        _ext.call("mda_wgrad_plan", M, Cout, Cin, KH, KW, Kp, s)
         v = _WG_PLANS[key] = s.value
     return v
 
@@ -336,7 +336,7 @@ class _ConvBNActTrain(torch.autograd.Function):
                       stride, pad, KpT, tile, splits)
         dw = None
         if ctx.needs_input_grad[1]:
-            sp = _wgrad_splits(M, Cout, Kp)
+            sp = _wgrad_splits(M, Cout, Cin, KH, KW, Kp)
             part = torch.empty(sp * Cout * Kp, dtype=torch.float32, device=dev)
             direct_w = weight.grad is not None and weight.grad.is_contiguous()
             target = weight.grad if direct_w else torch.empty_like(weight, memory_format=torch.contiguous_format)
@@ -473,7 +473,7 @@ def conv_wgrad(x, dy, weight_shape, stride, pad):
     Ho, Wo = dy.shape[2], dy.shape[3]
     Kp = (KH * KW * Cin + 63) // 64 * 64
     M = N * Ho * Wo
-    sp = _wgrad_splits(M, Cout, Kp)
+    sp = _wgrad_splits(M, Cout, Cin, KH, KW, Kp)
     part = torch.empty(sp * Cout * Kp, dtype=torch.float32, device=x.device)
     out = torch.empty(weight_shape, dtype=torch.float32, device=x.device)
     _ext.call("mda_conv_wgrad", x, dy, part, out, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
@@ -588,7 +588,7 @@ class _ConvTrain(torch.autograd.Function):
                       stride, pad, KpT, tile, splits)
         dw = None
         if ctx.needs_input_grad[1]:
-            sp = _wgrad_splits(M, Cout, Kp)
+            sp = _wgrad_splits(M, Cout, Cin, KH, KW, Kp)
             part = torch.empty(sp * Cout * Kp, dtype=torch.float32, device=dev)
             direct_w = weight.grad is not None and weight.grad.is_contiguous()
             target = weight.grad if direct_w else torch.empty_like(weight, memory_format=torch.contiguous_format)

@@ -63,6 +63,30 @@ def timeit(fn, iters):
     return a.elapsed_time(b) * 1000.0 / iters
 
 
+def timeit_graph(fn, iters):
+    """GPU time per call with the Python/launch overhead removed: `iters`
+    calls captured in one hipGraph, replayed."""
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(iters):
+                fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g.replay()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    g.replay()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) * 1000.0 / iters
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=50)
@@ -70,7 +94,11 @@ def main():
     ap.add_argument("--shape", type=int, default=-1, help="index into SHAPES (-1 = all)")
     ap.add_argument("--ops", default="fwd,mio,wgrad,dgrad")
     ap.add_argument("--set", default="cifar", choices=["cifar", "imagenet"])
+    ap.add_argument("--graph", action="store_true", help="time hipGraph replays (no CPU overhead)")
     args = ap.parse_args()
+    global timeit
+    if args.graph:
+        timeit = timeit_graph
     ops = set(args.ops.split(","))
     from mdistiller_ddp_amd.ops import hip_layers, hip_train
     torch.backends.cudnn.benchmark = True

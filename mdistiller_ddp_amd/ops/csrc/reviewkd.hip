@@ -59,39 +59,84 @@ __device__ __forceinline__ int cell_level(int cell, const int (&off)[3], const f
   return 2;
 }
 
-__global__ void __launch_bounds__(256)
-hcl_kernel(const HclTable table, int L, float* __restrict__ partial, float weight,
-           const float* __restrict__ epoch, float warmup) {
-  extern __shared__ float sd[];  // [HW][CPB] differences
-  __shared__ float scratch[4];
-  __shared__ float cells[21 * 8];  // 4x4 + 2x2 + 1x1 cells, CPB <= 8
-  const int64_t* tb = table.v;
-  int lv = 0;
-  while (lv + 1 < L && (int64_t)blockIdx.x >= tb[(lv + 1) * HCL_FIELDS + 8]) ++lv;
-  const int64_t* e = tb + lv * HCL_FIELDS;
+constexpr int HCL_MAX_CPB = 32;
+constexpr int HCL_BINS = 7;  // x-bins of the three levels: 4 + 2 + 1
+
+// VW consecutive bf16 (VW in 1, 2, 4, 8) <-> floats
+template <int VW>
+__device__ __forceinline__ void ld_bf16(const bf16_t* p, float* v) {
+  if constexpr (VW == 8) {
+    const uint4 u = *(const uint4*)p;
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { v[2 * e] = __uint_as_float(w[e] << 16); v[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u); }
+  } else if constexpr (VW == 4) {
+    const uint2 u = *(const uint2*)p;
+    v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
+    v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
+  } else if constexpr (VW == 2) {
+    const uint32_t u = *(const uint32_t*)p;
+    v[0] = __uint_as_float(u << 16); v[1] = __uint_as_float(u & 0xffff0000u);
+  } else {
+    v[0] = bf2f(*p);
+  }
+}
+template <int VW>
+__device__ __forceinline__ void st_bf16(bf16_t* p, const float* v) {
+  if constexpr (VW == 8) {
+    *(uint4*)p = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
+                            pack_bf16x2(v[6], v[7]));
+  } else if constexpr (VW == 4) {
+    *(uint2*)p = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+  } else if constexpr (VW == 2) {
+    *(uint32_t*)p = pack_bf16x2(v[0], v[1]);
+  } else {
+    *p = f2bf(v[0]);
+  }
+}
+
+// One block = one image x CPB channels of one level.  Phases (fixed order ->
+// deterministic): stage d = fs - ft in LDS with VW-wide loads; row-bin sums
+// R[y][b][k] over each level's x-bins; cell sums over each cell's y-bin of R
+// (separable: every serial sum is <= one bin wide, where summing a whole
+// 56x56 map per thread made this one kernel 290 us of a ResNet-34 step);
+// loss partial; gradient with VW-wide stores.
+template <int VW>
+__device__ __forceinline__ void hcl_block(const int64_t* e, int local, float* partial, float weight,
+                                          const float* epoch, float warmup, float* sd, float* scratch,
+                                          float* cells) {
   const bf16_t* fs = (const bf16_t*)e[0];
   const bf16_t* ft = (const bf16_t*)e[1];
   bf16_t* grad = (bf16_t*)e[2];
   const int N = (int)e[3], H = (int)e[4], W = (int)e[5], C = (int)e[6], CPB = (int)e[7];
-  const int local = blockIdx.x - (int)e[8];
   const int groups = C / CPB;
   const int n = local / groups;
   const int c0 = (local - n * groups) * CPB;
   const int HW = H * W;
   const int tid = threadIdx.x;
-  // ---- stage d = fs - ft (CPB channels of each pixel)
+  float* const R = sd + HW * CPB;  // [H][HCL_BINS][CPB]
   const int64_t base = (int64_t)n * HW * C + c0;
+  // ---- stage d = fs - ft
   float sq = 0.f;
-  for (int q = tid; q < HW * CPB; q += blockDim.x) {
-    const int p = q / CPB, k = q - p * CPB;
+  const int nv = HW * CPB / VW;
+  for (int q = tid; q < nv; q += blockDim.x) {
+    const int e0 = q * VW;
+    const int p = e0 / CPB, k = e0 - p * CPB;
     const int64_t o = base + (int64_t)p * C + k;
-    const float d = bf2f(fs[o]) - bf2f(ft[o]);
-    sd[q] = d;
-    sq += d * d;
+    float a[VW], b[VW];
+    ld_bf16<VW>(fs + o, a);
+    ld_bf16<VW>(ft + o, b);
+#pragma unroll
+    for (int v = 0; v < VW; ++v) {
+      const float d = a[v] - b[v];
+      sd[e0 + v] = d;
+      sq += d * d;
+    }
   }
   const float sqsum = block_sum(sq, scratch);  // also orders the LDS writes
-  // ---- adaptive-pool cells: levels l = 4, 2, 1 with l < H (and l < W)
+  // ---- levels l = 4, 2, 1 with l < H (and l < W)
   const int levels[3] = {4, 2, 1};
+  const int bin0[3] = {0, 4, 6};
   int cell_off[3];
   float cnt[3];
   float tot = 1.f, cw = 1.f;
@@ -107,7 +152,22 @@ hcl_kernel(const HclTable table, int L, float* __restrict__ partial, float weigh
       ncell += l * l;
     }
   }
-  // one thread per (cell, channel), fixed-order sum over the cell's pixels
+  // ---- row-bin sums
+  for (int q = tid; q < H * HCL_BINS * CPB; q += blockDim.x) {
+    const int y = q / (HCL_BINS * CPB);
+    const int rem = q - y * (HCL_BINS * CPB);
+    const int b = rem / CPB, k = rem - b * CPB;
+    const int t = b < 4 ? 0 : (b < 6 ? 1 : 2);
+    const int l = levels[t], ix = b - bin0[t];
+    float s = 0.f;
+    if (cnt[t] > 0.f) {
+      const int x0 = bin_start(ix, W, l), x1 = bin_end(ix, W, l);
+      for (int xx = x0; xx < x1; ++xx) s += sd[(y * W + xx) * CPB + k];
+    }
+    R[q] = s;
+  }
+  __syncthreads();
+  // ---- cell means
   for (int q = tid; q < ncell * CPB; q += blockDim.x) {
     const int cell = q / CPB, k = q - cell * CPB;
     const int t = cell_level(cell, cell_off, cnt);
@@ -117,8 +177,7 @@ hcl_kernel(const HclTable table, int L, float* __restrict__ partial, float weigh
     const int y0 = bin_start(iy, H, l), y1 = bin_end(iy, H, l);
     const int x0 = bin_start(ix, W, l), x1 = bin_end(ix, W, l);
     float s = 0.f;
-    for (int yy = y0; yy < y1; ++yy)
-      for (int xx = x0; xx < x1; ++xx) s += sd[(yy * W + xx) * CPB + k];
+    for (int yy = y0; yy < y1; ++yy) s += R[(yy * HCL_BINS + bin0[t] + ix) * CPB + k];
     cells[cell * CPB + k] = s / (float)((y1 - y0) * (x1 - x0));  // mean difference
   }
   __syncthreads();
@@ -137,10 +196,13 @@ hcl_kernel(const HclTable table, int L, float* __restrict__ partial, float weigh
   if (tid == 0) partial[blockIdx.x] = (sqsum / numel + cellsum) / tot;
   // ---- gradient of the weighted, warmed-up loss w.r.t. fs
   const float inv_tot = f / tot;
-  for (int q = tid; q < HW * CPB; q += blockDim.x) {
-    const int p = q / CPB, k = q - p * CPB;
+  for (int q = tid; q < nv; q += blockDim.x) {
+    const int e0 = q * VW;
+    const int p = e0 / CPB, k0 = e0 - p * CPB;
     const int yy = p / W, xx = p - yy * W;
-    float g = 2.f * sd[q] / numel;
+    float g[VW];
+#pragma unroll
+    for (int v = 0; v < VW; ++v) g[v] = 2.f * sd[e0 + v] / numel;
     for (int t = 0; t < 3; ++t) {
       if (cnt[t] == 0.f) continue;
       const int l = levels[t];
@@ -154,12 +216,35 @@ hcl_kernel(const HclTable table, int L, float* __restrict__ partial, float weigh
         for (int ix = ix_lo; ix < l && bin_start(ix, W, l) <= xx; ++ix) {
           if (xx >= bin_end(ix, W, l)) continue;
           const int aw = bin_end(ix, W, l) - bin_start(ix, W, l);
-          g += scale * cells[(cell_off[t] + iy * l + ix) * CPB + k] / (float)(ah * aw);
+          const float* cp = cells + (cell_off[t] + iy * l + ix) * CPB + k0;
+          const float sc = scale / (float)(ah * aw);
+#pragma unroll
+          for (int v = 0; v < VW; ++v) g[v] += sc * cp[v];
         }
       }
     }
-    grad[base + (int64_t)p * C + k] = f2bf(g * inv_tot);
+#pragma unroll
+    for (int v = 0; v < VW; ++v) g[v] *= inv_tot;
+    st_bf16<VW>(grad + base + (int64_t)p * C + k0, g);
   }
+}
+
+__global__ void __launch_bounds__(256)
+hcl_kernel(const HclTable table, int L, float* __restrict__ partial, float weight,
+           const float* __restrict__ epoch, float warmup) {
+  extern __shared__ float sd[];  // [HW][CPB] differences, then [H][HCL_BINS][CPB] row-bin sums
+  __shared__ float scratch[4];
+  __shared__ float cells[21 * HCL_MAX_CPB];  // 4x4 + 2x2 + 1x1 cells
+  const int64_t* tb = table.v;
+  int lv = 0;
+  while (lv + 1 < L && (int64_t)blockIdx.x >= tb[(lv + 1) * HCL_FIELDS + 8]) ++lv;
+  const int64_t* e = tb + lv * HCL_FIELDS;
+  const int local = blockIdx.x - (int)e[8];
+  const int CPB = (int)e[7];
+  if (CPB >= 8) hcl_block<8>(e, local, partial, weight, epoch, warmup, sd, scratch, cells);
+  else if (CPB == 4) hcl_block<4>(e, local, partial, weight, epoch, warmup, sd, scratch, cells);
+  else if (CPB == 2) hcl_block<2>(e, local, partial, weight, epoch, warmup, sd, scratch, cells);
+  else hcl_block<1>(e, local, partial, weight, epoch, warmup, sd, scratch, cells);
 }
 
 __global__ void __launch_bounds__(256)
@@ -405,13 +490,15 @@ abf_wgrad_finalize_kernel(const float* __restrict__ partial, int nblk, int C,
 MDA_API int mda_hcl_loss(const int64_t* table, int64_t L, int64_t nblk, int64_t lds_floats,
                          float* partial, float weight, const float* epoch, float warmup,
                          float* loss, hipStream_t st) {
-  if (L < 1 || L > HCL_MAX_LEVELS || nblk < 1 || lds_floats * 4 > 160 * 1024)
+  if (L < 1 || L > HCL_MAX_LEVELS || nblk < 1 || lds_floats * 4 > 150 * 1024)
     return (int)hipErrorInvalidValue;
   HclTable tb{};
   for (int64_t i = 0; i < L * HCL_FIELDS; ++i) tb.v[i] = table[i];
   for (int64_t l = 0; l < L; ++l) {  // shape sanity before touching device memory
     const int64_t* e = tb.v + l * HCL_FIELDS;
-    if (e[7] < 1 || e[7] > 8 || e[6] % e[7] || e[4] * e[5] * e[7] > lds_floats ||
+    const int64_t cpb = e[7];
+    if (cpb < 1 || cpb > HCL_MAX_CPB || (cpb & (cpb - 1)) || e[6] % cpb ||
+        (e[4] * e[5] + e[4] * HCL_BINS) * cpb > lds_floats ||
         e[9] != e[3] * (e[6] / e[7]))
       return (int)hipErrorInvalidValue;
   }

@@ -260,8 +260,10 @@ def hcl_loss(fstudent, fteacher):
 # fused HIP path of HCL (csrc/reviewkd.hip::mda_hcl_loss)
 
 def _hcl_cpb(C, HW):
-    for cpb in (8, 4, 2, 1):
-        if C % cpb == 0 and HW * cpb <= 16384:
+    # channels per block: ~8 K staged floats (~30 KB of LDS -> several blocks
+    # per CU); power of two <= 32 (csrc/reviewkd.hip HCL_MAX_CPB)
+    for cpb in (32, 16, 8, 4, 2, 1):
+        if C % cpb == 0 and HW * cpb <= 8192:
             return cpb
     return 0
 
@@ -298,7 +300,7 @@ class _HCL(torch.autograd.Function):
             nb = N * (C // cpb)
             rows.append([a.data_ptr(), b.data_ptr(), g.data_ptr(), N, H, W, C, cpb, nblk, nb])
             nblk += nb
-            lds = max(lds, H * W * cpb)
+            lds = max(lds, (H * W + H * 7) * cpb)  # staged d + row-bin sums
         table = np.asarray(rows, dtype=np.int64)
         dev = fs[0].device
         partial = torch.empty(nblk, dtype=torch.float32, device=dev)

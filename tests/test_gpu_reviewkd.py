@@ -21,6 +21,7 @@ def _bf(t):
     [(16, 64, 32), (16, 128, 16), (16, 256, 8), (16, 256, 1)],   # CIFAR ReviewKD levels
     [(4, 64, 56), (4, 128, 28), (4, 256, 14), (4, 512, 7), (4, 512, 1)],  # ImageNet (7x7: overlapping bins)
     [(3, 24, 5), (3, 12, 3), (3, 8, 2)],
+    [(2, 3, 64), (2, 6, 48), (2, 96, 9)],  # 1 / 2 / 32 channels per block
 ])
 @pytest.mark.parametrize("epoch,warmup", [(None, 0.0), (0.5, 1.0)])
 def test_hcl_fused(shapes, epoch, warmup):

@@ -46,7 +46,9 @@ def main(argv=None):
 
     import torch
     from mdistiller_ddp_amd.detection.data import build_detection_data
-    from mdistiller_ddp_amd.detection.engine import DetectionTrainer, coco_evaluate, dump_json, run_inference
+    from mdistiller_ddp_amd.detection.engine import DetectionTrainer, dump_json
+    from mdistiller_ddp_amd.detection.evaluation import build_evaluator, inference_on_dataset
+    from mdistiller_ddp_amd.detection.tta import GeneralizedRCNNWithTTA
     from mdistiller_ddp_amd.detection.rcnn import build_model
     from mdistiller_ddp_amd.ops.backend import set_backend
     from mdistiller_ddp_amd.parallel.dist import barrier, get_rank, get_world_size, init_distributed, is_master
@@ -101,13 +103,19 @@ def main(argv=None):
     if not args.eval_only:
         trainer.train(start_iter=start, ckpt_dir=out_dir)
     val_ds, _ = build_detection_data(cfg, train=False, device=device if cfg.RUNTIME.SYNTHETIC else "cpu")
-    n = len(val_ds)
-    preds, gts = run_inference(model, val_ds, n, device, trainer.autocast)
+    evaluator = build_evaluator(cfg.RUNTIME.EVALUATOR_TYPE, int(cfg.MODEL.ROI_HEADS.NUM_CLASSES),
+                                mask_on=bool(cfg.MODEL.MASK_ON))
+    res = inference_on_dataset(model, val_ds, evaluator, autocast=trainer.autocast)
+    if cfg.TEST.AUG.ENABLED:  # reference train_net.py:106-117 (test_with_TTA)
+        tta = build_evaluator(cfg.RUNTIME.EVALUATOR_TYPE, int(cfg.MODEL.ROI_HEADS.NUM_CLASSES))
+        res_tta = inference_on_dataset(GeneralizedRCNNWithTTA(cfg, model), val_ds, tta,
+                                       autocast=trainer.autocast)
+        res.update({k + "_TTA": v for k, v in res_tta.items()})
     if is_master():
-        res = coco_evaluate(preds, gts, int(cfg.MODEL.ROI_HEADS.NUM_CLASSES))
-        print("bbox:", json.dumps(res))
+        for k, v in res.items():
+            print(f"{k}:", json.dumps(v))
         os.makedirs(out_dir, exist_ok=True)
-        dump_json({"bbox": res}, os.path.join(out_dir, "metrics.json"))
+        dump_json(res, os.path.join(out_dir, "metrics.json"))
     return 0
 
 

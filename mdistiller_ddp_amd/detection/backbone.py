@@ -172,6 +172,53 @@ class BottleneckBlock(_Block):
         return self.conv3(self.conv2(self.conv1(x)), residual=sc)
 
 
+class DeformBottleneckBlock(_Block):
+    """Bottleneck with a deformable 3x3 (reference ``backbone/resnet.py:223-336``):
+    a plain 3x3 conv predicts per-tap offsets (and, modulated, a sigmoid mask)
+    from the 1x1 output; it starts at zero so the block begins as a regular
+    bottleneck."""
+
+    def __init__(self, in_channels, out_channels, *, bottleneck_channels, stride=1, num_groups=1,
+                 norm="BN", stride_in_1x1=False, dilation=1, deform_modulated=False,
+                 deform_num_groups=1):
+        super().__init__()
+        from .deform import DeformConv, ModulatedDeformConv
+        self.in_channels, self.out_channels, self.stride = in_channels, out_channels, stride
+        self.deform_modulated = deform_modulated
+        self.shortcut = (Conv2d(in_channels, out_channels, 1, stride=stride, bias=False,
+                                norm=get_norm(norm, out_channels))
+                         if in_channels != out_channels else None)
+        s1, s3 = (stride, 1) if stride_in_1x1 else (1, stride)
+        self.conv1 = Conv2d(in_channels, bottleneck_channels, 1, stride=s1, bias=False,
+                            norm=get_norm(norm, bottleneck_channels), activation="relu")
+        per_group = 27 if deform_modulated else 18  # (2 offsets [+ 1 mask]) x 3 x 3 taps
+        self.conv2_offset = Conv2d(bottleneck_channels, per_group * deform_num_groups, 3, stride=s3,
+                                   padding=dilation, dilation=dilation)
+        op = ModulatedDeformConv if deform_modulated else DeformConv
+        self.conv2 = op(bottleneck_channels, bottleneck_channels, 3, stride=s3, padding=dilation,
+                        bias=False, groups=num_groups, dilation=dilation,
+                        deformable_groups=deform_num_groups, norm=get_norm(norm, bottleneck_channels))
+        self.conv3 = Conv2d(bottleneck_channels, out_channels, 1, bias=False,
+                            norm=get_norm(norm, out_channels), activation="relu")
+        for layer in (self.conv1, self.conv2, self.conv3, self.shortcut):
+            if layer is not None:
+                c2_msra_fill(layer)
+        nn.init.constant_(self.conv2_offset.weight, 0)
+        nn.init.constant_(self.conv2_offset.bias, 0)
+
+    def forward(self, x):
+        out = self.conv1(x)
+        if self.deform_modulated:
+            om = self.conv2_offset(out)
+            n = om.shape[1] // 3
+            out = self.conv2(out, om[:, : 2 * n], om[:, 2 * n:].sigmoid())
+        else:
+            out = self.conv2(out, self.conv2_offset(out))
+        out = F.relu(out)
+        sc = self.shortcut(x) if self.shortcut is not None else x
+        return self.conv3(out, residual=sc)
+
+
 class ResNet(nn.Module):
     def __init__(self, stem, stages, out_features):
         super().__init__()
@@ -218,8 +265,6 @@ def build_resnet_backbone(mcfg, in_channels: int = 3) -> ResNet:
     freeze_at = mcfg.BACKBONE.FREEZE_AT
     if freeze_at >= 1:
         stem.freeze()
-    if any(r.DEFORM_ON_PER_STAGE):
-        raise NotImplementedError("deformable-conv ResNet stages are not built (no reference config uses them)")
     depth = r.DEPTH
     out_features = list(r.OUT_FEATURES)
     bott = r.NUM_GROUPS * r.WIDTH_PER_GROUP
@@ -234,10 +279,17 @@ def build_resnet_backbone(mcfg, in_channels: int = 3) -> ResNet:
         dil = r.RES5_DILATION if stage_idx == 5 else 1
         first_stride = 1 if idx == 0 or (stage_idx == 5 and dil == 2) else 2
         blocks = []
+        deform = bool(r.DEFORM_ON_PER_STAGE[idx])
+        if deform and depth < 50:
+            raise ValueError("deformable stages need bottleneck blocks (ResNet-50 and deeper)")
         for i in range(_BLOCKS_PER_DEPTH[depth][idx]):
-            blocks.append(cls(in_ch, out_ch, bottleneck_channels=bott,
-                              stride=first_stride if i == 0 else 1, num_groups=r.NUM_GROUPS,
-                              norm=norm, stride_in_1x1=r.STRIDE_IN_1X1, dilation=dil))
+            kw = dict(bottleneck_channels=bott, stride=first_stride if i == 0 else 1,
+                      num_groups=r.NUM_GROUPS, norm=norm, stride_in_1x1=r.STRIDE_IN_1X1, dilation=dil)
+            if deform:
+                blocks.append(DeformBottleneckBlock(in_ch, out_ch, deform_modulated=r.DEFORM_MODULATED,
+                                                    deform_num_groups=r.DEFORM_NUM_GROUPS, **kw))
+            else:
+                blocks.append(cls(in_ch, out_ch, **kw))
             in_ch = out_ch
         out_ch *= 2
         bott *= 2

@@ -171,6 +171,10 @@ def get_det_cfg() -> CN:
         "COCO_JSON": "",            # COCO-format instances json (+ COCO_IMAGE_ROOT) instead
         "COCO_IMAGE_ROOT": "",
         "RANDOM_INIT_DAMP": 0.25,   # residual-branch damping when no MODEL.WEIGHTS is loaded
+        # evaluator_type of the test set (the reference reads it from the
+        # dataset metadata): coco | lvis | pascal_voc | cityscapes_instance |
+        # cityscapes_sem_seg | sem_seg | coco_panoptic_seg
+        "EVALUATOR_TYPE": "coco",
     })
     add_distillation_cfg(C)
     return C

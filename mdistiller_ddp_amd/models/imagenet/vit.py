@@ -5,8 +5,10 @@ timm is not available here (and the reference file fails to import),
 so this is a self-contained implementation with timm's parameter names
 (``patch_embed.proj``, ``cls_token``, ``pos_embed``, ``blocks.N.{norm1,attn.qkv,
 attn.proj,norm2,mlp.fc1,mlp.fc2}``, ``norm``, ``head``) so timm checkpoints
-load with ``strict=True``.  Attention runs on PyTorch's fused SDPA; at 197
-tokens there is nothing to shard.
+load with ``strict=True``.  Attention is the in-tree MFMA flash-attention
+kernel on the HIP path (``ops/attention.py``, head_dim 64: tiny / small /
+base / large) and PyTorch SDPA elsewhere; at 197 tokens there is nothing to
+shard.
 """
 from __future__ import annotations
 
@@ -17,6 +19,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ...ops.attention import attention
 from .._base import ModelBase
 
 
@@ -40,11 +43,8 @@ class Attention(nn.Module):
         self.proj = nn.Linear(dim, dim)
 
     def forward(self, x):
-        B, N, C = x.shape
-        qkv = self.qkv(x).reshape(B, N, 3, self.num_heads, self.head_dim).permute(2, 0, 3, 1, 4)
-        q, k, v = qkv.unbind(0)
-        x = F.scaled_dot_product_attention(q, k, v)
-        return self.proj(x.transpose(1, 2).reshape(B, N, C))
+        # fused MFMA flash attention on the HIP path (ops/attention.py), SDPA elsewhere
+        return self.proj(attention(self.qkv(x), self.num_heads))
 
 
 class Mlp(nn.Module):

@@ -74,6 +74,8 @@ SIGNATURES = {
     "mda_meters_update": "ippii" + "pppp" + "ips",
     # ReviewKD HCL + ABF (csrc/reviewkd.hip)
     "mda_hcl_loss": "piiipfpfps",
+    "mda_attn_fwd": "pppiiifs",
+    "mda_attn_bwd": "ppppppiiifs",
     "mda_abf_fwd": "pppppp" + "iiiiii" + "s",
     "mda_abf_bwd_blocks": "iiiip",
     "mda_abf_bwd": "ppppppppppp" + "iiiiii" + "ii" + "s",

@@ -1556,7 +1556,11 @@ MDA_API int mda_conv_set_stamps(void* buf) {
 // Host-side tile / split-K choice (also used by Python to size the workspace).
 // Returns tile code BM*1000+BN in *tile and the split count in *splits.
 MDA_API int mda_conv_plan(int64_t M, int64_t Cout, int64_t Kp, int64_t* tile, int64_t* splits) {
-  const int64_t target = 512;  // >= 2 workgroups per CU on 256 CUs
+  // >= 1 workgroup per CU on 256 CUs before splitting K (MDA_CONV_TARGET overrides)
+  static const int64_t target = [] {
+    const char* e = getenv("MDA_CONV_TARGET");
+    return e ? (int64_t)atoi(e) : (int64_t)256;  // A/B: profiles/r2_conv_target_ab.md
+  }();
   int bn = Cout <= 32 ? 32 : (Cout <= 64 ? 64 : 128);
   int bm = 128;
   auto blocks = [&](int bm_, int bn_) { return ((M + bm_ - 1) / bm_) * ((Cout + bn_ - 1) / bn_); };

@@ -394,8 +394,15 @@ MDA_API int mda_dw_wgrad_blocks(int64_t N, int64_t Ho, int64_t Wo, int64_t C, in
   const int64_t CG = C / V;
   const int64_t PL = CG >= 256 ? 1 : 256 / CG;
   const int64_t items = N * Ho * ((Wo + OWT - 1) / OWT);
-  int64_t b = (items + PL * 4 - 1) / (PL * 4);  // ~4 items (16 pixels) per lane
-  if (b > 512) b = 512;
+  // ~ITEMS_PER_LANE work items (4 pixels each) per lane: enough blocks that the
+  // lanes' independent load batches hide the memory latency (the finalize
+  // reads the nblk partials in parallel)
+  static const int64_t ipl = [] {
+    const char* e = getenv("MDA_DW_WG_IPL");
+    return e ? (int64_t)atoi(e) : (int64_t)2;
+  }();
+  int64_t b = (items + PL * ipl - 1) / (PL * ipl);
+  if (b > 1024) b = 1024;
   if (b < 1) b = 1;
   *nblk = b;
   return 0;

@@ -21,6 +21,7 @@ gradients against them.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 import torch.nn as nn
@@ -52,6 +53,21 @@ def _ws(device):
     if w is None:
         w = _WSS[key] = _WS(device)
     return w
+
+
+_BN_INKERNEL = os.environ.get("MDA_BN_INKERNEL", "0") == "1"
+
+
+def _bn_bwd_reduce(dout, dpre, y, res, stats, M, C, act, ws, sums, dg, db):
+    """dbeta / dgamma sums of the BN backward: per-block partials combined by a
+    separate channel-parallel finalize launch (default), or in-kernel by the
+    last-arriving blocks (``MDA_BN_INKERNEL=1``, A/B)."""
+    if _BN_INKERNEL:
+        _ext.call("mda_bn_bwd_reduce", dout, dpre, y, res, stats[2], stats[3], stats[0], stats[1],
+                  M, C, act, ws.partial, ws.counter, sums, dg, db)
+    else:
+        _ext.call("mda_bn_bwd_reduce2", dout, dpre, y, res, stats[2], stats[3], stats[0], stats[1],
+                  M, C, act, ws.partial, sums, dg, db)
 
 
 _WG_PLANS: dict = {}
@@ -318,8 +334,7 @@ class _ConvBNActTrain(torch.autograd.Function):
         direct_gb = gamma.grad is not None and beta.grad is not None
         dg = gamma.grad if direct_gb else None
         db = beta.grad if direct_gb else None
-        _ext.call("mda_bn_bwd_reduce2", dout, dpre, y, res, stats[2], stats[3], stats[0], stats[1],
-                  M, Cout, act, ws.partial, sums, dg, db)
+        _bn_bwd_reduce(dout, dpre, y, res, stats, M, Cout, act, ws, sums, dg, db)
         need_res = ctx.has_res and ctx.needs_input_grad[4]
         dy = torch.empty_like(y)
         dres = torch.empty_like(y) if need_res else None
@@ -377,8 +392,7 @@ def _bn_train_backward(ctx, dout, dpre, y, res, stats, gamma, beta, M, C, act):
     direct_gb = gamma.grad is not None and beta.grad is not None
     dg = gamma.grad if direct_gb else None
     db = beta.grad if direct_gb else None
-    _ext.call("mda_bn_bwd_reduce2", dout, dpre, y, res, stats[2], stats[3], stats[0], stats[1],
-              M, C, act, ws.partial, sums, dg, db)
+    _bn_bwd_reduce(dout, dpre, y, res, stats, M, C, act, ws, sums, dg, db)
     dy = torch.empty_like(y)
     dres = torch.empty_like(y) if res is not None else None
     _ext.call("mda_bn_bwd_apply", dout, dpre, y, res, stats[2], stats[3], stats[0], stats[1],

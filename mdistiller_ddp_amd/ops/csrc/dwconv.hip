@@ -397,10 +397,12 @@ MDA_API int mda_dw_wgrad_blocks(int64_t N, int64_t Ho, int64_t Wo, int64_t C, in
   // ~ITEMS_PER_LANE work items (4 pixels each) per lane: enough blocks that the
   // lanes' independent load batches hide the memory latency (the finalize
   // reads the nblk partials in parallel)
-  static const int64_t ipl = [] {
+  // (A/B, profiles/r2_misc_ab.md: 1 for CIFAR-size maps, 2 for 112^2 ImageNet ones)
+  static const int64_t forced = [] {
     const char* e = getenv("MDA_DW_WG_IPL");
-    return e ? (int64_t)atoi(e) : (int64_t)2;
+    return e ? (int64_t)atoi(e) : (int64_t)0;
   }();
+  const int64_t ipl = forced > 0 ? forced : (N * Ho * ((Wo + OWT - 1) / OWT) < 200000 ? 1 : 2);
   int64_t b = (items + PL * ipl - 1) / (PL * ipl);
   if (b > 1024) b = 1024;
   if (b < 1) b = 1;

@@ -55,19 +55,12 @@ def _ws(device):
     return w
 
 
-_BN_INKERNEL = os.environ.get("MDA_BN_INKERNEL", "0") == "1"
-
-
 def _bn_bwd_reduce(dout, dpre, y, res, stats, M, C, act, ws, sums, dg, db):
     """dbeta / dgamma sums of the BN backward: per-block partials combined by a
-    separate channel-parallel finalize launch (default), or in-kernel by the
-    last-arriving blocks (``MDA_BN_INKERNEL=1``, A/B)."""
-    if _BN_INKERNEL:
-        _ext.call("mda_bn_bwd_reduce", dout, dpre, y, res, stats[2], stats[3], stats[0], stats[1],
-                  M, C, act, ws.partial, ws.counter, sums, dg, db)
-    else:
-        _ext.call("mda_bn_bwd_reduce2", dout, dpre, y, res, stats[2], stats[3], stats[0], stats[1],
-                  M, C, act, ws.partial, sums, dg, db)
+    separate channel-parallel finalize launch (the in-kernel last-arriver
+    combine, ``mda_bn_bwd_reduce``, measured slower: profiles/r2_misc_ab.md)."""
+    _ext.call("mda_bn_bwd_reduce2", dout, dpre, y, res, stats[2], stats[3], stats[0], stats[1],
+              M, C, act, ws.partial, sums, dg, db)
 
 
 _WG_PLANS: dict = {}

@@ -1336,6 +1336,22 @@ conv_halo2_kernel(const ConvParams p) {
   }
   const int bswz = (frow >> 1) & 7;
 
+  // A fragments (patch rows) of tap t+1 are read during tap t: the patch is
+  // resident from tap 0 on, only the weight tile of a tap needs its own wait
+  bf16x8 af[2][2][MI];  // [buffer][kk][i]
+  auto load_a = [&](int tap, int buf) {
+    const int kh = tap / 3, kw = tap - (tap / 3) * 3;
+    const int toff = kh * PW + kw;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int q = kk * 4 + g4;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int pr = a_prow[i] + toff;
+        af[buf][kk][i] = *(const bf16x8*)(smem + pr * 128 + ((q ^ ((pr >> 1) & 7)) * 16));
+      }
+    }
+  };
 #pragma unroll
   for (int tap = 0; tap < 9; ++tap) {
     // the patch and weight taps 0..tap have landed: 8 - tap younger DMAs
@@ -1350,29 +1366,28 @@ conv_halo2_kernel(const ConvParams p) {
       case 7: vm_wait_barrier<1>(); break;
       default: vm_wait_barrier<0>(); break;
     }
-    if (tap == 0) stamp(p, 2);
-    const char* Ps = smem;
+    if (tap == 0) {
+      stamp(p, 2);
+      load_a(0, 0);
+    }
     const char* Bs = smem + PATCH + tap * BT;
-    const int kh = tap / 3, kw = tap - (tap / 3) * 3;
-    const int toff = kh * PW + kw;
+    bf16x8 bfr[2][NI];
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int q = kk * 4 + g4;
-      bf16x8 af[MI], bfr[NI];
-#pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        const int pr = a_prow[i] + toff;
-        af[i] = *(const bf16x8*)(Ps + pr * 128 + ((q ^ ((pr >> 1) & 7)) * 16));
-      }
 #pragma unroll
       for (int j = 0; j < NI; ++j)
-        bfr[j] = *(const bf16x8*)(Bs + (wn * (BN / 2) + j * 16 + frow) * 128 + ((q ^ bswz) * 16));
+        bfr[kk][j] = *(const bf16x8*)(Bs + (wn * (BN / 2) + j * 16 + frow) * 128 + ((q ^ bswz) * 16));
+    }
+    if (tap + 1 < 9) load_a(tap + 1, (tap + 1) & 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NI; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[tap & 1][kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
   }
   __syncthreads();  // every LDS read of the patch / weights done: the C tile aliases them
   stamp(p, 3);

@@ -1476,6 +1476,14 @@ bool use_halo2() {
   return on;
 }
 
+bool halo_narrow() {
+  static const bool on = [] {
+    const char* e = getenv("MDA_HALO_NARROW");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 bool use_halo1() {
   static const bool on = [] {
     const char* e = getenv("MDA_CONV_HALO1");
@@ -1628,7 +1636,12 @@ int dispatch(ConvParams& p, int mode, int64_t tile, int64_t splits, hipStream_t 
   if (halo) {  // halo kernel: split over 64-channel chunks, hpb pixels per block
     const int nchunks = p.Cin / BK;
     p.steps_per_split = (int)((nchunks + splits - 1) / splits);
-    const int bn = p.Cout <= 32 ? 32 : 64;
+    int bn = p.Cout <= 32 ? 32 : 64;
+    // fewer blocks than CUs (8x8 maps: 128-pixel blocks of two images): halve
+    // the channel tile rather than leave half the CUs idle
+    if (bn == 64 && (int64_t)((p.M + p.hpb - 1) / p.hpb) * ((p.Cout + 63) / 64) * splits < 256 &&
+        halo_narrow())
+      bn = 32;
     dim3 grid((p.M + p.hpb - 1) / p.hpb, (p.Cout + bn - 1) / bn, (int)splits);
     if (nchunks == 1 && splits == 1 && use_halo1()) {
       if (bn == 32) {

@@ -26,7 +26,43 @@ def _norm_cdf(x: float) -> float:
     return 0.5 * (1.0 + math.erf(x / math.sqrt(2.0)))
 
 
+class _OFDLossHIP(torch.autograd.Function):
+    """One fused pass (csrc/feat.hip ``mda_ofd_loss``): the partial-L2 value and
+    d/d source, bf16 NHWC in, the ~15 fp32 elementwise launches (and their
+    backward) of the PyTorch expression out."""
+
+    @staticmethod
+    def forward(ctx, source, target, margin, scale):
+        from ..ops import _ext
+        from ..ops.losses import workspace
+        N, C, H, W = source.shape
+        s = source.contiguous(memory_format=torch.channels_last)
+        t = target.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        m = margin.reshape(-1).float().contiguous()
+        grad = torch.empty_like(s)
+        loss = torch.empty(1, dtype=torch.float32, device=s.device)
+        ws = workspace(s.device)
+        _ext.call("mda_ofd_loss", s, t, m, grad, loss, ws.partial, ws.counter, N * H * W, C, float(scale))
+        ctx.save_for_backward(grad)
+        return loss.reshape(())
+
+    @staticmethod
+    def backward(ctx, go):
+        (grad,) = ctx.saved_tensors
+        return grad * go.to(grad.dtype), None, None, None
+
+
+def _ofd_native_ok(source, target):
+    from ..ops.backend import hip_enabled_for
+    return (hip_enabled_for(source) and source.dtype == torch.bfloat16 and source.dim() == 4
+            and source.shape == target.shape and source.shape[1] % 8 == 0
+            and source.is_contiguous(memory_format=torch.channels_last))
+
+
 def feat_loss(source, target, margin):
+    """`distillers/OFD.py:11-21`: sum over (C, H, W) of the batch mean."""
+    if _ofd_native_ok(source, target):
+        return _OFDLossHIP.apply(source, target, margin, 1.0 / source.shape[0])
     source = source.float()
     target = target.float()
     margin = margin.to(source)
@@ -112,7 +148,9 @@ class OFD(Distiller):
         margins = self.margins
         loss = 0.0
         for i in range(n):
-            t = F.adaptive_avg_pool2d(feature_teacher[i].float(), feature_student[i].shape[-2:]).detach()
+            t = feature_teacher[i].detach()
+            if t.shape[-2:] != feature_student[i].shape[-2:]:
+                t = F.adaptive_avg_pool2d(t.float(), feature_student[i].shape[-2:])
             loss = loss + feat_loss(feature_student[i], t, margins[i]) / 2 ** (n - i - 1)
         return loss
 

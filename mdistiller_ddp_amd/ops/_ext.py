@@ -75,6 +75,8 @@ SIGNATURES = {
     # ReviewKD HCL + ABF (csrc/reviewkd.hip)
     "mda_hcl_loss": "piiipfpfps",
     "mda_attn_fwd": "pppiiifs",
+    "mda_channel_shuffle": "ppiiis",
+    "mda_ofd_loss": "ppppppp" + "ii" + "fs",
     "mda_attn_bwd": "ppppppiiifs",
     "mda_abf_fwd": "pppppp" + "iiiiii" + "s",
     "mda_abf_bwd_blocks": "iiiip",

@@ -426,45 +426,46 @@ conv_wgrad_glds_kernel(const WgParams p) {
 }
 
 // grad[co][ci][kh][kw] (+)= scale * sum_s partial[s][co][(kh*KW+kw)*Cin+ci]
-// Block = 4 waves x 64 lanes; a lane owns 4 consecutive packed (co, k)
-// elements (one float4 per partial set), wave w sums the sets s = w (mod 4)
-// with four loads in flight, and wave 0 combines the four in a fixed order
-// (deterministic).  The element-per-thread version walked all the sets
-// serially per thread (~9 us for a 64-set ResNet layer).
+// Block = 16 float4 columns (64 packed (co, k) elements) x 16 set-slices:
+// thread (c, sl) sums the partial sets s = sl (mod 16), two loads in flight,
+// and the 16 slice sums combine in a fixed order (deterministic).  With up to
+// 128 sets per layer the earlier 4-slice version walked ~30 dependent loads
+// per thread (14 us per ResNet-18 layer); this one issues ~8.
+constexpr int WGR_COLS = 16, WGR_SLICES = 16;
+
 __global__ void __launch_bounds__(256)
 wgrad_reduce_kernel(const float* __restrict__ partial, float* __restrict__ grad, int splits,
                     int Cout, int Cin, int KH, int KW, int Kp, float scale, int accumulate,
                     int cin_keep) {
-  __shared__ float4 red[4][64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __shared__ float4 red[WGR_SLICES][WGR_COLS];
+  const int c = threadIdx.x % WGR_COLS, sl = threadIdx.x / WGR_COLS;
   const int64_t total4 = (int64_t)Cout * Kp / 4;
-  const int64_t e4 = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t e4 = (int64_t)blockIdx.x * WGR_COLS + c;
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
   if (e4 < total4) {
     const float4* src = (const float4*)partial + e4;
-    float4 b = a, c = a, d = a;
-    int s = w;
-    for (; s + 12 < splits; s += 16) {
-      const float4 u0 = src[(int64_t)s * total4], u1 = src[(int64_t)(s + 4) * total4];
-      const float4 u2 = src[(int64_t)(s + 8) * total4], u3 = src[(int64_t)(s + 12) * total4];
+    float4 b = a;
+    int s = sl;
+    for (; s + WGR_SLICES < splits; s += 2 * WGR_SLICES) {
+      const float4 u0 = src[(int64_t)s * total4], u1 = src[(int64_t)(s + WGR_SLICES) * total4];
       a.x += u0.x; a.y += u0.y; a.z += u0.z; a.w += u0.w;
       b.x += u1.x; b.y += u1.y; b.z += u1.z; b.w += u1.w;
-      c.x += u2.x; c.y += u2.y; c.z += u2.z; c.w += u2.w;
-      d.x += u3.x; d.y += u3.y; d.z += u3.z; d.w += u3.w;
     }
-    for (; s < splits; s += 4) {
+    if (s < splits) {
       const float4 u = src[(int64_t)s * total4];
       a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
     }
-    a.x += b.x + (c.x + d.x); a.y += b.y + (c.y + d.y);
-    a.z += b.z + (c.z + d.z); a.w += b.w + (c.w + d.w);
+    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
   }
-  red[w][lane] = a;
+  red[sl][c] = a;
   __syncthreads();
-  if (w != 0 || e4 >= total4) return;
-  const float4 r0 = red[0][lane], r1 = red[1][lane], r2 = red[2][lane], r3 = red[3][lane];
-  const float v[4] = {(r0.x + r1.x) + (r2.x + r3.x), (r0.y + r1.y) + (r2.y + r3.y),
-                      (r0.z + r1.z) + (r2.z + r3.z), (r0.w + r1.w) + (r2.w + r3.w)};
+  if (sl != 0 || e4 >= total4) return;
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < WGR_SLICES; ++q) {
+    const float4 r = red[q][c];
+    v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
+  }
   const int K = Cin * KH * KW;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -738,7 +739,7 @@ MDA_API int mda_conv_wgrad(const void* x, const void* dy, float* partial, float*
   int rc = (int)hipGetLastError();
   if (rc) return rc;
   const int64_t total4 = Cout * Kp / 4;  // Kp % 64 == 0
-  const int blocks = (int)((total4 + 63) / 64);
+  const int blocks = (int)((total4 + WGR_COLS - 1) / WGR_COLS);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, partial, grad,
                      (int)splits, (int)Cout, (int)Cin, (int)KH, (int)KW, (int)Kp, scale,
                      (int)accumulate, (int)cin_keep);

@@ -90,7 +90,72 @@ at_loss_kernel(const TS* __restrict__ fs, const TT* __restrict__ ft, TS* __restr
   }
 }
 
+// OFD partial L2 (reference distillers/OFD.py:11-21) with its gradient in one
+// pass.  s (student connector output) and t (teacher pre-ReLU feature) are
+// [M, C] bf16 (NHWC, M = N*H*W), m the per-channel margin:
+//   l = (s-m)^2 [s>m & t<=m] + (s-t)^2 [s>t & m<t<=0] + (s-t)^2 [t>0]
+// loss = scale * sum l (scale = weight / N: the reference's mean over the
+// batch then sum), grad = scale * dl/ds.  8 channels per thread-iteration,
+// per-block partials summed in block order by the last-arriving block.
+__global__ void __launch_bounds__(256)
+ofd_loss_kernel(const bf16_t* __restrict__ s, const bf16_t* __restrict__ t,
+                const float* __restrict__ margin, bf16_t* __restrict__ grad, float* __restrict__ partial,
+                unsigned* __restrict__ counter, float* __restrict__ loss, int64_t M, int C, float scale) {
+  __shared__ float red[4];
+  const int64_t total8 = M * C / 8;
+  const int C8 = C / 8;
+  float acc = 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total8;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % C8) * 8;
+    const uint4 us = *(const uint4*)(s + i * 8);
+    const uint4 ut = *(const uint4*)(t + i * 8);
+    const uint32_t ws[4] = {us.x, us.y, us.z, us.w}, wt[4] = {ut.x, ut.y, ut.z, ut.w};
+    float g[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float sv = __uint_as_float((e & 1) ? (ws[e >> 1] & 0xffff0000u) : (ws[e >> 1] << 16));
+      const float tv = __uint_as_float((e & 1) ? (wt[e >> 1] & 0xffff0000u) : (wt[e >> 1] << 16));
+      const float mv = margin[c0 + e];
+      float l = 0.f, d = 0.f;
+      if (sv > mv && tv <= mv) { const float q = sv - mv; l += q * q; d += 2.f * q; }
+      if (sv > tv && tv > mv && tv <= 0.f) { const float q = sv - tv; l += q * q; d += 2.f * q; }
+      if (tv > 0.f) { const float q = sv - tv; l += q * q; d += 2.f * q; }
+      acc += l;
+      g[e] = scale * d;
+    }
+    *(uint4*)(grad + i * 8) = make_uint4(pack_bf16x2(g[0], g[1]), pack_bf16x2(g[2], g[3]),
+                                         pack_bf16x2(g[4], g[5]), pack_bf16x2(g[6], g[7]));
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+  if (mda_arrive(counter, gridDim.x)) {
+    if (threadIdx.x < 64) {
+      float v = 0.f;
+      for (int i = threadIdx.x; i < (int)gridDim.x; i += 64) v += partial[i];
+      v = wave_sum(v);
+      if (threadIdx.x == 0) loss[0] = v * scale;
+    }
+  }
+}
+
 }  // namespace
+
+// s, t: [M, C] bf16 NHWC (C % 8 == 0); margin [C] fp32; grad like s; loss[1];
+// partial >= 1024 floats; counter: one zeroed uint (reset by the kernel).
+MDA_API int mda_ofd_loss(const void* s, const void* t, const float* margin, void* grad, float* loss,
+                         float* partial, unsigned* counter, int64_t M, int64_t C, float scale,
+                         hipStream_t st) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  int64_t blocks = (M * C / 8 + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(ofd_loss_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const bf16_t*)s,
+                     (const bf16_t*)t, margin, (bf16_t*)grad, partial, counter, loss, M, (int)C, scale);
+  MDA_CHECK_LAUNCH();
+}
 
 // fs [N, HW, C] (NHWC), ft [N, HW, Ct]; grad like fs; loss[1]; partial >= N floats.
 MDA_API int mda_at_loss(int64_t dts, int64_t dtt, const void* fs, const void* ft, void* grad,

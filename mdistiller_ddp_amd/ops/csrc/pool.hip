@@ -131,3 +131,37 @@ MDA_API int mda_maxpool_bwd(const void* dy, const void* idx, void* dx, int64_t N
                      (const bf16_t*)dy, (const uint8_t*)idx, (bf16_t*)dx, q);
   MDA_CHECK_LAUNCH();
 }
+
+// ---------------------------------------------------------------------------
+// Channel shuffle on NHWC bf16 (ShuffleNet, reference models/cifar/
+// ShuffleNetv1.py:7-15 / ShuffleNetv2.py:22-31): y[m, j*g + i] = x[m, i*cpg + j]
+// with cpg = C / g.  One thread per 2-channel output pair (4-byte stores),
+// gathering inside the pixel's row (an L1/L2-resident C*2-byte span).  Its own
+// inverse with g' = cpg, which is the backward.
+namespace {
+__global__ void __launch_bounds__(256)
+channel_shuffle_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int64_t M, int C, int g) {
+  const int cpg = C / g;
+  const int64_t total2 = M * C / 2;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total2;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = (i * 2) / C;
+    const int c = (int)(i * 2 - m * C);
+    const bf16_t* row = x + m * C;
+    const int c1 = c + 1;
+    const bf16_t a = row[(c % g) * cpg + c / g];
+    const bf16_t b = row[(c1 % g) * cpg + c1 / g];
+    *(uint32_t*)(y + i * 2) = (uint32_t)a | ((uint32_t)b << 16);
+  }
+}
+}  // namespace
+
+MDA_API int mda_channel_shuffle(const void* x, void* y, int64_t M, int64_t C, int64_t g, hipStream_t st) {
+  if (C % g || C % 2) return (int)hipErrorInvalidValue;
+  int64_t blocks = (M * C / 2 + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(channel_shuffle_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const bf16_t*)x,
+                     (bf16_t*)y, M, (int)C, (int)g);
+  MDA_CHECK_LAUNCH();
+}

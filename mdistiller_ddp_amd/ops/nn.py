@@ -60,6 +60,10 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d | None = No
     # forward through this op -- e.g. the detection Conv2d with a norm child --
     # must not recurse
     y = nn.Conv2d._conv_forward(conv, x, conv.weight, conv.bias) if isinstance(conv, nn.Conv2d) else conv(x)
+    if bn is not None and isinstance(bn, nn.BatchNorm2d) and hip_enabled_for(y):
+        # convolution on PyTorch (grouped 1x1 of ShuffleNetV1, odd shapes), the
+        # BN (+res) (+act) still on the fused native kernels
+        return bn_act(y, bn, act, residual, want_preact)
     if bn is not None:
         y = _bn(y, bn)
     if residual is not None:
@@ -89,8 +93,35 @@ def conv(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
     return conv_bn_act(x, conv, None, "none")[0]
 
 
+class _ChannelShuffle(torch.autograd.Function):
+    """NHWC bf16 channel shuffle in one gather pass (csrc/pool.hip); the
+    backward is the inverse shuffle (groups' = C / groups)."""
+
+    @staticmethod
+    def forward(ctx, x, groups):
+        from . import _ext
+        x = x.contiguous(memory_format=torch.channels_last)
+        n, c, h, w = x.shape
+        y = torch.empty_like(x)
+        _ext.call("mda_channel_shuffle", x, y, n * h * w, c, groups)
+        ctx.groups = groups
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import _ext
+        dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        n, c, h, w = dy.shape
+        dx = torch.empty_like(dy)
+        _ext.call("mda_channel_shuffle", dy, dx, n * h * w, c, c // ctx.groups)
+        return dx, None
+
+
 def channel_shuffle(x: torch.Tensor, groups: int) -> torch.Tensor:
     n, c, h, w = x.shape
+    if (hip_enabled_for(x) and x.dtype == torch.bfloat16 and c % groups == 0 and c % 2 == 0
+            and x.is_contiguous(memory_format=torch.channels_last)):
+        return _ChannelShuffle.apply(x, groups)
     return x.reshape(n, groups, c // groups, h, w).transpose(1, 2).reshape(n, c, h, w)
 
 

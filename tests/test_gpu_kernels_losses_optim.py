@@ -135,3 +135,25 @@ def test_at_loss_kernel(shape_s, shape_t, dtype):
     tol = 1e-4 if dtype == torch.float32 else 3e-2
     torch.testing.assert_close(l1.float(), l2, rtol=tol, atol=1e-7)
     torch.testing.assert_close(a.grad.float(), b.grad, rtol=tol, atol=tol * b.grad.abs().max().item())
+
+
+@pytest.mark.parametrize("N,C,H", [(8, 64, 8), (16, 256, 4), (3, 24, 5)])
+def test_ofd_fused_loss_matches_torch(N, C, H):
+    import importlib
+    ofd_mod = importlib.import_module("mdistiller_ddp_amd.distillers.OFD")
+    from mdistiller_ddp_amd.ops.backend import use_backend
+    torch.manual_seed(7)
+    s = torch.randn(N, C, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    t = torch.randn(N, C, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    m = -torch.rand(1, C, 1, 1, device="cuda")
+    sh = s.clone().requires_grad_(True)
+    with use_backend("hip"):
+        assert ofd_mod._ofd_native_ok(sh, t)
+        l = ofd_mod.feat_loss(sh, t, m)
+    (l * 0.5).backward()
+    sr = s.float().clone().requires_grad_(True)
+    with use_backend("torch"):
+        lr = ofd_mod.feat_loss(sr, t.float(), m)
+    (lr * 0.5).backward()
+    torch.testing.assert_close(l, lr, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(sh.grad.float(), sr.grad, rtol=2e-2, atol=1e-4)

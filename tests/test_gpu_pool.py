@@ -43,3 +43,22 @@ def test_pad_channels8(dtype):
     assert hip_train.pad_channels8(x) is y  # cached for the same version / stream
     x.add_(1.0)
     assert hip_train.pad_channels8(x) is not y
+
+
+@pytest.mark.parametrize("C,g", [(240, 3), (58, 2), (120, 4)])
+def test_channel_shuffle_native(C, g):
+    from mdistiller_ddp_amd.ops import nn as mnn
+    from mdistiller_ddp_amd.ops.backend import use_backend
+    torch.manual_seed(0)
+    x = torch.randn(4, C, 6, 5, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    xh = x.clone().requires_grad_(True)
+    with use_backend("hip"):
+        y = mnn.channel_shuffle(xh, g)
+    n, c, h, w = x.shape
+    ref = x.float().reshape(n, g, c // g, h, w).transpose(1, 2).reshape(n, c, h, w)
+    torch.testing.assert_close(y.float(), ref, rtol=0, atol=0)
+    go = torch.randn_like(ref)
+    y.backward(go.to(torch.bfloat16))
+    xr = x.float().clone().requires_grad_(True)
+    (xr.reshape(n, g, c // g, h, w).transpose(1, 2).reshape(n, c, h, w) * go.to(torch.bfloat16).float()).sum().backward()
+    torch.testing.assert_close(xh.grad.float(), xr.grad, rtol=0, atol=0)

@@ -39,7 +39,8 @@ SIGNATURES = {
     "mda_conv_set_stamps": "p",
     "mda_conv_fwd_bnstats": "ppppp" + "i" * 15 + "p" * 8 + "ff" + "ps",
     "mda_conv_dgrad": "pppp" + "i" * 14 + "s",
-    "mda_conv_wgrad": "pppp" + "i" * 13 + "fiis",
+    "mda_conv_wgrad": "pppp" + "i" * 13 + "fiiis",
+    "mda_pack_conv_weights_grouped": "ppp" + "i" * 7 + "s",
     "mda_pad_channels": "ippiiis",
     # max pooling (csrc/pool.hip)
     "mda_maxpool_fwd": "ppp" + "i" * 9 + "s",

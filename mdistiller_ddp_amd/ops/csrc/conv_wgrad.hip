@@ -436,7 +436,7 @@ constexpr int WGR_COLS = 16, WGR_SLICES = 16;
 __global__ void __launch_bounds__(256)
 wgrad_reduce_kernel(const float* __restrict__ partial, float* __restrict__ grad, int splits,
                     int Cout, int Cin, int KH, int KW, int Kp, float scale, int accumulate,
-                    int cin_keep) {
+                    int cin_keep, int groups) {
   __shared__ float4 red[WGR_SLICES][WGR_COLS];
   const int c = threadIdx.x % WGR_COLS, sl = threadIdx.x / WGR_COLS;
   const int64_t total4 = (int64_t)Cout * Kp / 4;
@@ -476,7 +476,14 @@ wgrad_reduce_kernel(const float* __restrict__ partial, float* __restrict__ grad,
     const int tap = k / Cin, ci = k - tap * Cin;
     // channel-padded stems (Cin 3 -> 8): only the real input channels exist in grad
     if (ci >= cin_keep) continue;
-    const int64_t dst = ((int64_t)co * cin_keep + ci) * KH * KW + tap;
+    int ciw = ci, cin_w = cin_keep;
+    if (groups > 1) {  // block-diagonal dense product: keep the co's own group
+      const int cin_g = Cin / groups, g = co / (Cout / groups);
+      if (ci / cin_g != g) continue;
+      ciw = ci - g * cin_g;
+      cin_w = cin_g;
+    }
+    const int64_t dst = ((int64_t)co * cin_w + ciw) * KH * KW + tap;
     grad[dst] = (accumulate ? grad[dst] : 0.f) + scale * v[q];
   }
 }
@@ -703,9 +710,10 @@ MDA_API int mda_conv_wgrad(const void* x, const void* dy, float* partial, float*
                            int64_t H, int64_t W, int64_t Cin, int64_t Ho, int64_t Wo, int64_t Cout,
                            int64_t KH, int64_t KW, int64_t stride, int64_t pad, int64_t Kp,
                            int64_t splits, float scale, int64_t accumulate, int64_t cin_keep,
-                           hipStream_t st) {
+                           int64_t groups, hipStream_t st) {
   if (Cout % 8 || Kp % TK) return (int)hipErrorInvalidValue;
   if (cin_keep <= 0 || cin_keep > Cin) cin_keep = Cin;
+  if (groups > 1 && (Cin % groups || Cout % groups)) return (int)hipErrorInvalidValue;
   WgParams p;
   p.x = (const bf16_t*)x; p.dy = (const bf16_t*)dy; p.partial = partial;
   p.N = N; p.H = H; p.W = W; p.Cin = Cin; p.Ho = Ho; p.Wo = Wo; p.Cout = Cout; p.KH = KH;
@@ -742,7 +750,53 @@ MDA_API int mda_conv_wgrad(const void* x, const void* dy, float* partial, float*
   const int blocks = (int)((total4 + WGR_COLS - 1) / WGR_COLS);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, partial, grad,
                      (int)splits, (int)Cout, (int)Cin, (int)KH, (int)KW, (int)Kp, scale,
-                     (int)accumulate, (int)cin_keep);
+                     (int)accumulate, (int)cin_keep, (int)(groups > 1 ? groups : 1));
+  MDA_CHECK_LAUNCH();
+}
+
+namespace {
+// Grouped conv (groups G, not depthwise) as ONE dense GEMM on the block-
+// diagonal weight: w fp32 [Cout, Cin/G, KH, KW] -> wf bf16 [Cout, Kp] with
+// k = tap*Cin + ci (zero where ci is outside co's group, and k >= K) and,
+// optionally, wt bf16 [Cin, KpT] with k = tap*Cout + co (padding zeroed).
+// G x the MFMA work of a grouped kernel, but the grouped 1x1 convs this
+// serves (ShuffleNetV1, G = 3) are a small part of their network's FLOPs.
+__global__ void __launch_bounds__(256)
+pack_grouped_kernel(const float* __restrict__ w, bf16_t* __restrict__ wf, bf16_t* __restrict__ wt,
+                    int Cout, int Cin, int KH, int KW, int Kp, int KpT, int G) {
+  const int cin_g = Cin / G, cout_g = Cout / G, KK = KH * KW, K = KK * Cin;
+  const int64_t total = (int64_t)Cout * Kp;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int co = (int)(i / Kp), k = (int)(i - (i / Kp) * Kp);
+    float v = 0.f;
+    if (k < K) {
+      const int tap = k / Cin, ci = k - tap * Cin;
+      const int g = co / cout_g;
+      if (ci / cin_g == g) v = w[((int64_t)co * cin_g + (ci - g * cin_g)) * KK + tap];
+      if (wt) wt[(int64_t)ci * KpT + tap * Cout + co] = f2bf(v);
+    }
+    wf[i] = f2bf(v);
+  }
+  if (wt) {
+    const int padw = KpT - KK * Cout;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < (int64_t)Cin * padw;
+         i += (int64_t)gridDim.x * blockDim.x) {
+      const int ci = (int)(i / padw), j = (int)(i - (i / padw) * padw);
+      wt[(int64_t)ci * KpT + KK * Cout + j] = 0;
+    }
+  }
+}
+}  // namespace
+
+MDA_API int mda_pack_conv_weights_grouped(const float* w, void* wf, void* wt, int64_t Cout, int64_t Cin,
+                                          int64_t KH, int64_t KW, int64_t Kp, int64_t KpT, int64_t G,
+                                          hipStream_t st) {
+  if (G < 1 || Cin % G || Cout % G) return (int)hipErrorInvalidValue;
+  const int64_t total = Cout * Kp;
+  const int blocks = (int)std::min<int64_t>((total + 255) / 256, 2048);
+  hipLaunchKernelGGL(pack_grouped_kernel, dim3(blocks), dim3(256), 0, st, w, (bf16_t*)wf, (bf16_t*)wt,
+                     (int)Cout, (int)Cin, (int)KH, (int)KW, (int)Kp, (int)KpT, (int)G);
   MDA_CHECK_LAUNCH();
 }
 

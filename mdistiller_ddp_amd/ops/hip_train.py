@@ -186,6 +186,13 @@ def pad_channels8(x):
     return y
 
 
+_GROUPED_NATIVE = [os.environ.get("MDA_GROUPED_NATIVE", "0") == "1"]
+
+
+def set_grouped_native(on: bool) -> None:
+    _GROUPED_NATIVE[0] = bool(on)
+
+
 def train_supported(x, conv, bn) -> bool:
     if not (x.is_cuda and x.dim() == 4 and isinstance(conv, nn.Conv2d)):
         return False
@@ -194,7 +201,14 @@ def train_supported(x, conv, bn) -> bool:
     if conv.dilation != (1, 1) or conv.padding_mode != "zeros" or conv.bias is not None:
         return False
     if conv.groups != 1:
-        return dw_train_supported(x, conv, bn)
+        if is_depthwise(conv):
+            return dw_train_supported(x, conv, bn)
+        # grouped (ShuffleNetV1): one dense GEMM on the block-diagonal weight.
+        # Opt-in (MDA_GROUPED_NATIVE=1): G x the MFMA work plus a per-call pack
+        # measured slower than MIOpen's grouped kernels on ShuffleV1 (5.48 vs
+        # 5.34 ms/step, profiles/r2_misc_ab.md); the GPU test runs it either way.
+        if conv.in_channels % 8 or conv.out_channels % 8 or not _GROUPED_NATIVE[0]:
+            return False
     if conv.stride[0] != conv.stride[1] or not isinstance(conv.padding, tuple) or conv.padding[0] != conv.padding[1]:
         return False
     if conv.kernel_size[0] != conv.kernel_size[1]:
@@ -258,9 +272,11 @@ class _ConvBNActTrain(torch.autograd.Function):
             return _dw_forward(ctx, x, weight, gamma, beta, residual, stride, pad, act, bn,
                                want_preact)
         ctx.kind = "dense"
+        G = meta[4] if len(meta) > 4 and meta[3] == "grouped" else 1
+        ctx.groups = G
         need_dx = ctx.needs_input_grad[0]
         cin_w = weight.shape[1]
-        chpad = (not need_dx) and needs_channel_pad(cin_w)
+        chpad = G == 1 and (not need_dx) and needs_channel_pad(cin_w)
         x = pad_channels8(x) if chpad else _cl_bf16(x)
         N, Cin, H, W = x.shape
         Cout, _, KH, KW = weight.shape
@@ -273,8 +289,13 @@ class _ConvBNActTrain(torch.autograd.Function):
         dev = x.device
         ctx.cin_keep = cin_w if chpad else 0
         packs = _ACTIVE[0]
-        ent = packs.lookup(weight, need_dx) if (packs is not None and not chpad) else None
-        if chpad:  # stem: forward operand with zero weights for the pad channels
+        ent = packs.lookup(weight, need_dx) if (packs is not None and not chpad and G == 1) else None
+        if G > 1:  # block-diagonal dense operands, packed per call (no multi-layer table)
+            wf = torch.empty(Cout, Kp, dtype=torch.bfloat16, device=dev)
+            wt = torch.empty(Cin, KpT, dtype=torch.bfloat16, device=dev) if need_dx else None
+            _ext.call("mda_pack_conv_weights_grouped", weight.detach().float().contiguous(), wf, wt,
+                      Cout, Cin, KH, KW, Kp, KpT, G)
+        elif chpad:  # stem: forward operand with zero weights for the pad channels
             wf = torch.empty(Cout, Kp, dtype=torch.bfloat16, device=dev)
             wt = None
             _ext.call("mda_pack_conv_weights_pad", weight.detach().contiguous(), wf, Cout, cin_w,
@@ -349,7 +370,7 @@ class _ConvBNActTrain(torch.autograd.Function):
             direct_w = weight.grad is not None and weight.grad.is_contiguous()
             target = weight.grad if direct_w else torch.empty_like(weight, memory_format=torch.contiguous_format)
             _ext.call("mda_conv_wgrad", x, dy, part, target, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
-                      stride, pad, Kp, sp, 1.0, 1 if direct_w else 0, ctx.cin_keep)
+                      stride, pad, Kp, sp, 1.0, 1 if direct_w else 0, ctx.cin_keep, ctx.groups)
             dw = None if direct_w else target
             if direct_w:
                 notify_grad(weight)
@@ -484,7 +505,7 @@ def conv_wgrad(x, dy, weight_shape, stride, pad):
     part = torch.empty(sp * Cout * Kp, dtype=torch.float32, device=x.device)
     out = torch.empty(weight_shape, dtype=torch.float32, device=x.device)
     _ext.call("mda_conv_wgrad", x, dy, part, out, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
-              Kp, sp, 1.0, 0, 0)
+              Kp, sp, 1.0, 0, 0, 1)
     return out
 
 
@@ -600,7 +621,7 @@ class _ConvTrain(torch.autograd.Function):
             direct_w = weight.grad is not None and weight.grad.is_contiguous()
             target = weight.grad if direct_w else torch.empty_like(weight, memory_format=torch.contiguous_format)
             _ext.call("mda_conv_wgrad", x, dz, part, target, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
-                      stride, pad, Kp, sp, 1.0, 1 if direct_w else 0, ctx.cin_keep)
+                      stride, pad, Kp, sp, 1.0, 1 if direct_w else 0, ctx.cin_keep, 1)
             dw = None if direct_w else target
             if direct_w:
                 notify_grad(weight)
@@ -696,8 +717,10 @@ def conv_trainbn_nograd(x, conv, bn, act, residual, want_preact):
 
 def conv_bn_act_train(x, conv, bn, act, residual, want_preact):
     meta = (conv.stride[0], conv.padding[0], _ACT[act])
-    if conv.groups != 1:
+    if is_depthwise(conv):
         meta = meta + ("dw",)
+    elif conv.groups != 1:
+        meta = meta + ("grouped", conv.groups)
     out, pre = _ConvBNActTrain.apply(x, conv.weight, bn.weight, bn.bias, residual, meta, bn,
                                      bool(want_preact))
     return out, pre

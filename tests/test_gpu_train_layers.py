@@ -216,3 +216,44 @@ def test_wrn_convs_take_native_training_path():
     n_bn = sum(1 for mod in m.modules() if isinstance(mod, nn.BatchNorm2d))
     assert calls["conv"] == n_conv - sum(1 for b in m.modules() if hasattr(b, "bn2")), calls
     assert calls["bn"] == n_bn - sum(1 for b in m.modules() if hasattr(b, "bn2")), calls
+
+
+@pytest.mark.parametrize("N,Cin,H,Cout,G,with_res", [(8, 240, 16, 120, 3, False), (8, 120, 8, 480, 3, True),
+                                                      (4, 480, 8, 240, 3, False), (8, 64, 16, 32, 2, True)])
+def test_grouped_conv_bn_act_train(N, Cin, H, Cout, G, with_res):
+    """Grouped 1x1 conv (ShuffleNetV1) + BN (+res) + ReLU on the native path (dense
+    block-diagonal GEMM) vs fp32 PyTorch: outputs, running stats, all gradients."""
+    torch.manual_seed(2)
+    conv = nn.Conv2d(Cin, Cout, 1, 1, 0, groups=G, bias=False).cuda()
+    bn = nn.BatchNorm2d(Cout).cuda()
+    conv_r, bn_r = copy.deepcopy(conv), copy.deepcopy(bn)
+    x = torch.randn(N, Cin, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    res = torch.randn(N, Cout, H, H, device="cuda").to(torch.bfloat16) if with_res else None
+    x1 = x.clone().requires_grad_(True)
+    r1 = res.clone().requires_grad_(True) if with_res else None
+    hip_train.set_grouped_native(True)
+    try:
+        assert hip_train.train_supported(x1, conv, bn)
+        out, _ = hip_train.conv_bn_act_train(x1, conv, bn, "relu", r1, False)
+    finally:
+        hip_train.set_grouped_native(False)
+    g = torch.randn_like(out.float()).to(torch.bfloat16).float()
+    out.float().backward(g)
+    x2 = x.float().clone().requires_grad_(True)
+    r2 = res.float().clone().requires_grad_(True) if with_res else None
+    z = bn_r(conv_r(x2))
+    if with_res:
+        z = z + r2
+    F.relu(z).backward(g)
+    torch.testing.assert_close(out.float(), F.relu(z), atol=4e-2, rtol=4e-2)
+    torch.testing.assert_close(bn.running_mean, bn_r.running_mean, atol=1e-3, rtol=1e-3)
+
+    def rel(a, b):
+        return ((a.float() - b).norm() / (b.norm() + 1e-12)).item()
+
+    assert conv.weight.grad.shape == conv_r.weight.grad.shape
+    assert rel(conv.weight.grad, conv_r.weight.grad) < 5e-2
+    assert rel(x1.grad, x2.grad) < 5e-2
+    assert rel(bn.weight.grad, bn_r.weight.grad) < 5e-2
+    if with_res:
+        assert rel(r1.grad, r2.grad) < 5e-2

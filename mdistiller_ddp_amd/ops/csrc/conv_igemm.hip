@@ -995,50 +995,9 @@ conv_halo_kernel(const ConvParams p) {
   }
   const int bswz = (frow >> 1) & 7;
 
-  // BN = 32 (deep-K 8x8 layers: 36 short steps): the A fragments (patch rows)
-  // of tap t+1 are read during tap t, within a chunk (its patch is resident
-  // from tap 0 on).  (At BN = 64 the extra registers made the kernel spill.)
-  constexpr bool APRE = BN == 32;
-  bf16x8 afp[APRE ? 2 : 1][2][MI];  // [buffer][kk][i]
-  auto load_a = [&](int pbuf, int tap, int buf) {
-    const char* Ps = smem + pbuf * PATCH;
-    const int kh = tap / 3, kw = tap - (tap / 3) * 3;
-    const int toff = kh * PW + kw;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int q = kk * 4 + g4;
-#pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        const int pr = a_prow[i] + toff;
-        afp[buf][kk][i] = *(const bf16x8*)(Ps + pr * 128 + ((q ^ ((pr >> 1) & 7)) * 16));
-      }
-    }
-  };
   auto compute = [&](int pbuf, int bbuf, int tap) {
     const char* Ps = smem + pbuf * PATCH;
     const char* Bs = smem + 2 * PATCH + bbuf * BT;
-    if constexpr (APRE) {
-      if (tap == 0) load_a(pbuf, 0, 0);
-      bf16x8 bfr[2][NI];
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int q = kk * 4 + g4;
-#pragma unroll
-        for (int j = 0; j < NI; ++j)
-          bfr[kk][j] = *(const bf16x8*)(Bs + (wn * (BN / 2) + j * 16 + frow) * 128 + ((q ^ bswz) * 16));
-      }
-      if (tap < 8) load_a(pbuf, tap + 1, (tap + 1) & 1);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-          for (int j = 0; j < NI; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afp[(APRE ? tap : 0) & 1][kk][i], bfr[kk][j],
-                                                                acc[i][j], 0, 0, 0);
-      return;
-    }
     const int kh = tap / 3, kw = tap - (tap / 3) * 3;
     const int toff = kh * PW + kw;
 #pragma unroll

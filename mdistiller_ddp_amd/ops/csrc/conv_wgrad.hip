@@ -697,7 +697,11 @@ MDA_API int mda_wgrad_plan(int64_t M, int64_t Cout, int64_t Cin, int64_t KH, int
     // one round of blocks over the CU slots (LDS-limited blocks per CU), each
     // split >= 8 stages of 64 pixels, at most 128 partial sets
     const int64_t occ = tile == 128128 ? 1 : (tile == 64064 ? 3 : 2);
-    sp = (256 * occ + tiles - 1) / tiles;
+    static const int64_t slots = [] {  // CU slots to fill (MDA_WG_SLOTS, A/B)
+      const char* e = getenv("MDA_WG_SLOTS");
+      return e ? (int64_t)atoi(e) : (int64_t)256;
+    }();
+    sp = (slots * occ + tiles - 1) / tiles;
     sp = std::min<int64_t>(sp, std::max<int64_t>(1, M / (8 * TM)));
     sp = std::max<int64_t>(1, std::min<int64_t>(sp, 128));
   }

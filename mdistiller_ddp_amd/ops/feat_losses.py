@@ -86,11 +86,20 @@ def single_stage_nst_loss(f_s, f_t):
     an (N, C, C, HW) tensor.
     """
     f_s, f_t = _pool_to_match(f_s, f_t)
-    f_s = F.normalize(f_s.float().reshape(f_s.shape[0], f_s.shape[1], -1), dim=2)
-    f_t = F.normalize(f_t.float().reshape(f_t.shape[0], f_t.shape[1], -1), dim=2)
 
-    def kmean(a, b):
-        return torch.bmm(a, b.transpose(1, 2)).pow(2).mean()
+    def rows(f):
+        # [N, HW, C] channel columns: a free view of a channels_last map (the
+        # [N, C, HW] view of one costs a transposing copy, fwd and bwd)
+        n, c = f.shape[0], f.shape[1]
+        if f.is_contiguous(memory_format=torch.channels_last) and not f.is_contiguous():
+            return f.permute(0, 2, 3, 1).reshape(n, -1, c).float()
+        return f.float().reshape(n, c, -1).transpose(1, 2)
+
+    f_s = F.normalize(rows(f_s), dim=1)
+    f_t = F.normalize(rows(f_t), dim=1)
+
+    def kmean(a, b):  # mean_{cd} (a_c . b_d)^2 with a, b [N, HW, C]
+        return torch.bmm(a.transpose(1, 2), b).pow(2).mean()
 
     return kmean(f_t, f_t).detach() + kmean(f_s, f_s) - 2 * kmean(f_s, f_t)
 
@@ -100,10 +109,23 @@ def nst_loss(g_s, g_t):
 
 
 # ---------------------------------------------------------------- PKT
+def _flat(f):
+    """``f.reshape(N, -1)`` in fp32 up to a fixed column permutation.
+
+    PKT, SP and RKD only use row norms, row dot products and row differences, which
+    are invariant to permuting the flattened columns, so a channels_last map is
+    flattened in its memory order (a free view) instead of being made NCHW first.
+    """
+    n = f.shape[0]
+    if f.dim() == 4 and f.is_contiguous(memory_format=torch.channels_last) and not f.is_contiguous():
+        return f.permute(0, 2, 3, 1).reshape(n, -1).float()
+    return f.float().reshape(n, -1)
+
+
 def pkt_loss(f_s, f_t, eps=1e-7):
     """`distillers/PKT.py:8-35`."""
-    f_s = f_s.float().reshape(f_s.shape[0], -1)
-    f_t = f_t.float().reshape(f_t.shape[0], -1)
+    f_s = _flat(f_s)
+    f_t = _flat(f_t)
     f_s = f_s / (f_s.pow(2).sum(1, keepdim=True).sqrt() + eps)
     f_s = torch.nan_to_num(f_s, nan=0.0)
     f_t = f_t / (f_t.pow(2).sum(1, keepdim=True).sqrt() + eps)
@@ -119,8 +141,8 @@ def pkt_loss(f_s, f_t, eps=1e-7):
 def similarity_loss(f_s, f_t):
     """`distillers/SP.py:12-24`."""
     bsz = f_s.shape[0]
-    f_s = f_s.float().reshape(bsz, -1)
-    f_t = f_t.float().reshape(bsz, -1)
+    f_s = _flat(f_s)
+    f_t = _flat(f_t)
     G_s = F.normalize(f_s @ f_s.t())
     G_t = F.normalize(f_t @ f_t.t())
     d = G_t - G_s
@@ -157,8 +179,8 @@ def _positive_mean(x):
 
 def rkd_loss(f_s, f_t, squared=False, eps=1e-12, distance_weight=25, angle_weight=50):
     """`distillers/RKD.py:21-50`."""
-    stu = f_s.float().reshape(f_s.shape[0], -1)
-    tea = f_t.float().reshape(f_t.shape[0], -1)
+    stu = _flat(f_s)
+    tea = _flat(f_t)
     with torch.no_grad():
         t_d = _pdist(tea, squared, eps)
         t_d = t_d / _positive_mean(t_d)

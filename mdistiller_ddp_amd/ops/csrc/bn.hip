@@ -354,16 +354,21 @@ bn_finalize_kernel(const float* __restrict__ partial, int nblk, int M, int C,
   const int c = blockIdx.x * 8 + k;
   double acc = 0.0;
   if (c < C) {
+    // 8 independent loads in flight per round: a 512-row partial is 4 L2
+    // round trips per thread instead of 8 (the finalize is latency-bound)
     const float* src = partial + q * C + c;
-    float x[4];
+    float x[8];
     int r = g;
-    for (; r + 48 < nblk; r += 64) {
+    for (; r + 112 < nblk; r += 128) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) x[u] = src[(int64_t)(r + 16 * u) * 2 * C];
+      for (int u = 0; u < 8; ++u) x[u] = src[(int64_t)(r + 16 * u) * 2 * C];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) acc += (double)x[u];
+      for (int u = 0; u < 8; ++u) acc += (double)x[u];
     }
-    for (; r < nblk; r += 16) acc += (double)src[(int64_t)r * 2 * C];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = r + 16 * u < nblk ? src[(int64_t)(r + 16 * u) * 2 * C] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += (double)x[u];  // + 0.0 is exact
   }
   red[g][v] = acc;
   __syncthreads();

@@ -12,7 +12,8 @@
 //  * dgrad     -- dx[h, w] = sum over taps whose (h + p - kh, w + p - kw) lands
 //    on the stride grid of dy; same V x OWT thread tile.
 //  * wgrad     -- per-block partial sums of dy * x for every (tap, channel),
-//    reduced over pixel lanes through LDS one tap at a time, then a
+//    reduced over pixel lanes through LDS by all threads (three taps per
+//    round, (output, slice) pairs), then a
 //    channel-parallel finalize kernel combines the blocks in fixed order and
 //    writes/accumulates the fp32 [C, K, K] gradient (deterministic).
 // Weights arrive as fp32 packed tap-major [KH*KW, C] (coalesced per-channel
@@ -212,7 +213,9 @@ dw_wgrad_partial_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__
                         int pad) {
   constexpr int NCOLS = (OWT - 1) * S + KS;
   constexpr int KK = KS * KS;
-  __shared__ float red[256 * 8];
+  constexpr int TG = 3;  // taps per reduction round
+  __shared__ float red[TG * 256 * V];
+  __shared__ float red2[1024];  // (output, slice) pair sums when SL > 1 (OUT*SL <= 1024)
   const int CG = C / V;
   const int PL = max(1, 256 / CG);  // lanes per block
   const int tid = threadIdx.x;
@@ -269,20 +272,40 @@ dw_wgrad_partial_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__
       }
     }
   }
-  // reduce over lanes, one tap at a time: LDS [PL][C]
+  // Reduce over the PL lanes with every thread, three taps per round (LDS
+  // red[3][PL][C], PL*C <= 256*V: 24.6 KB, so load-phase occupancy stays at
+  // 5+ blocks/CU): (output, slice) pairs each sum PL/SL lanes (slice-major,
+  // neighbouring threads read neighbouring channels), then each output sums
+  // its SL slices -- fixed order.  (One thread per channel walking all PL
+  // lanes tap by tap was ~1150 dependent LDS reads for C = 16, PL = 128.)
+  const int OUT = TG * C;  // outputs per round
+  int SL = 1;
+  while (SL * 2 <= PL && OUT * SL * 2 <= 1024) SL *= 2;
 #pragma unroll
-  for (int t = 0; t < KK; ++t) {
+  for (int g = 0; g < KK / TG; ++g) {
     if (active) {
 #pragma unroll
-      for (int v = 0; v < V; ++v) red[pl * C + c0 + v] = acc[t][v];
+      for (int t = 0; t < TG; ++t)
+#pragma unroll
+        for (int v = 0; v < V; ++v) red[(t * PL + pl) * C + c0 + v] = acc[g * TG + t][v];
     }
     __syncthreads();
-    for (int c = tid; c < C; c += blockDim.x) {
-      float s = 0.f;
-      for (int q = 0; q < PL; ++q) s += red[q * C + c];
-      partial[((int64_t)blockIdx.x * KK + t) * C + c] = s;
+    float* dst = partial + ((int64_t)blockIdx.x * KK + g * TG) * C;  // [blk][tap][c]
+    for (int pr = tid; pr < OUT * SL; pr += blockDim.x) {
+      const int s = pr / OUT, o = pr - s * OUT;
+      const int t = o / C, c = o - t * C;
+      float a = 0.f;
+      for (int q = s; q < PL; q += SL) a += red[(t * PL + q) * C + c];
+      if (SL == 1) dst[o] = a; else red2[pr] = a;
     }
     __syncthreads();
+    if (SL > 1) {
+      for (int o = tid; o < OUT; o += blockDim.x) {
+        float a = 0.f;
+        for (int j = 0; j < SL; ++j) a += red2[j * OUT + o];
+        dst[o] = a;
+      }
+    }
   }
 }
 

@@ -526,6 +526,8 @@ pack_kernel(const float* __restrict__ w, bf16_t* __restrict__ wf, bf16_t* __rest
 // coalesced reads of the OIHW fp32 rows (taps contiguous per (co, ci)) and
 // written as T-long contiguous runs of both packed layouts:
 //   wf[co][tap*Cin + ci]   and   wt[ci][tap*Cout + co].
+// Depthwise layers ride along (Cin = -1 rows): fp32 [C,1,3,3] -> tap-major
+// [9, C] (csrc/dwconv.hip's operand), 256 elements per tile.
 // Padding columns (k >= K, and the dgrad tail) are never touched: they are
 // zeroed once by the per-layer pack at registration and stay zero.
 // (The previous element-per-thread version scattered 2-byte stores at
@@ -547,6 +549,14 @@ pack_multi_kernel(const int64_t* __restrict__ table, int L) {
   int l = 0;
   while (l + 1 < L && (int64_t)blockIdx.x >= tb[(l + 1) * PACK_FIELDS + 9]) ++l;
   const int64_t* e = tb + l * PACK_FIELDS;
+  if (e[4] < 0) {  // depthwise row {w [C,1,3,3], dst fp32 [9, C], 0, C, -1, ...}: 256 elements a tile
+    const float* w = (const float*)e[0];
+    float* dst = (float*)e[1];
+    const int C = (int)e[3];
+    const int i = (int)(blockIdx.x - e[9]) * 256 + threadIdx.x;
+    if (i < 9 * C) dst[i] = w[(i % C) * 9 + i / C];
+    return;  // block-uniform branch (l depends on blockIdx only)
+  }
   const float* w = (const float*)e[0];
   bf16_t* wf = (bf16_t*)e[1];
   bf16_t* wt = (bf16_t*)e[2];

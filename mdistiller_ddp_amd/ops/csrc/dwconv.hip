@@ -49,6 +49,38 @@ __device__ __forceinline__ void st_vec(bf16_t* p, const float (&v)[V]) {
   *reinterpret_cast<typename vec<V>::t*>(p) = r;
 }
 
+// Raw (packed bf16) vector load with zero fill, and its unpack: the kernels
+// below issue every load of a work item before any math (the layers of the
+// CIFAR students are a few dozen blocks: latency, not bandwidth, bound).
+template <int V>
+__device__ __forceinline__ typename vec<V>::t ld_raw(const bf16_t* p, bool ok) {
+  typename vec<V>::t r{};
+  if (ok) r = *reinterpret_cast<const typename vec<V>::t*>(p);
+  return r;
+}
+
+template <int V>
+__device__ __forceinline__ void unpack(const typename vec<V>::t& r, float (&o)[V]) {
+  const bf16_t* e = reinterpret_cast<const bf16_t*>(&r);
+#pragma unroll
+  for (int i = 0; i < V; ++i) o[i] = bf2f(e[i]);
+}
+
+// V consecutive fp32 weights of one tap (16-byte loads when V >= 4).
+template <int V>
+__device__ __forceinline__ void ld_w(const float* p, float (&o)[V]) {
+  if constexpr (V >= 4) {
+#pragma unroll
+    for (int i = 0; i < V; i += 4) {
+      const float4 t = *reinterpret_cast<const float4*>(p + i);
+      o[i] = t.x; o[i + 1] = t.y; o[i + 2] = t.z; o[i + 3] = t.w;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i) o[i] = p[i];
+  }
+}
+
 __device__ __forceinline__ float act_fn(float v, int act) {
   if (act == 1) return fmaxf(v, 0.f);
   if (act == 2) return fminf(fmaxf(v, 0.f), 6.f);
@@ -83,6 +115,21 @@ __global__ void __launch_bounds__(256) dw_fwd_kernel(const DwParams p) {
     const int c0 = cg * V;
     const int wo0 = wt * OWT;
     const int iw0 = wo0 * S - p.pad;
+    float wv[KS * KS][V];
+#pragma unroll
+    for (int t = 0; t < KS * KS; ++t) ld_w<V>(p.w + t * p.C + c0, wv[t]);
+    typename vec<V>::t raw[KS][NCOLS];
+#pragma unroll
+    for (int kh = 0; kh < KS; ++kh) {
+      const int ih = ho * S - p.pad + kh;
+      const bool okr = (unsigned)ih < (unsigned)p.H;
+      const bf16_t* row = p.x + (((int64_t)n * p.H + (okr ? ih : 0)) * p.W) * p.C + c0;
+#pragma unroll
+      for (int q = 0; q < NCOLS; ++q) {
+        const int iw = iw0 + q;
+        raw[kh][q] = ld_raw<V>(row + (int64_t)iw * p.C, okr && (unsigned)iw < (unsigned)p.W);
+      }
+    }
     float acc[OWT][V];
 #pragma unroll
     for (int j = 0; j < OWT; ++j)
@@ -90,31 +137,15 @@ __global__ void __launch_bounds__(256) dw_fwd_kernel(const DwParams p) {
       for (int v = 0; v < V; ++v) acc[j][v] = 0.f;
 #pragma unroll
     for (int kh = 0; kh < KS; ++kh) {
-      const int ih = ho * S - p.pad + kh;
-      if ((unsigned)ih >= (unsigned)p.H) continue;
-      const bf16_t* row = p.x + (((int64_t)n * p.H + ih) * p.W) * p.C + c0;
       float xin[NCOLS][V];
 #pragma unroll
-      for (int q = 0; q < NCOLS; ++q) {
-        const int iw = iw0 + q;
-        if ((unsigned)iw < (unsigned)p.W) {
-          ld_vec<V>(row + (int64_t)iw * p.C, xin[q]);
-        } else {
+      for (int q = 0; q < NCOLS; ++q) unpack<V>(raw[kh][q], xin[q]);
 #pragma unroll
-          for (int v = 0; v < V; ++v) xin[q][v] = 0.f;
-        }
-      }
-#pragma unroll
-      for (int kw = 0; kw < KS; ++kw) {
-        float wv[V];
-        const float* wp = p.w + (kh * KS + kw) * p.C + c0;
-#pragma unroll
-        for (int v = 0; v < V; ++v) wv[v] = wp[v];
+      for (int kw = 0; kw < KS; ++kw)
 #pragma unroll
         for (int j = 0; j < OWT; ++j)
 #pragma unroll
-          for (int v = 0; v < V; ++v) acc[j][v] += xin[j * S + kw][v] * wv[v];
-      }
+          for (int v = 0; v < V; ++v) acc[j][v] += xin[j * S + kw][v] * wv[kh * KS + kw][v];
     }
     float sc[V], bi[V];
 #pragma unroll
@@ -146,7 +177,9 @@ __global__ void __launch_bounds__(256) dw_fwd_kernel(const DwParams p) {
 
 // dx[n, h, w, c] = sum_{kh, kw} dy[n, (h + p - kh)/s, (w + p - kw)/s, c] * w[kh, kw, c]
 // over taps landing on the stride grid.  p.x = dy, p.y = dx; H/W = input dims.
-template <int V>
+// S = 1: dx[h, w0 + j] = sum dy[h + p - kh, w0 + j + p - kw] * w[kh, kw], the
+// OWT + 2 dy columns of each of the three rows loaded once, all up front.
+template <int V, int S>
 __global__ void __launch_bounds__(256) dw_dgrad_kernel(const DwParams p) {
   const int CG = p.C / V;
   const int WT = (p.W + OWT - 1) / OWT;
@@ -166,6 +199,37 @@ __global__ void __launch_bounds__(256) dw_dgrad_kernel(const DwParams p) {
     for (int j = 0; j < OWT; ++j)
 #pragma unroll
       for (int v = 0; v < V; ++v) acc[j][v] = 0.f;
+    if constexpr (S == 1) {
+      constexpr int NC = OWT + KS - 1;
+      float wv[KS * KS][V];
+#pragma unroll
+      for (int t = 0; t < KS * KS; ++t) ld_w<V>(p.w + t * p.C + c0, wv[t]);
+      const int ow0 = w0 + p.pad - (KS - 1);
+      typename vec<V>::t raw[KS][NC];
+#pragma unroll
+      for (int kh = 0; kh < KS; ++kh) {
+        const int oh = h + p.pad - kh;
+        const bool okr = (unsigned)oh < (unsigned)p.Ho;
+        const bf16_t* row = p.x + (((int64_t)n * p.Ho + (okr ? oh : 0)) * p.Wo) * p.C + c0;
+#pragma unroll
+        for (int q = 0; q < NC; ++q) {
+          const int ow = ow0 + q;
+          raw[kh][q] = ld_raw<V>(row + (int64_t)ow * p.C, okr && (unsigned)ow < (unsigned)p.Wo);
+        }
+      }
+#pragma unroll
+      for (int kh = 0; kh < KS; ++kh) {
+        float d[NC][V];
+#pragma unroll
+        for (int q = 0; q < NC; ++q) unpack<V>(raw[kh][q], d[q]);
+#pragma unroll
+        for (int kw = 0; kw < KS; ++kw)
+#pragma unroll
+          for (int j = 0; j < OWT; ++j)
+#pragma unroll
+            for (int v = 0; v < V; ++v) acc[j][v] += d[j + KS - 1 - kw][v] * wv[kh * KS + kw][v];
+      }
+    } else {
 #pragma unroll
     for (int kh = 0; kh < KS; ++kh) {
       const int t = h + p.pad - kh;
@@ -191,6 +255,7 @@ __global__ void __launch_bounds__(256) dw_dgrad_kernel(const DwParams p) {
           for (int v = 0; v < V; ++v) acc[j][v] += d[v] * wv[v];
         }
       }
+    }
     }
 #pragma unroll
     for (int j = 0; j < OWT; ++j) {
@@ -236,33 +301,30 @@ dw_wgrad_partial_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__
       const int ho = (int)(r % Ho);
       const int n = (int)(r / Ho);
       const int wo0 = wt * OWT;
-      float d[OWT][V];
-#pragma unroll
-      for (int j = 0; j < OWT; ++j) {
-        if (wo0 + j < Wo) {
-          ld_vec<V>(dy + (((int64_t)n * Ho + ho) * Wo + wo0 + j) * C + c0, d[j]);
-        } else {
-#pragma unroll
-          for (int v = 0; v < V; ++v) d[j][v] = 0.f;
-        }
-      }
       const int iw0 = wo0 * S - pad;
+      typename vec<V>::t draw[OWT], raw[KS][NCOLS];
+      const bf16_t* drow = dy + (((int64_t)n * Ho + ho) * Wo + wo0) * C + c0;
+#pragma unroll
+      for (int j = 0; j < OWT; ++j) draw[j] = ld_raw<V>(drow + (int64_t)j * C, wo0 + j < Wo);
 #pragma unroll
       for (int kh = 0; kh < KS; ++kh) {
         const int ih = ho * S - pad + kh;
-        if ((unsigned)ih >= (unsigned)H) continue;
-        const bf16_t* row = x + (((int64_t)n * H + ih) * W) * C + c0;
-        float xin[NCOLS][V];
+        const bool okr = (unsigned)ih < (unsigned)H;
+        const bf16_t* row = x + (((int64_t)n * H + (okr ? ih : 0)) * W) * C + c0;
 #pragma unroll
         for (int q = 0; q < NCOLS; ++q) {
           const int iw = iw0 + q;
-          if ((unsigned)iw < (unsigned)W) {
-            ld_vec<V>(row + (int64_t)iw * C, xin[q]);
-          } else {
-#pragma unroll
-            for (int v = 0; v < V; ++v) xin[q][v] = 0.f;
-          }
+          raw[kh][q] = ld_raw<V>(row + (int64_t)iw * C, okr && (unsigned)iw < (unsigned)W);
         }
+      }
+      float d[OWT][V];
+#pragma unroll
+      for (int j = 0; j < OWT; ++j) unpack<V>(draw[j], d[j]);
+#pragma unroll
+      for (int kh = 0; kh < KS; ++kh) {
+        float xin[NCOLS][V];
+#pragma unroll
+        for (int q = 0; q < NCOLS; ++q) unpack<V>(raw[kh][q], xin[q]);
 #pragma unroll
         for (int kw = 0; kw < KS; ++kw)
 #pragma unroll
@@ -406,8 +468,12 @@ MDA_API int mda_dw_dgrad(const void* dy, const float* w, void* dx, int64_t N, in
   const int V = vwidth((int)C);
   const int64_t work = N * H * ((W + OWT - 1) / OWT) * (C / V);
   const dim3 g(grid_for(work));
-#define DW_DG(VV) hipLaunchKernelGGL(dw_dgrad_kernel<VV>, g, dim3(256), 0, st, p)
-  if (V == 8) DW_DG(8); else if (V == 4) DW_DG(4); else if (V == 2) DW_DG(2); else DW_DG(1);
+#define DW_DG(VV, SS) hipLaunchKernelGGL((dw_dgrad_kernel<VV, SS>), g, dim3(256), 0, st, p)
+  if (stride == 1) {
+    if (V == 8) DW_DG(8, 1); else if (V == 4) DW_DG(4, 1); else if (V == 2) DW_DG(2, 1); else DW_DG(1, 1);
+  } else {
+    if (V == 8) DW_DG(8, 2); else if (V == 4) DW_DG(4, 2); else if (V == 2) DW_DG(2, 2); else DW_DG(1, 2);
+  }
 #undef DW_DG
   MDA_CHECK_LAUNCH();
 }

@@ -109,13 +109,24 @@ class PackCache:
         self.entries[id(weight)] = dict(weight=weight, wf=wf, wt=wt, meta=(Cout, Cin, KH, KW, Kp, KpT))
         self._dirty = True
 
+    def register_dw(self, weight, wp):
+        """Depthwise weight: fp32 tap-major [9, C] operand, refreshed by the same launch."""
+        if torch.cuda.is_current_stream_capturing():
+            return
+        C = weight.shape[0]
+        self.entries[id(weight)] = dict(weight=weight, wf=wp, wt=None, meta=(C, -1, 3, 3, 0, 0))
+        self._dirty = True
+
     def _build(self, device):
         rows, start = [], 0
         for e in self.entries.values():
             Cout, Cin, KH, KW, Kp, KpT = e["meta"]
-            t = ctypes.c_int64(0)
-            _ext.call("mda_pack_tiles", Cout, Cin, KH, KW, t)
-            n = t.value  # tiles of this layer (padding stays zero from registration)
+            if Cin < 0:  # depthwise row: 256 packed elements per tile
+                n = (9 * Cout + 255) // 256
+            else:
+                t = ctypes.c_int64(0)
+                _ext.call("mda_pack_tiles", Cout, Cin, KH, KW, t)
+                n = t.value  # tiles of this layer (padding stays zero from registration)
             w = e["weight"]
             rows.append([w.data_ptr(), e["wf"].data_ptr(), e["wt"].data_ptr() if e["wt"] is not None else 0,
                          Cout, Cin, KH, KW, Kp, KpT, start])
@@ -423,7 +434,15 @@ def _dw_forward(ctx, x, weight, gamma, beta, residual, stride, pad, act, bn, wan
     N, C, H, W = x.shape
     Ho = (H + 2 * pad - 3) // stride + 1
     Wo = (W + 2 * pad - 3) // stride + 1
-    wp = dw_pack(weight)
+    packs = _ACTIVE[0]
+    ent = packs.lookup(weight, False) if packs is not None else None
+    if ent is not None and ent["meta"][1] < 0:  # packed for this step by PackCache.pack_all
+        wp = ent["wf"]
+    else:
+        wp = dw_pack(weight)
+        wc = weight.detach()
+        if packs is not None and wc.is_contiguous() and wc.dtype == torch.float32:
+            packs.register_dw(weight, wp)
     y = torch.empty((N, C, Ho, Wo), dtype=torch.bfloat16, device=x.device,
                     memory_format=torch.channels_last)
     _ext.call("mda_dw_fwd", x, wp, None, None, None, y, None, N, H, W, C, Ho, Wo, 3, 3, stride,

@@ -126,9 +126,11 @@ def test_student_train_step_uses_native_path(name):
     assert e_native < max(2.0 * e_miopen, 0.05), (e_native, e_miopen)
 
 
-def test_pack_cache_matches_per_layer_packing():
+@pytest.mark.parametrize("student", ["resnet8x4", "MobileNetV2"])
+def test_pack_cache_matches_per_layer_packing(student):
     """TrainStep with the one-launch PackCache == per-layer packing, over a few
-    steps (the packed weights must track every optimizer update)."""
+    steps (the packed weights must track every optimizer update; MobileNetV2's
+    depthwise weights ride in the same launch)."""
     from mdistiller_ddp_amd.config import get_cfg
     from mdistiller_ddp_amd.engine.build import build_distiller
     from mdistiller_ddp_amd.engine.step import TrainStep
@@ -136,7 +138,7 @@ def test_pack_cache_matches_per_layer_packing():
     cfg = get_cfg()
     cfg.DISTILLER.TYPE = "KD"
     cfg.DISTILLER.TEACHER = "resnet32x4"
-    cfg.DISTILLER.STUDENT = "resnet8x4"
+    cfg.DISTILLER.STUDENT = student
     cfg.DISTILLER.RANDOM_TEACHER = True
     torch.manual_seed(0)
     d1 = build_distiller(cfg, 100, "cuda")
@@ -154,8 +156,19 @@ def test_pack_cache_matches_per_layer_packing():
         torch.cuda.synchronize()
         if use_cache:
             assert st._packs.entries and st._packs._table is not None
+            if student == "MobileNetV2":
+                assert any(e["meta"][1] < 0 for e in st._packs.entries.values())
         out.append(st.flat.data.clone())
-    torch.testing.assert_close(out[0], out[1], rtol=0, atol=0)
+    if student == "resnet8x4":
+        torch.testing.assert_close(out[0], out[1], rtol=0, atol=0)
+    else:
+        # MobileNetV2's 12-channel layers and its classifier run on MIOpen /
+        # hipBLASLt, whose backward kernels are not bitwise reproducible run to
+        # run (one classifier element in 8e5 differed by 2e-5); stale packs
+        # would move every layer
+        diff = (out[0] - out[1]).abs()
+        assert (diff > 0).float().mean().item() < 1e-4, (diff > 0).sum().item()
+        assert diff.max().item() < 1e-3, diff.max().item()
 
 
 @pytest.mark.parametrize("shapes", [
@@ -257,3 +270,25 @@ def test_grouped_conv_bn_act_train(N, Cin, H, Cout, G, with_res):
     assert rel(bn.weight.grad, bn_r.weight.grad) < 5e-2
     if with_res:
         assert rel(r1.grad, r2.grad) < 5e-2
+
+
+def test_pack_multi_depthwise_rows_equal_dw_pack():
+    """Depthwise rows of the multi-layer pack == the per-layer dw pack."""
+    torch.manual_seed(0)
+    cache = hip_train.PackCache()
+    ws, outs = [], []
+    for C in (16, 96, 480, 1024):
+        w = torch.randn(C, 1, 3, 3, device="cuda")
+        wp = torch.full((9, C), 7.0, device="cuda")
+        cache.register_dw(w, wp)
+        ws.append(w)
+        outs.append(wp)
+    w2 = torch.randn(64, 32, 3, 3, device="cuda")  # a dense layer in the same launch
+    wf, wt, Kp, KpT = hip_train.pack_weights(w2, True)
+    cache.register(w2, wf, wt, 64, 32, 3, 3, Kp, KpT)
+    assert cache.pack_all(torch.device("cuda"))
+    torch.cuda.synchronize()
+    for w, wp in zip(ws, outs):
+        assert torch.equal(wp, hip_train.dw_pack(w))
+    wf_r, wt_r, _, _ = hip_train.pack_weights(w2, True)
+    assert torch.equal(wf, wf_r) and torch.equal(wt, wt_r)

@@ -33,6 +33,12 @@ SIGNATURES = {
     "mda_axpby": "ipppppis",
     # feature losses (csrc/feat.hip)
     "mda_at_loss": "iipppppp" + "iiii" + "fs",
+    # relational losses on the batch Gram (csrc/relation.hip)
+    "mda_gram_plan": "ipp",
+    "mda_gram_partial": "ppp" + "i" * 7 + "s",
+    "mda_relation_core": "piiiipps",
+    "mda_rkd_loss": "piiii" + "fff" + "pppppps",
+    "mda_gram_bwd": "ppppiis",
     # convolution (csrc/conv_igemm.hip)
     "mda_conv_fwd": "pppppppp" + "i" * 15 + "s",
     "mda_conv_plan": "iiipp",

@@ -3,8 +3,10 @@
 Formulas follow the reference distillers line by line (cited per function);
 the implementations are written for the device: fp32 math on bf16
 activations, Gram-form kernels instead of materialised B x B x D tensors
-where the algebra allows, and the AT loss as a fused HIP kernel
-(``csrc/feat.hip``) on MI355X.
+where the algebra allows, the AT loss as a fused HIP kernel
+(``csrc/feat.hip``) and SP / PKT / RKD on the batch Gram
+(``csrc/relation.hip``) on MI355X; ``*_ref`` are the PyTorch forms (CPU and
+unsupported shapes).
 """
 from __future__ import annotations
 
@@ -108,6 +110,83 @@ def nst_loss(g_s, g_t):
     return sum(single_stage_nst_loss(f_s, f_t) for f_s, f_t in zip(g_s, g_t))
 
 
+# ------------------------------------------------- native Gram-form relations
+# SP, PKT and RKD on the batch Gram G = F F^T (csrc/relation.hip): one MFMA
+# Gram launch over the features, the B x B algebra and its gradient dL/dG in
+# one (SP/PKT) or two (RKD) launches, and dF = go (dG + dG^T) F in the backward.
+_REL_SP, _REL_PKT, _REL_RKD = 0, 1, 2
+
+
+def _flat_bf16(f):
+    """[B, D] bf16 row-major view of ``f`` in its memory order (see :func:`_flat`)."""
+    n = f.shape[0]
+    if f.dim() == 4 and f.is_contiguous(memory_format=torch.channels_last) and not f.is_contiguous():
+        v = f.permute(0, 2, 3, 1).reshape(n, -1)
+    else:
+        v = f.reshape(n, -1)
+    if v.dtype != torch.bfloat16:
+        v = v.to(torch.bfloat16)
+    return v.contiguous()
+
+
+def _gram_plan(D):
+    import ctypes
+    kc, nc = ctypes.c_int64(0), ctypes.c_int64(0)
+    _ext.call("mda_gram_plan", D, kc, nc)
+    return kc.value, nc.value
+
+
+class _RelationLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, f_s, f_t, mode, squared, eps, dist_w, angle_w):
+        a_s, a_t = _flat_bf16(f_s), _flat_bf16(f_t)
+        B, Ds = a_s.shape
+        Dt = a_t.shape[1]
+        kc_s, nc_s = _gram_plan(Ds)
+        kc_t, nc_t = _gram_plan(Dt)
+        dev = a_s.device
+        part = torch.empty((nc_s + nc_t) * 4096, dtype=torch.float32, device=dev)
+        _ext.call("mda_gram_partial", a_s, a_t, part, B, Ds, Dt, kc_s, kc_t, nc_s, nc_t)
+        loss = torch.empty(1, dtype=torch.float32, device=dev)
+        S = torch.empty(64 * 64, dtype=torch.float32, device=dev)
+        if mode == _REL_RKD:
+            scratch = torch.empty(3 * 4096 + 64, dtype=torch.float32, device=dev)
+            _ext.call("mda_rkd_loss", part, nc_s, nc_t, B, int(bool(squared)), float(eps),
+                      float(dist_w), float(angle_w), scratch[:4096], scratch[4096:8192],
+                      scratch[8192:12288], scratch[12288:], loss, S)
+        else:
+            _ext.call("mda_relation_core", part, nc_s, nc_t, B, mode, loss, S)
+        ctx.save_for_backward(a_s, S)
+        ctx.fshape = (f_s.shape, f_s.dtype, f_s.dim() == 4 and not f_s.is_contiguous()
+                      and f_s.is_contiguous(memory_format=torch.channels_last))
+        return loss if mode == _REL_SP else loss[0]
+
+    @staticmethod
+    def backward(ctx, go):
+        a_s, S = ctx.saved_tensors
+        shape, dtype, cl = ctx.fshape
+        B, D = a_s.shape
+        g = torch.empty(shape, dtype=torch.bfloat16, device=a_s.device,
+                        memory_format=torch.channels_last if cl else torch.contiguous_format)
+        gflat = g.permute(0, 2, 3, 1).reshape(B, -1) if cl else g.reshape(B, -1)
+        _ext.call("mda_gram_bwd", a_s, S, go.float().contiguous(), gflat, B, D)
+        if dtype != torch.bfloat16:
+            g = g.to(dtype)
+        return g, None, None, None, None, None, None
+
+
+def _relation_native_ok(f_s, f_t, min_batch=1) -> bool:
+    if not hip_enabled_for(f_s):
+        return False
+    B = f_s.shape[0]
+    if f_t.shape[0] != B or not (min_batch <= B <= 64):
+        return False
+    if f_s.dtype not in (torch.float32, torch.bfloat16) or f_t.dtype not in (torch.float32, torch.bfloat16):
+        return False
+    ds, dt = f_s[0].numel(), f_t[0].numel()
+    return ds % 8 == 0 and dt % 8 == 0 and ds > 0 and dt > 0
+
+
 # ---------------------------------------------------------------- PKT
 def _flat(f):
     """``f.reshape(N, -1)`` in fp32 up to a fixed column permutation.
@@ -124,6 +203,12 @@ def _flat(f):
 
 def pkt_loss(f_s, f_t, eps=1e-7):
     """`distillers/PKT.py:8-35`."""
+    if eps == 1e-7 and _relation_native_ok(f_s, f_t):
+        return _RelationLoss.apply(f_s, f_t.detach(), _REL_PKT, False, 0.0, 0.0, 0.0)
+    return pkt_loss_ref(f_s, f_t, eps)
+
+
+def pkt_loss_ref(f_s, f_t, eps=1e-7):
     f_s = _flat(f_s)
     f_t = _flat(f_t)
     f_s = f_s / (f_s.pow(2).sum(1, keepdim=True).sqrt() + eps)
@@ -140,6 +225,12 @@ def pkt_loss(f_s, f_t, eps=1e-7):
 # ---------------------------------------------------------------- SP
 def similarity_loss(f_s, f_t):
     """`distillers/SP.py:12-24`."""
+    if _relation_native_ok(f_s, f_t):
+        return _RelationLoss.apply(f_s, f_t.detach(), _REL_SP, False, 0.0, 0.0, 0.0)
+    return similarity_loss_ref(f_s, f_t)
+
+
+def similarity_loss_ref(f_s, f_t):
     bsz = f_s.shape[0]
     f_s = _flat(f_s)
     f_t = _flat(f_t)
@@ -179,6 +270,13 @@ def _positive_mean(x):
 
 def rkd_loss(f_s, f_t, squared=False, eps=1e-12, distance_weight=25, angle_weight=50):
     """`distillers/RKD.py:21-50`."""
+    if _relation_native_ok(f_s, f_t, min_batch=2):
+        return _RelationLoss.apply(f_s, f_t.detach(), _REL_RKD, squared, eps, distance_weight,
+                                   angle_weight)
+    return rkd_loss_ref(f_s, f_t, squared, eps, distance_weight, angle_weight)
+
+
+def rkd_loss_ref(f_s, f_t, squared=False, eps=1e-12, distance_weight=25, angle_weight=50):
     stu = _flat(f_s)
     tea = _flat(f_t)
     with torch.no_grad():

@@ -2,7 +2,7 @@
 # default bench, 200-step bench and a steady-state rocprofv3 kernel summary.
 set -x
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 ; rc=$?; tail -25 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit 1
+timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 ; rc=$?; tail -25 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit 1
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
 tail -2 gpurun_out/smoke.log
 timeout -k 10 300 python bench.py > gpurun_out/bench_default.log 2>&1 || { tail -20 gpurun_out/bench_default.log; exit 1; }

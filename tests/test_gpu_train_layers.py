@@ -140,14 +140,20 @@ def test_pack_cache_matches_per_layer_packing(student):
     cfg.DISTILLER.TEACHER = "resnet32x4"
     cfg.DISTILLER.STUDENT = student
     cfg.DISTILLER.RANDOM_TEACHER = True
+    cfg.SOLVER.LR = 0.005  # a random teacher's KD steps at 0.05 are chaotic (tiny diffs blow up)
     torch.manual_seed(0)
     d1 = build_distiller(cfg, 100, "cuda")
     d2 = copy.deepcopy(d1)
+    init = None
+    det = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
     out = []
     for d, use_cache in ((d1, True), (d2, False)):
         d.train()
         st = TrainStep(d, cfg, "cuda", use_graph=False, dtype=torch.bfloat16)
         st.set_epoch(1.0)
+        if init is None:
+            init = st.flat.data.clone()
         if not use_cache:
             st._packs = hip_train.PackCache()
             st._packs.pack_all = lambda device: False
@@ -159,16 +165,17 @@ def test_pack_cache_matches_per_layer_packing(student):
             if student == "MobileNetV2":
                 assert any(e["meta"][1] < 0 for e in st._packs.entries.values())
         out.append(st.flat.data.clone())
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det
     if student == "resnet8x4":
         torch.testing.assert_close(out[0], out[1], rtol=0, atol=0)
     else:
         # MobileNetV2's 12-channel layers and its classifier run on MIOpen /
-        # hipBLASLt, whose backward kernels are not bitwise reproducible run to
-        # run (one classifier element in 8e5 differed by 2e-5); stale packs
-        # would move every layer
-        diff = (out[0] - out[1]).abs()
-        assert (diff > 0).float().mean().item() < 1e-4, (diff > 0).sum().item()
-        assert diff.max().item() < 1e-3, diff.max().item()
+        # hipBLASLt, which are not guaranteed bitwise reproducible even in
+        # deterministic mode; stale packs would put an error of the order of the
+        # steps' own movement
+        moved = (out[1] - init).norm()
+        rel = ((out[0] - out[1]).norm() / moved).item()
+        assert moved.item() > 0 and rel < 1e-3, rel
 
 
 @pytest.mark.parametrize("shapes", [

@@ -199,6 +199,8 @@ class TrainStep:
         self._reach_ready = False
         self._units = {}
         self._packs = None
+        self._dual = None  # DOT: (fwd, kd-bwd, ce-bwd, opt, upd graphs, side stream, event)
+        self.dot_dual = self.is_dot and bool(cfg.RUNTIME.get("DOT_DUAL_STREAM", True))
 
     def _graph_comm_mode(self, cfg) -> bool:
         """True: the gradient all-reduce is captured inside the step's hipGraph.
@@ -272,6 +274,30 @@ class TrainStep:
         self._reach_ready = True
 
     def _fwd_bwd(self, b: dict, overlap_comm: bool):
+        preds, losses = self._fwd(b)
+        if self.is_dot:
+            self.flat.bind_grads(1)
+            losses["loss_kd"].backward(retain_graph=True)
+            self.flat.bind_grads(0)
+            losses["loss_ce"].backward()
+        else:
+            if overlap_comm:
+                self.reducer.arm()
+            # backward of the loss terms with unit seeds straight into each term
+            # (no sum node, no per-step fill kernels)
+            terms = [v for v in losses.values() if v.requires_grad]
+            if terms:
+                torch.autograd.backward(terms, [self._unit(v) for v in terms])
+        self._post_backward()
+        return preds, losses
+
+    def _post_backward(self):
+        post = getattr(self.distiller, "post_backward", None)
+        if post is not None:
+            post()
+
+    def _fwd(self, b: dict):
+        """Zero the gradients, repack the student's weights, forward + losses."""
         self.flat.zero_grad()
         packs = None
         if self.device.type == "cuda":
@@ -291,24 +317,8 @@ class TrainStep:
                 hip_train.set_active_packs(None)
         if not self.is_dot and not self._reach_ready:
             self._grad_reachability(losses)
-        if self.is_dot:
-            if not self._dot_ready:
-                self._dot_reachability(losses)
-            self.flat.bind_grads(1)
-            losses["loss_kd"].backward(retain_graph=True)
-            self.flat.bind_grads(0)
-            losses["loss_ce"].backward()
-        else:
-            if overlap_comm:
-                self.reducer.arm()
-            # backward of the loss terms with unit seeds straight into each term
-            # (no sum node, no per-step fill kernels)
-            terms = [v for v in losses.values() if v.requires_grad]
-            if terms:
-                torch.autograd.backward(terms, [self._unit(v) for v in terms])
-        post = getattr(self.distiller, "post_backward", None)
-        if post is not None:
-            post()
+        if self.is_dot and not self._dot_ready:
+            self._dot_reachability(losses)
         return preds, losses
 
     def _reduce(self):
@@ -350,6 +360,8 @@ class TrainStep:
             out = self._eager(static)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
+        if self.is_dot and self.dot_dual and not self.graph_comm:
+            return self._capture_dot_dual(static, pool, s, out)
         g1 = torch.cuda.CUDAGraph()
         if self.world <= 1:
             with torch.cuda.graph(g1, pool=pool, stream=s):
@@ -375,6 +387,64 @@ class TrainStep:
         self._static = (static, preds.detach(), {k: v.detach() for k, v in losses.items()})
         return out
 
+    def _capture_dot_dual(self, static, pool, s, out):
+        """DOT: the task (CE) and KD backwards are independent -- both only read
+        the forward's saved tensors and write their own half of the ``[2, n]``
+        gradient buffer -- so they are captured as separate graphs and replayed
+        on two streams, the CE pass overlapping the KD pass (the CIFAR student's
+        backward kernels are small; one pass alone leaves most CUs idle).  The CE
+        graph allocates from its own memory pool and its BN scratch is tagged
+        (``hip_train.set_ws_tag``), so nothing it writes aliases the KD graph.
+        """
+        from ..ops import hip_train
+        g_fwd, g_kd, g_ce, g_opt = (torch.cuda.CUDAGraph() for _ in range(4))
+        with torch.cuda.graph(g_fwd, pool=pool, stream=s):
+            preds, losses = self._fwd(static)
+        with torch.cuda.graph(g_kd, pool=pool, stream=s):
+            self.flat.bind_grads(1)
+            losses["loss_kd"].backward(retain_graph=True)
+        hip_train.set_ws_tag("dot_ce")
+        try:
+            with torch.cuda.stream(s):
+                hip_train._ws(self.device)  # the tagged scratch exists before the capture
+            with torch.cuda.graph(g_ce, pool=torch.cuda.graph_pool_handle(), stream=s):
+                self.flat.bind_grads(0)
+                losses["loss_ce"].backward()
+        finally:
+            hip_train.set_ws_tag(None)
+        if self.world > 1:
+            # split mode: the bucketed all-reduce runs eagerly between the backward
+            # graphs and the optimizer graph
+            with torch.cuda.graph(g_opt, pool=pool, stream=s):
+                self._post_backward()
+            g_upd = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g_upd, pool=pool, stream=s):
+                self._update(preds, static["target"], losses)
+        else:
+            with torch.cuda.graph(g_opt, pool=pool, stream=s):
+                self._post_backward()
+                self._update(preds, static["target"], losses)
+            g_upd = None
+        self._dual = (g_fwd, g_kd, g_ce, g_opt, g_upd, torch.cuda.Stream(), torch.cuda.Event())
+        self._graphs = (None, None)
+        self._static = (static, preds.detach(), {k: v.detach() for k, v in losses.items()})
+        return out
+
+    def _replay_dot_dual(self):
+        g_fwd, g_kd, g_ce, g_opt, g_upd, s2, ev = self._dual
+        cur = torch.cuda.current_stream()
+        g_fwd.replay()
+        ev.record(cur)
+        g_kd.replay()
+        s2.wait_event(ev)
+        with torch.cuda.stream(s2):
+            g_ce.replay()
+        cur.wait_stream(s2)
+        g_opt.replay()
+        if g_upd is not None:
+            self._reduce()
+            g_upd.replay()
+
     def step(self, batch: dict):
         """Run one step; returns device ``(preds, losses)`` (no host sync)."""
         from ..ops.hip_layers import bump_weight_generation
@@ -391,7 +461,7 @@ class TrainStep:
                 import warnings
                 warnings.warn(f"hipGraph capture failed ({e}); continuing without graphs")
                 self.use_graph = False
-                self._graphs = self._static = None
+                self._graphs = self._static = self._dual = None
                 torch.cuda.synchronize()
                 out = self._eager(b)
                 self.steps_done += 1
@@ -406,6 +476,10 @@ class TrainStep:
             return out
         for k, v in b.items():
             static[k].copy_(v, non_blocking=True)
+        if self._dual is not None:
+            self._replay_dot_dual()
+            self.steps_done += 1
+            return preds, losses
         g1, g2 = self._graphs
         g1.replay()
         if g2 is not None:  # split mode: eager all-reduce between the graphs
@@ -418,6 +492,7 @@ class TrainStep:
         """Drop captured graphs (shape change, e.g. the last partial batch)."""
         self._graphs = None
         self._static = None
+        self._dual = None
 
     # ------------------------------------------------------------------
     def state_dict(self) -> dict:

@@ -79,16 +79,34 @@ __global__ void __launch_bounds__(256) gram_partial_kernel(const GramArgs g) {
     for (int i = 0; i < 4; ++i) out[(16 * w + 4 * kq + i) * RB + 16 * c + r] = acc[c][i];
 }
 
-// Both Grams into LDS (fixed-order sum of the chunk partials).
+// Both Grams into LDS (fixed-order sum of the chunk partials, <= 16 chunks).
+// float4 rows and every chunk's load issued together: a thread's loads are
+// independent (one L2 round trip per 4 x 4 elements, not one per chunk).
 __device__ void load_grams(const float* __restrict__ part, int nc0, int nc1, int B, float* Gs,
                            float* Gt) {
-  for (int e = threadIdx.x; e < B * B; e += blockDim.x) {
-    const int i = e / B, j = e - i * B;
-    float s = 0.f, u = 0.f;
-    for (int c = 0; c < nc0; ++c) s += part[(int64_t)c * GG + i * RB + j];
-    for (int c = 0; c < nc1; ++c) u += part[(int64_t)(nc0 + c) * GG + i * RB + j];
-    Gs[i * LDG + j] = s;
-    Gt[i * LDG + j] = u;
+  const int B4 = (B + 3) / 4;
+  for (int e = threadIdx.x; e < B * B4; e += blockDim.x) {
+    const int i = e / B4, j0 = 4 * (e - i * B4);
+    float4 s[16], u[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+      s[c] = c < nc0 ? *(const float4*)(part + (int64_t)c * GG + i * RB + j0) : z;
+      u[c] = c < nc1 ? *(const float4*)(part + (int64_t)(nc0 + c) * GG + i * RB + j0) : z;
+    }
+    float4 a = s[0], b = u[0];
+#pragma unroll
+    for (int c = 1; c < 16; ++c) {
+      a.x += s[c].x; a.y += s[c].y; a.z += s[c].z; a.w += s[c].w;
+      b.x += u[c].x; b.y += u[c].y; b.z += u[c].z; b.w += u[c].w;
+    }
+    const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (j0 + q < B) {
+        Gs[i * LDG + j0 + q] = av[q];
+        Gt[i * LDG + j0 + q] = bv[q];
+      }
   }
 }
 
@@ -343,9 +361,15 @@ rkd_finalize_kernel(const float* __restrict__ part, int nc0, int nc1, int B, int
   }
   ld = block_sum(ld, red);
   gd = block_sum(gd, red);
+  __shared__ float Ps[RB * LDG];
+  for (int e = tid; e < B * B; e += blockDim.x) {  // P into LDS: independent loads
+    const int i = e / B, j = e - i * B;
+    Ps[i * LDG + j] = P[i * RB + j];
+  }
+  __syncthreads();
   if (tid < B) {
     float s = 0.f;
-    for (int j = 0; j < B; ++j) s += P[tid * RB + j];
+    for (int j = 0; j < B; ++j) s += Ps[tid * LDG + j];
     rowP[tid] = s;
   }
   __syncthreads();
@@ -367,7 +391,7 @@ rkd_finalize_kernel(const float* __restrict__ part, int nc0, int nc1, int B, int
   for (int e = tid; e < B * B; e += blockDim.x) {
     const int i = e / B, j = e - i * B;
     // angle: +Q_ij (G_jk term, indices (j,k) -> (i,j)), -2 P_ij (G_ij and G_ik terms)
-    float v = Q[i * RB + j] - 2.f * P[i * RB + j];
+    float v = Q[i * RB + j] - 2.f * Ps[i * LDG + j];
     // distance: -2 dpre_ij on G_ij
     v -= 2.f * dG[i * LDG + j];
     // angle norms r_ij: dr = -2 Rg_ij / r_ij, dD2 = dr / (2 r): -2 dD2 on G_ij
@@ -407,27 +431,36 @@ __global__ void __launch_bounds__(256)
 gram_bwd_kernel(const bf16_t* __restrict__ A, const float* __restrict__ S,
                 const float* __restrict__ go, bf16_t* __restrict__ dA, int B, int64_t D) {
   __shared__ float St[RB * RB];
-  for (int e = threadIdx.x; e < B * B; e += blockDim.x) {
-    const int i = e / B, j = e - i * B;
-    St[j * RB + i] = S[i * RB + j];
+  for (int e = threadIdx.x; e < RB * RB; e += blockDim.x) {
+    const int i = e / RB, j = e - i * RB;
+    St[j * RB + i] = (i < B && j < B) ? S[i * RB + j] : 0.f;
   }
   __syncthreads();
   const int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (d >= D) return;
   const float gs = go[0];
+  // the thread's column: all rows' loads issued at once, parked in LDS
+  __shared__ float Av[RB * 256];
+  {
+    float av[RB];
+#pragma unroll
+    for (int jj = 0; jj < RB; ++jj) av[jj] = (jj < B && d < D) ? bf2f(A[(int64_t)jj * D + d]) : 0.f;
+#pragma unroll
+    for (int jj = 0; jj < RB; ++jj) Av[jj * 256 + threadIdx.x] = av[jj];
+  }
+  if (d >= D) return;
   float acc[RB];
 #pragma unroll
   for (int i = 0; i < RB; ++i) acc[i] = 0.f;
-  for (int j = 0; j < B; ++j) {
-    const float a = bf2f(A[(int64_t)j * D + d]);
-    const float4* srow = (const float4*)(St + j * RB);
+  for (int jj = 0; jj < B; ++jj) {
+    const float a = Av[jj * 256 + threadIdx.x];
+    const float4* srow = (const float4*)(St + jj * RB);
 #pragma unroll
     for (int i4 = 0; i4 < RB / 4; ++i4) {
-      const float4 s = srow[i4];
-      acc[4 * i4] += s.x * a;
-      acc[4 * i4 + 1] += s.y * a;
-      acc[4 * i4 + 2] += s.z * a;
-      acc[4 * i4 + 3] += s.w * a;
+      const float4 sv = srow[i4];
+      acc[4 * i4] += sv.x * a;
+      acc[4 * i4 + 1] += sv.y * a;
+      acc[4 * i4 + 2] += sv.z * a;
+      acc[4 * i4 + 3] += sv.w * a;
     }
   }
 #pragma unroll

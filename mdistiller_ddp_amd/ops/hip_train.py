@@ -41,14 +41,22 @@ class _WS:
 
 
 _WSS: dict = {}
+_WS_TAG = [None]
+
+
+def set_ws_tag(tag) -> None:
+    """Give the BN scratch of the code that follows its own buffers: a graph
+    captured under a tag may be replayed concurrently with one captured on the
+    same stream without it (DOT's task and KD backwards, engine/step.py)."""
+    _WS_TAG[0] = tag
 
 
 def _ws(device):
-    # one scratch buffer PER STREAM: the teacher's train-mode BN (OFD) runs on
-    # the teacher stream concurrently with the student's BN kernels, and a
-    # shared partials buffer raced under hipGraph replay (NaN OFD losses)
+    # one scratch buffer PER STREAM (and tag): the teacher's train-mode BN (OFD)
+    # runs on the teacher stream concurrently with the student's BN kernels,
+    # and a shared partials buffer raced under hipGraph replay (NaN OFD losses)
     dev = torch.device(device)
-    key = (dev.index or 0, torch.cuda.current_stream(dev).cuda_stream)
+    key = (dev.index or 0, torch.cuda.current_stream(dev).cuda_stream, _WS_TAG[0])
     w = _WSS.get(key)
     if w is None:
         w = _WSS[key] = _WS(device)

@@ -201,6 +201,15 @@ class TrainStep:
         self._packs = None
         self._dual = None  # DOT: (fwd, kd-bwd, ce-bwd, opt, upd graphs, side stream, event)
         self.dot_dual = self.is_dot and bool(cfg.RUNTIME.get("DOT_DUAL_STREAM", True))
+        # measured (profiles/r2_wgrad_stream_ab.md): the forked wgrads pay off on ImageNet-sized
+        # students (-4 %) and cost 5-9 % on the CIFAR ones, whose steps are too short for the
+        # extra graph edges; "auto" = on for inputs of >= 128 px
+        ws = cfg.RUNTIME.get("WGRAD_STREAM", "auto")
+        ws = ws.lower() if isinstance(ws, str) else bool(ws)
+        self.wgrad_side = (False if self.device.type != "cuda" else
+                           "auto" if ws == "auto" else ws in (True, "true", "1", "on"))
+        self._wg_auto = False
+        self._wg_stream = None
 
     def _graph_comm_mode(self, cfg) -> bool:
         """True: the gradient all-reduce is captured inside the step's hipGraph.
@@ -275,21 +284,49 @@ class TrainStep:
 
     def _fwd_bwd(self, b: dict, overlap_comm: bool):
         preds, losses = self._fwd(b)
-        if self.is_dot:
-            self.flat.bind_grads(1)
-            losses["loss_kd"].backward(retain_graph=True)
-            self.flat.bind_grads(0)
-            losses["loss_ce"].backward()
-        else:
-            if overlap_comm:
-                self.reducer.arm()
-            # backward of the loss terms with unit seeds straight into each term
-            # (no sum node, no per-step fill kernels)
-            terms = [v for v in losses.values() if v.requires_grad]
-            if terms:
-                torch.autograd.backward(terms, [self._unit(v) for v in terms])
+        armed = self._arm_wgrad_stream()
+        try:
+            if self.is_dot:
+                self.flat.bind_grads(1)
+                losses["loss_kd"].backward(retain_graph=True)
+                self.flat.bind_grads(0)
+                losses["loss_ce"].backward()
+            else:
+                if overlap_comm:
+                    self.reducer.arm()
+                # backward of the loss terms with unit seeds straight into each term
+                # (no sum node, no per-step fill kernels)
+                terms = [v for v in losses.values() if v.requires_grad]
+                if terms:
+                    torch.autograd.backward(terms, [self._unit(v) for v in terms])
+        finally:
+            self._join_wgrad_stream(armed)
         self._post_backward()
         return preds, losses
+
+    def _arm_wgrad_stream(self) -> bool:
+        """While a backward is being captured, fork the native weight-gradient
+        GEMMs onto a side stream (``hip_train.set_wgrad_stream``): the captured
+        DAG then runs them beside the dgrad / BN-backward chain.  Not with the
+        all-reduce captured in the same graph (its bucket hooks assume the
+        gradients are complete on the main stream)."""
+        if not (self.wgrad_side and torch.cuda.is_current_stream_capturing()) or self.graph_comm:
+            return False
+        if self.is_dot and self.dot_dual:
+            return False  # measured: the forks serialise the two concurrently replayed passes
+        if self.wgrad_side == "auto" and not self._wg_auto:
+            return False
+        from ..ops import hip_train
+        if self._wg_stream is None:
+            self._wg_stream = torch.cuda.Stream(device=self.device)
+        hip_train.set_wgrad_stream(self._wg_stream)
+        return True
+
+    def _join_wgrad_stream(self, armed: bool) -> None:
+        if armed:
+            from ..ops import hip_train
+            hip_train.join_wgrad_stream()
+            hip_train.set_wgrad_stream(None)
 
     def _post_backward(self):
         post = getattr(self.distiller, "post_backward", None)
@@ -351,6 +388,8 @@ class TrainStep:
         eagerly on the capture stream.
         """
         static = {k: v.clone() for k, v in b.items()}
+        img = static.get("image")
+        self._wg_auto = img is not None and img.dim() == 4 and min(img.shape[-2:]) >= 128
         pool = torch.cuda.graph_pool_handle()
         s = self._cap_stream = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
@@ -402,21 +441,32 @@ class TrainStep:
             preds, losses = self._fwd(static)
         with torch.cuda.graph(g_kd, pool=pool, stream=s):
             self.flat.bind_grads(1)
-            losses["loss_kd"].backward(retain_graph=True)
+            armed = self._arm_wgrad_stream()
+            try:
+                losses["loss_kd"].backward(retain_graph=True)
+            finally:
+                self._join_wgrad_stream(armed)
         hip_train.set_ws_tag("dot_ce")
         try:
             with torch.cuda.stream(s):
                 hip_train._ws(self.device)  # the tagged scratch exists before the capture
             with torch.cuda.graph(g_ce, pool=torch.cuda.graph_pool_handle(), stream=s):
                 self.flat.bind_grads(0)
-                losses["loss_ce"].backward()
+                armed = self._arm_wgrad_stream()
+                try:
+                    losses["loss_ce"].backward()
+                finally:
+                    self._join_wgrad_stream(armed)
         finally:
             hip_train.set_ws_tag(None)
         if self.world > 1:
             # split mode: the bucketed all-reduce runs eagerly between the backward
-            # graphs and the optimizer graph
-            with torch.cuda.graph(g_opt, pool=pool, stream=s):
-                self._post_backward()
+            # graphs (+ the post-backward hook, if any) and the optimizer graph
+            if getattr(self.distiller, "post_backward", None) is not None:
+                with torch.cuda.graph(g_opt, pool=pool, stream=s):
+                    self._post_backward()
+            else:
+                g_opt = None
             g_upd = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g_upd, pool=pool, stream=s):
                 self._update(preds, static["target"], losses)
@@ -440,7 +490,8 @@ class TrainStep:
         with torch.cuda.stream(s2):
             g_ce.replay()
         cur.wait_stream(s2)
-        g_opt.replay()
+        if g_opt is not None:
+            g_opt.replay()
         if g_upd is not None:
             self._reduce()
             g_upd.replay()

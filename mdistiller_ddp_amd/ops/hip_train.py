@@ -63,6 +63,44 @@ def _ws(device):
     return w
 
 
+_WG_SIDE = [None]
+
+
+def set_wgrad_stream(stream) -> None:
+    """Arm (a stream) or disarm (None) the weight-gradient side stream.
+
+    While armed, every native backward launches its weight-gradient GEMM and
+    split reduction on ``stream``, forked from the current stream once dy is
+    ready: the dgrad / BN-backward chain that carries the backward forward no
+    longer waits for them, and they fill the CUs the chain leaves idle.  Only
+    for gradients written straight into the flat buffer; the caller joins the
+    side stream (:func:`join_wgrad_stream`) before anything reads the grads.
+    """
+    _WG_SIDE[0] = stream
+
+
+def join_wgrad_stream() -> None:
+    s = _WG_SIDE[0]
+    if s is not None:
+        torch.cuda.current_stream().wait_stream(s)
+
+
+def _wgrad_launch(fn, direct, *tensors):
+    """Run ``fn`` (a wgrad launch sequence) on the armed side stream when its
+    result goes straight into the flat gradient; inputs are recorded as used
+    there so the allocator does not hand their memory out early."""
+    s = _WG_SIDE[0]
+    if s is None or not direct:
+        fn()
+        return
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn()
+    for t in tensors:
+        if t is not None:
+            t.record_stream(s)
+
+
 def _bn_bwd_reduce(dout, dpre, y, res, stats, M, C, act, ws, sums, dg, db):
     """dbeta / dgamma sums of the BN backward: per-block partials combined by a
     separate channel-parallel finalize launch (the in-kernel last-arriver
@@ -385,11 +423,15 @@ class _ConvBNActTrain(torch.autograd.Function):
         dw = None
         if ctx.needs_input_grad[1]:
             sp = _wgrad_splits(M, Cout, Cin, KH, KW, Kp)
-            part = torch.empty(sp * Cout * Kp, dtype=torch.float32, device=dev)
             direct_w = weight.grad is not None and weight.grad.is_contiguous()
             target = weight.grad if direct_w else torch.empty_like(weight, memory_format=torch.contiguous_format)
-            _ext.call("mda_conv_wgrad", x, dy, part, target, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
-                      stride, pad, Kp, sp, 1.0, 1 if direct_w else 0, ctx.cin_keep, ctx.groups)
+
+            def wg():
+                part = torch.empty(sp * Cout * Kp, dtype=torch.float32, device=dev)
+                _ext.call("mda_conv_wgrad", x, dy, part, target, N, H, W, Cin, Ho, Wo, Cout, KH,
+                          KW, stride, pad, Kp, sp, 1.0, 1 if direct_w else 0, ctx.cin_keep,
+                          ctx.groups)
+            _wgrad_launch(wg, direct_w, x, dy)
             dw = None if direct_w else target
             if direct_w:
                 notify_grad(weight)
@@ -479,11 +521,14 @@ def _dw_backward(ctx, dout, dpre):
     dw = None
     if ctx.needs_input_grad[1]:
         nblk = _dw_wgrad_blocks(N, Ho, Wo, C)
-        part = torch.empty(nblk * 9 * C, dtype=torch.float32, device=y.device)
         direct_w = weight.grad is not None and weight.grad.is_contiguous()
         target = weight.grad if direct_w else torch.empty_like(weight, memory_format=torch.contiguous_format)
-        _ext.call("mda_dw_wgrad", x, dy, part, target, N, H, W, C, Ho, Wo, 3, 3, stride, pad,
-                  nblk, 1 if direct_w else 0)
+
+        def wg():
+            part = torch.empty(nblk * 9 * C, dtype=torch.float32, device=y.device)
+            _ext.call("mda_dw_wgrad", x, dy, part, target, N, H, W, C, Ho, Wo, 3, 3, stride, pad,
+                      nblk, 1 if direct_w else 0)
+        _wgrad_launch(wg, direct_w, x, dy)
         dw = None if direct_w else target
         if direct_w:
             notify_grad(weight)
@@ -644,11 +689,14 @@ class _ConvTrain(torch.autograd.Function):
         dw = None
         if ctx.needs_input_grad[1]:
             sp = _wgrad_splits(M, Cout, Cin, KH, KW, Kp)
-            part = torch.empty(sp * Cout * Kp, dtype=torch.float32, device=dev)
             direct_w = weight.grad is not None and weight.grad.is_contiguous()
             target = weight.grad if direct_w else torch.empty_like(weight, memory_format=torch.contiguous_format)
-            _ext.call("mda_conv_wgrad", x, dz, part, target, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
-                      stride, pad, Kp, sp, 1.0, 1 if direct_w else 0, ctx.cin_keep, 1)
+
+            def wg():
+                part = torch.empty(sp * Cout * Kp, dtype=torch.float32, device=dev)
+                _ext.call("mda_conv_wgrad", x, dz, part, target, N, H, W, Cin, Ho, Wo, Cout, KH,
+                          KW, stride, pad, Kp, sp, 1.0, 1 if direct_w else 0, ctx.cin_keep, 1)
+            _wgrad_launch(wg, direct_w, x, dz)
             dw = None if direct_w else target
             if direct_w:
                 notify_grad(weight)

@@ -69,7 +69,10 @@ def _worker(rank, world, port, scenario, outdir):
         st.step(b)
     torch.cuda.synchronize()
     out["graph"] = st._graphs is not None
-    out["split"] = st._graphs is not None and st._graphs[1] is not None
+    # split = the optimizer replays as its own graph after the eager all-reduce
+    # (DOT: the dual-stream backward graphs, then the update graph)
+    out["split"] = st._graphs is not None and (
+        st._graphs[1] is not None or (st._dual is not None and st._dual[4] is not None))
     flat = st.flat.data.clone()
     allf = [torch.empty_like(flat) for _ in range(world)]
     dist.all_gather(allf, flat)

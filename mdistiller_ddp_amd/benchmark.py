@@ -5,7 +5,9 @@ Shared by ``bench.py`` (the headline metric) and
 framework's real ``TrainStep``: batch copy into the step's input buffers,
 teacher forward (no grad, own stream), student forward, losses, backward,
 gradient all-reduce (world > 1), optimizer update, BN running-stat updates
-and on-device metrics.  Timing: W untimed warm-up steps, then K steps
+and on-device metrics (with the teacher look-ahead, the teacher forward a step
+runs is that of the next batch -- still one teacher forward of fresh data
+per step).  Timing: W untimed warm-up steps, then K steps
 bracketed by a barrier and a device synchronisation on both sides; the
 slowest rank's time is reported.
 """
@@ -64,14 +66,24 @@ def run(cfg_file: str, per_gpu_batch: int, steps: int, warmup: int, opts=(), use
         if dev.type == "cuda":
             torch.cuda.synchronize()
 
+    # each step is handed the batch of the step after it (what a prefetching data
+    # loader has ready), so the captured step can run that batch's teacher forward
+    # beside this step's student work (TrainStep teacher look-ahead)
+    cur = next(it)
+
+    def advance(b):
+        nb = next(it)
+        step.step(b, next_batch=nb)
+        return nb
+
     for _ in range(warmup):
-        step.step(next(it))
+        cur = advance(cur)
     sync()
     D.barrier()
     sync()
     t0 = time.perf_counter()
     for _ in range(steps):
-        step.step(next(it))
+        cur = advance(cur)
     sync()
     D.barrier()
     sync()

@@ -100,6 +100,9 @@ class Distiller(nn.Module):
         # conv_trainbn_nograd), which is capture-safe -- MIOpen's bf16 train-mode
         # BN replayed from a hipGraph went non-finite run to run (r1 evidence,
         # profiles/r1_ofd_graph_ab.md)
+        feed = self.__dict__.get("_teacher_feed")
+        if feed is not None:  # TrainStep's teacher look-ahead (runtime/streams.py::TeacherFeed)
+            return feed.forward(self.teacher, image)
         return streams.run_teacher_async(self.teacher, image)
 
     def forward_train(self, **kwargs):

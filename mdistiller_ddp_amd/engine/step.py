@@ -206,6 +206,12 @@ class TrainStep:
         # extra graph edges; "auto" = on for inputs of >= 128 px
         ws = cfg.RUNTIME.get("WGRAD_STREAM", "auto")
         ws = ws.lower() if isinstance(ws, str) else bool(ws)
+        la = cfg.RUNTIME.get("TEACHER_LOOKAHEAD", "auto")
+        la = la.lower() if isinstance(la, str) else bool(la)
+        self.lookahead = "auto" if la == "auto" else la in (True, "true", "1", "on")
+        self._pipe = None       # (teacher-only graph, TeacherFeed) when the look-ahead is captured
+        self._static_next = None
+        self._x_for = None      # the image tensor whose teacher outputs the feed holds
         self.wgrad_side = (False if self.device.type != "cuda" else
                            "auto" if ws == "auto" else ws in (True, "true", "1", "on"))
         self._wg_auto = False
@@ -253,6 +259,12 @@ class TrainStep:
                 v = v.to(self.device, non_blocking=True)
             out[k] = v
         return out
+
+    def _prep_image(self, v):
+        v = v.to(self.device, non_blocking=True).float() if v.device != self.device else v
+        if self.channels_last and v.dim() == 4:
+            v = v.contiguous(memory_format=torch.channels_last)
+        return v
 
     def _forward(self, b: dict):
         with _autocast(self.device, self.dtype):
@@ -302,6 +314,9 @@ class TrainStep:
         finally:
             self._join_wgrad_stream(armed)
         self._post_backward()
+        feed = self.distiller.__dict__.get("_teacher_feed")
+        if feed is not None:
+            feed.finish()  # look-ahead: join the next batch's teacher forward
         return preds, losses
 
     def _arm_wgrad_stream(self) -> bool:
@@ -401,6 +416,58 @@ class TrainStep:
         torch.cuda.synchronize()
         if self.is_dot and self.dot_dual and not self.graph_comm:
             return self._capture_dot_dual(static, pool, s, out)
+        feed = None
+        if self._lookahead_on(static) and getattr(self.distiller, "teacher", None) is not None:
+            feed = self._capture_teacher_feed(static, pool, s)
+        try:
+            self._capture_step(static, pool, s)
+        finally:
+            if feed is not None:
+                feed.mode = None  # eager steps (e.g. a partial batch) run the teacher inline
+        return out
+
+    def _lookahead_on(self, static) -> bool:
+        """Measured (profiles/r2_teacher_lookahead_ab.md): the look-ahead takes the
+        CIFAR steps and the logit-only ImageNet pair down 5-30 %; with an ImageNet
+        teacher whose feature maps the student also consumes (ReviewKD R34->R18)
+        both sides already fill the GPU and it costs 6 %: ``auto`` skips that case."""
+        if self.lookahead != "auto":
+            return bool(self.lookahead)
+        img = static.get("image")
+        big = img is not None and img.dim() == 4 and min(img.shape[-2:]) >= 128
+        needs = tuple(getattr(self.distiller, "teacher_needs", ("logits",)))
+        return not (big and needs != ("logits",))
+
+    def _capture_teacher_feed(self, static, pool, s):
+        """Teacher look-ahead (``runtime/streams.py::TeacherFeed``): prime the
+        persistent teacher-output buffers eagerly, capture the teacher-only
+        graph that fills them for a batch that was not prefetched, and leave the
+        feed in pipelined mode for the step capture that follows."""
+        from ..runtime.streams import TeacherFeed
+        needs = tuple(getattr(self.distiller, "teacher_needs", ()))
+        feed = TeacherFeed(logits_only=needs == ("logits",))
+        self._static_next = {"image": static["image"].clone()}
+        feed.next_image = self._static_next["image"]
+        self.distiller._teacher_feed = feed
+        g_teach = torch.cuda.CUDAGraph()
+        try:
+            feed.mode = "teach"
+            with torch.cuda.stream(s), _autocast(self.device, self.dtype):
+                self.distiller.teacher_forward(None)
+            torch.cuda.current_stream().wait_stream(s)
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g_teach, pool=pool, stream=s), _autocast(self.device, self.dtype):
+                self.distiller.teacher_forward(None)
+        except Exception:
+            feed.mode = None
+            self.distiller.__dict__.pop("_teacher_feed", None)
+            raise
+        feed.mode = "pipe"
+        self._pipe = (g_teach, feed)
+        self._x_for = None
+        return feed
+
+    def _capture_step(self, static, pool, s):
         g1 = torch.cuda.CUDAGraph()
         if self.world <= 1:
             with torch.cuda.graph(g1, pool=pool, stream=s):
@@ -424,7 +491,6 @@ class TrainStep:
                 self._update(preds, static["target"], losses)
         self._graphs = (g1, g2)
         self._static = (static, preds.detach(), {k: v.detach() for k, v in losses.items()})
-        return out
 
     def _capture_dot_dual(self, static, pool, s, out):
         """DOT: the task (CE) and KD backwards are independent -- both only read
@@ -496,8 +562,14 @@ class TrainStep:
             self._reduce()
             g_upd.replay()
 
-    def step(self, batch: dict):
-        """Run one step; returns device ``(preds, losses)`` (no host sync)."""
+    def step(self, batch: dict, next_batch: dict = None):
+        """Run one step; returns device ``(preds, losses)`` (no host sync).
+
+        ``next_batch`` (optional): the batch the NEXT call will receive.  With the
+        teacher look-ahead captured, its teacher forward runs during this step
+        (beside the student's forward / backward / update), and the next call
+        finds its teacher outputs ready.
+        """
         from ..ops.hip_layers import bump_weight_generation
         bump_weight_generation()  # parameters / BN stats change: inference packs are stale
         b = self._prep(batch)
@@ -513,6 +585,7 @@ class TrainStep:
                 warnings.warn(f"hipGraph capture failed ({e}); continuing without graphs")
                 self.use_graph = False
                 self._graphs = self._static = self._dual = None
+                self._drop_feed()
                 torch.cuda.synchronize()
                 out = self._eager(b)
                 self.steps_done += 1
@@ -522,6 +595,7 @@ class TrainStep:
         static, preds, losses = self._static
         if any(static[k].shape != v.shape for k, v in b.items()):
             # e.g. the last partial batch of an epoch: run it eagerly
+            self._x_for = None
             out = self._eager(b)
             self.steps_done += 1
             return out
@@ -531,6 +605,18 @@ class TrainStep:
             self._replay_dot_dual()
             self.steps_done += 1
             return preds, losses
+        if self._pipe is not None:
+            g_teach, _ = self._pipe
+            nxt = self._static_next["image"]
+            if self._x_for is None or self._x_for is not batch.get("image"):
+                nxt.copy_(static["image"], non_blocking=True)  # this batch was not prefetched
+                g_teach.replay()
+            if next_batch is not None and next_batch.get("image") is not None \
+                    and tuple(next_batch["image"].shape) == tuple(nxt.shape):
+                nxt.copy_(self._prep_image(next_batch["image"]), non_blocking=True)
+                self._x_for = next_batch["image"]
+            else:
+                self._x_for = None  # the step's teacher prefetch is discarded
         g1, g2 = self._graphs
         g1.replay()
         if g2 is not None:  # split mode: eager all-reduce between the graphs
@@ -544,6 +630,13 @@ class TrainStep:
         self._graphs = None
         self._static = None
         self._dual = None
+        self._drop_feed()
+
+    def _drop_feed(self) -> None:
+        if self._pipe is not None:
+            self._pipe = None
+            self.distiller.__dict__.pop("_teacher_feed", None)
+        self._x_for = None
 
     # ------------------------------------------------------------------
     def state_dict(self) -> dict:

@@ -273,14 +273,20 @@ class BaseTrainer:
         t0 = time.perf_counter()
         lr = cfg.SOLVER.LR
         prof = StepProfiler(cfg, self.log_path, self.device) if epoch == 1 else None
-        for idx, data in enumerate(self.train_loader):
-            if idx >= max_iter:
+        keys = BATCH_KEYS[self.kind]
+        loader_it = iter(self.train_loader)
+        nxt = next(loader_it, None)
+        for idx in range(n_iter):
+            if nxt is None or idx >= max_iter:
                 break
+            batch = _as_batch(nxt, keys)
+            # one batch of look-ahead (the teacher of batch idx+1 runs during step idx)
+            nxt = next(loader_it, None) if idx + 1 < max_iter else None
             lr = adjust_learning_rate(epoch, idx, cfg, n_iter)
             self.step.set_lr(lr)
             if prof is not None:
                 prof.before(idx)
-            self.step.step(_as_batch(data, BATCH_KEYS[self.kind]))
+            self.step.step(batch, next_batch=None if nxt is None else _as_batch(nxt, keys))
             if prof is not None:
                 prof.after(idx)
             self.global_step += 1

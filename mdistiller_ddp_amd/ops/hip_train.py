@@ -226,8 +226,11 @@ def pad_channels8(x):
     version and stream, so a second consumer on the same stream (e.g. two
     stems) reuses it."""
     key = (x._version, torch.cuda.current_stream(x.device).cuda_stream)
+    # never across a graph capture: a hit would leave the pad kernel out of the
+    # graph, whose replays then read the padded copy of the capture-time image
+    capturing = torch.cuda.is_current_stream_capturing()
     cache = getattr(x, "_mda_pad8", None)
-    if cache is not None and cache[0] == key:
+    if cache is not None and cache[0] == key and not capturing:
         return cache[1]
     xc = x.contiguous(memory_format=torch.channels_last)
     if xc.dtype not in (torch.float32, torch.bfloat16):
@@ -237,7 +240,10 @@ def pad_channels8(x):
                     memory_format=torch.channels_last)
     _ext.call("mda_pad_channels", 0 if xc.dtype == torch.float32 else 1, xc, y, N * H * W, C, 8)
     try:
-        x._mda_pad8 = (key, y)
+        if capturing:
+            x.__dict__.pop("_mda_pad8", None)
+        else:
+            x._mda_pad8 = (key, y)
     except Exception:  # noqa: BLE001 -- caching is optional
         pass
     return y

@@ -89,3 +89,80 @@ def run_teacher_async(teacher, image, train_bn: bool = False) -> TeacherOutput:
 def run_teacher(teacher, image, train_bn: bool = False):
     """Synchronous convenience wrapper (joins immediately)."""
     return run_teacher_async(teacher, image, train_bn).get()
+
+
+def _clone_struct(obj):
+    if isinstance(obj, torch.Tensor):
+        return obj.detach().clone(memory_format=torch.preserve_format)
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_clone_struct(o) for o in obj)
+    if isinstance(obj, dict):
+        return {k: _clone_struct(v) for k, v in obj.items()}
+    return obj
+
+
+def _copy_struct(dst, src):
+    if isinstance(dst, torch.Tensor):
+        dst.copy_(src)
+    elif isinstance(dst, (list, tuple)):
+        for d, s_ in zip(dst, src):
+            _copy_struct(d, s_)
+    elif isinstance(dst, dict):
+        for k, d in dst.items():
+            _copy_struct(d, src[k])
+
+
+class TeacherFeed:
+    """Teacher look-ahead: a software pipeline across training steps.
+
+    The teacher is frozen, so its forward for batch t+1 does not depend on the
+    student update of step t.  A captured step (``engine/step.py``) therefore
+    runs the student's forward / backward / update of batch t on the current
+    stream while the teacher forward of batch t+1 runs on the teacher stream,
+    and at the end of the step moves that result into the persistent buffers
+    ``X`` the next step's loss reads.  Every step still runs exactly one
+    teacher forward (of fresh data) and one student step; the critical path
+    becomes max(teacher, student) instead of teacher + student backward.
+
+    Modes: ``None`` -- inline (teacher of the current batch, joined before
+    the loss); ``"teach"`` -- teacher of :attr:`next_image` straight into
+    ``X`` (priming); ``"pipe"`` -- hand out ``X`` and launch the teacher of
+    :attr:`next_image` (joined and copied into ``X`` by :meth:`finish`).
+    ``logits_only`` keeps just the logits (KD-style methods ignore the
+    teacher's features, so those are not copied).
+    """
+
+    def __init__(self, logits_only: bool = False):
+        self.mode = None
+        self.next_image = None
+        self.X = None
+        self.logits_only = logits_only
+        self._pending = None
+
+    def _keep(self, out):
+        if self.logits_only and isinstance(out, (list, tuple)) and len(out) == 2:
+            return (out[0], None)
+        return out
+
+    def forward(self, teacher, image):
+        if self.mode == "teach":
+            out = self._keep(run_teacher_async(teacher, self.next_image).get())
+            if self.X is None:
+                if torch.cuda.is_current_stream_capturing():
+                    raise RuntimeError("TeacherFeed: prime the buffers eagerly before capture")
+                self.X = _clone_struct(out)
+            else:
+                _copy_struct(self.X, out)
+            return TeacherOutput(self.X)
+        if self.mode == "pipe":
+            if self.X is None:
+                raise RuntimeError("TeacherFeed: pipelined step before the buffers were primed")
+            self._pending = run_teacher_async(teacher, self.next_image)
+            return TeacherOutput(self.X)
+        return run_teacher_async(teacher, image)
+
+    def finish(self) -> None:
+        """End of a pipelined step: join the prefetch and move it into ``X``."""
+        if self._pending is not None:
+            _copy_struct(self.X, self._keep(self._pending.get()))
+            self._pending = None

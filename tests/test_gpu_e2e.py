@@ -214,3 +214,43 @@ def test_native_bf16_tracks_fp32_over_300_steps(typ):
     (f_n, l_n), (f_r, l_r) = curves
     assert l_n < 0.8 * f_n and l_r < 0.8 * f_r, curves  # both learn
     assert abs(l_n - l_r) / abs(l_r) < 0.05, curves
+
+
+@pytest.mark.parametrize("typ", ["DKD", "FITNET", "REVIEWKD"])
+def test_teacher_lookahead_matches_inline_teacher(typ):
+    """The captured step with the teacher look-ahead (teacher of batch t+1 beside
+    the student step t, runtime/streams.py::TeacherFeed) trains like the inline
+    teacher: same batches, same teacher outputs, same updates.  The native path
+    is deterministic (DKD: equal to 1e-5); methods with PyTorch / MIOpen layers
+    (FitNet's ConvReg, ReviewKD's ABF) are held to a second inline run's spread."""
+    torch.manual_seed(0)
+    cfg = _cfg(typ)
+    d0 = build_distiller(cfg, 100, "cuda")
+    outs = []
+    det = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    try:
+        for la in (True, False, False):
+            d = copy.deepcopy(d0)
+            c = cfg.clone()
+            c.RUNTIME.TEACHER_LOOKAHEAD = "on" if la else "off"
+            d.train()
+            st = TrainStep(d, c, "cuda", use_graph=True, dtype=torch.bfloat16)
+            torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+            st.set_epoch(30.0)
+            batches = list(SyntheticLoader("cifar100", 64, "cuda", steps_per_epoch=16,
+                                           channels_last=True))
+            for i, b in enumerate(batches):
+                # a gap in the chain (step 9 gets no next batch) re-primes via the teacher-only graph
+                nb = batches[i + 1] if i + 1 < len(batches) and i != 9 else None
+                st.step(b, next_batch=nb)
+            torch.cuda.synchronize()
+            assert (st._pipe is not None) == la
+            outs.append((st.flat.data.clone(), st.meters.summary(reduce=False)))
+    finally:
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det
+    ref = outs[1][0].norm()
+    spread = ((outs[2][0] - outs[1][0]).norm() / ref).item()
+    rel = ((outs[0][0] - outs[1][0]).norm() / ref).item()
+    assert rel <= 10 * spread + 1e-5, (rel, spread)
+    assert abs(outs[0][1]["loss"] - outs[1][1]["loss"]) <= max(
+        1e-4 * abs(outs[1][1]["loss"]), 10 * abs(outs[2][1]["loss"] - outs[1][1]["loss"]))

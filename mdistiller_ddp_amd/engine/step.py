@@ -502,6 +502,15 @@ class TrainStep:
         (``hip_train.set_ws_tag``), so nothing it writes aliases the KD graph.
         """
         from ..ops import hip_train
+        feed = None
+        needs = tuple(getattr(self.distiller, "teacher_needs", ("logits",)))
+        if (self._lookahead_on(static) and needs == ("logits",)
+                and getattr(self.distiller, "teacher", None) is not None):
+            # look-ahead under the dual replay: the forward reads the prefetched
+            # logits, and the NEXT batch's teacher runs inside the CE-backward graph
+            # (beside both backward passes); the KD backward does not read them
+            feed = self._capture_teacher_feed(static, pool, s)
+            feed.mode = "use"
         g_fwd, g_kd, g_ce, g_opt = (torch.cuda.CUDAGraph() for _ in range(4))
         with torch.cuda.graph(g_fwd, pool=pool, stream=s):
             preds, losses = self._fwd(static)
@@ -517,14 +526,21 @@ class TrainStep:
             with torch.cuda.stream(s):
                 hip_train._ws(self.device)  # the tagged scratch exists before the capture
             with torch.cuda.graph(g_ce, pool=torch.cuda.graph_pool_handle(), stream=s):
+                if feed is not None:
+                    with _autocast(self.device, self.dtype):
+                        feed.prefetch(self.distiller.teacher)
                 self.flat.bind_grads(0)
                 armed = self._arm_wgrad_stream()
                 try:
                     losses["loss_ce"].backward()
                 finally:
                     self._join_wgrad_stream(armed)
+                if feed is not None:
+                    feed.finish()
         finally:
             hip_train.set_ws_tag(None)
+            if feed is not None:
+                feed.mode = None
         if self.world > 1:
             # split mode: the bucketed all-reduce runs eagerly between the backward
             # graphs (+ the post-backward hook, if any) and the optimizer graph
@@ -601,10 +617,6 @@ class TrainStep:
             return out
         for k, v in b.items():
             static[k].copy_(v, non_blocking=True)
-        if self._dual is not None:
-            self._replay_dot_dual()
-            self.steps_done += 1
-            return preds, losses
         if self._pipe is not None:
             g_teach, _ = self._pipe
             nxt = self._static_next["image"]
@@ -617,6 +629,10 @@ class TrainStep:
                 self._x_for = next_batch["image"]
             else:
                 self._x_for = None  # the step's teacher prefetch is discarded
+        if self._dual is not None:
+            self._replay_dot_dual()
+            self.steps_done += 1
+            return preds, losses
         g1, g2 = self._graphs
         g1.replay()
         if g2 is not None:  # split mode: eager all-reduce between the graphs

@@ -154,12 +154,18 @@ class TeacherFeed:
             else:
                 _copy_struct(self.X, out)
             return TeacherOutput(self.X)
-        if self.mode == "pipe":
+        if self.mode in ("pipe", "use"):
             if self.X is None:
                 raise RuntimeError("TeacherFeed: pipelined step before the buffers were primed")
-            self._pending = run_teacher_async(teacher, self.next_image)
+            if self.mode == "pipe":
+                self.prefetch(teacher)
             return TeacherOutput(self.X)
         return run_teacher_async(teacher, image)
+
+    def prefetch(self, teacher) -> None:
+        """Launch the teacher forward of :attr:`next_image` on the teacher stream
+        (``"use"`` mode leaves this to the caller, e.g. DOT's CE-backward graph)."""
+        self._pending = run_teacher_async(teacher, self.next_image)
 
     def finish(self) -> None:
         """End of a pipelined step: join the prefetch and move it into ``X``."""

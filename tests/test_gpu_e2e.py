@@ -216,15 +216,16 @@ def test_native_bf16_tracks_fp32_over_300_steps(typ):
     assert abs(l_n - l_r) / abs(l_r) < 0.05, curves
 
 
-@pytest.mark.parametrize("typ", ["DKD", "FITNET", "REVIEWKD"])
-def test_teacher_lookahead_matches_inline_teacher(typ):
+@pytest.mark.parametrize("typ,trainer", [("DKD", "base"), ("FITNET", "base"), ("REVIEWKD", "base"),
+                                         ("KD", "dot")])
+def test_teacher_lookahead_matches_inline_teacher(typ, trainer):
     """The captured step with the teacher look-ahead (teacher of batch t+1 beside
     the student step t, runtime/streams.py::TeacherFeed) trains like the inline
     teacher: same batches, same teacher outputs, same updates.  The native path
     is deterministic (DKD: equal to 1e-5); methods with PyTorch / MIOpen layers
     (FitNet's ConvReg, ReviewKD's ABF) are held to a second inline run's spread."""
     torch.manual_seed(0)
-    cfg = _cfg(typ)
+    cfg = _cfg(typ, trainer)
     d0 = build_distiller(cfg, 100, "cuda")
     outs = []
     det = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
@@ -234,7 +235,7 @@ def test_teacher_lookahead_matches_inline_teacher(typ):
             c = cfg.clone()
             c.RUNTIME.TEACHER_LOOKAHEAD = "on" if la else "off"
             d.train()
-            st = TrainStep(d, c, "cuda", use_graph=True, dtype=torch.bfloat16)
+            st = TrainStep(d, c, "cuda", trainer=trainer, use_graph=True, dtype=torch.bfloat16)
             torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
             st.set_epoch(30.0)
             batches = list(SyntheticLoader("cifar100", 64, "cuda", steps_per_epoch=16,

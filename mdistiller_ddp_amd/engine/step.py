@@ -212,6 +212,7 @@ class TrainStep:
         self._pipe = None       # (teacher-only graph, TeacherFeed) when the look-ahead is captured
         self._static_next = None
         self._x_for = None      # the image tensor whose teacher outputs the feed holds
+        self._la_misses = 0     # consecutive look-ahead steps without a next batch
         self.wgrad_side = (False if self.device.type != "cuda" else
                            "auto" if ws == "auto" else ws in (True, "true", "1", "on"))
         self._wg_auto = False
@@ -627,8 +628,19 @@ class TrainStep:
                     and tuple(next_batch["image"].shape) == tuple(nxt.shape):
                 nxt.copy_(self._prep_image(next_batch["image"]), non_blocking=True)
                 self._x_for = next_batch["image"]
+                self._la_misses = 0
             else:
                 self._x_for = None  # the step's teacher prefetch is discarded
+                self._la_misses += 1
+                if self._la_misses >= 3:
+                    # a caller that never passes next_batch would pay two teacher
+                    # forwards per step: this step eagerly, then recapture without
+                    # the look-ahead
+                    self.lookahead = False
+                    self.invalidate_graph()
+                    out = self._eager(b)
+                    self.steps_done += 1
+                    return out
         if self._dual is not None:
             self._replay_dot_dual()
             self.steps_done += 1

@@ -124,7 +124,7 @@ def main():
             "scaling": args.scaling,
             "vs_baseline": round(r["images_per_s"] / BASELINE_IMG_S, 3),
             "dtype": r["dtype"],
-            "data": "synthetic (CIFAR-100 shape 3x32x32, 100 classes, device-resident), random-init weights",
+            "data": "synthetic (CIFAR-100 shape 3x32x32, 100 classes, device-resident), random-init weights (random teacher classifier rescaled to logit std 4)",
             "config": {
                 "model": "DKD resnet32x4->resnet8x4",
                 "global_batch": r["global_batch"],

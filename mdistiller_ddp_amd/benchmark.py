@@ -18,6 +18,42 @@ import time
 import torch
 
 
+TEACHER_LOGIT_STD = 4.0
+
+
+def _calibrate_random_teacher(distiller, ds, dev) -> None:
+    """Rescale a random-init teacher's classifier to a trained teacher's logit range.
+
+    A random ResNet32x4 in eval mode emits logits with std ~25.  A DKD loss
+    on those (~450) drives some students to inf/NaN on the first step; the
+    ShuffleNetV1 pair does this in the reference's PyTorch formulation on
+    the CPU too.  Scaling the last Linear to logit std TEACHER_LOGIT_STD is
+    still a random teacher of the same architecture.  It keeps every
+    configuration's loss finite and leaves the timed work unchanged.
+    """
+    import torch.nn as nn
+    teacher = getattr(distiller, "teacher", None)
+    if teacher is None:
+        return
+    fc = [m for m in teacher.modules() if isinstance(m, nn.Linear)]
+    if not fc:
+        return
+    from .data.synthetic import SyntheticLoader
+    b = next(iter(SyntheticLoader(ds, 32, dev, steps_per_epoch=1, pool=1, seed=99,
+                                  channels_last=(dev.type == "cuda"))))
+    was = teacher.training
+    teacher.eval()
+    with torch.no_grad():
+        out = teacher(b["image"])
+        logits = out[0] if isinstance(out, (tuple, list)) else out
+        std = float(logits.float().std())
+        if std > 0:
+            fc[-1].weight.mul_(TEACHER_LOGIT_STD / std)
+            if fc[-1].bias is not None:
+                fc[-1].bias.mul_(TEACHER_LOGIT_STD / std)
+    teacher.train(was)
+
+
 def run(cfg_file: str, per_gpu_batch: int, steps: int, warmup: int, opts=(), use_graph=True,
         backend="auto", dtype="bf16", teacher_stream=True, dataset=None, crd_k=None,
         check_replicas=False):
@@ -48,6 +84,7 @@ def run(cfg_file: str, per_gpu_batch: int, steps: int, warmup: int, opts=(), use
     # full state (C2) -- rank-dependent seeding here proves it
     torch.manual_seed(1234 + info.rank)
     distiller = build_distiller(cfg, num_classes=ncls, device=dev, num_data=ntrain)
+    _calibrate_random_teacher(distiller, ds, dev)
     dt = torch.bfloat16 if (dtype == "bf16" and dev.type == "cuda") else torch.float32
     trainer = cfg.SOLVER.TRAINER
     step = TrainStep(distiller, cfg, dev, trainer=trainer, use_graph=use_graph, dtype=dt,

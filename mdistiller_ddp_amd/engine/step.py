@@ -217,6 +217,7 @@ class TrainStep:
                            "auto" if ws == "auto" else ws in (True, "true", "1", "on"))
         self._wg_auto = False
         self._wg_stream = None
+        self.wgrad_defer = self.device.type == "cuda" and bool(cfg.RUNTIME.get("WGRAD_DEFER", True))
 
     def _graph_comm_mode(self, cfg) -> bool:
         """True: the gradient all-reduce is captured inside the step's hipGraph.
@@ -298,6 +299,7 @@ class TrainStep:
     def _fwd_bwd(self, b: dict, overlap_comm: bool):
         preds, losses = self._fwd(b)
         armed = self._arm_wgrad_stream()
+        deferred = (not armed) and self._arm_wgrad_defer()
         try:
             if self.is_dot:
                 self.flat.bind_grads(1)
@@ -313,12 +315,31 @@ class TrainStep:
                 if terms:
                     torch.autograd.backward(terms, [self._unit(v) for v in terms])
         finally:
+            self._flush_wgrad_defer(deferred)
             self._join_wgrad_stream(armed)
         self._post_backward()
         feed = self.distiller.__dict__.get("_teacher_feed")
         if feed is not None:
             feed.finish()  # look-ahead: join the next batch's teacher forward
         return preds, losses
+
+    def _arm_wgrad_defer(self) -> bool:
+        """While a backward is being captured (and the wgrads stay on the main
+        stream), defer every layer's split reduction to one multi-layer launch
+        at the end of the backward (``hip_train.set_wgrad_defer``)."""
+        if not (self.wgrad_defer and torch.cuda.is_current_stream_capturing()) or self.graph_comm:
+            return False
+        from ..ops import hip_train
+        hip_train.set_wgrad_defer(True)
+        return True
+
+    def _flush_wgrad_defer(self, armed: bool) -> None:
+        if armed:
+            from ..ops import hip_train
+            try:
+                hip_train.flush_wgrad_reduces()
+            finally:
+                hip_train.set_wgrad_defer(False)
 
     def _arm_wgrad_stream(self) -> bool:
         """While a backward is being captured, fork the native weight-gradient
@@ -518,9 +539,11 @@ class TrainStep:
         with torch.cuda.graph(g_kd, pool=pool, stream=s):
             self.flat.bind_grads(1)
             armed = self._arm_wgrad_stream()
+            deferred = (not armed) and self._arm_wgrad_defer()
             try:
                 losses["loss_kd"].backward(retain_graph=True)
             finally:
+                self._flush_wgrad_defer(deferred)
                 self._join_wgrad_stream(armed)
         hip_train.set_ws_tag("dot_ce")
         try:
@@ -532,9 +555,11 @@ class TrainStep:
                         feed.prefetch(self.distiller.teacher)
                 self.flat.bind_grads(0)
                 armed = self._arm_wgrad_stream()
+                deferred = (not armed) and self._arm_wgrad_defer()
                 try:
                     losses["loss_ce"].backward()
                 finally:
+                    self._flush_wgrad_defer(deferred)
                     self._join_wgrad_stream(armed)
                 if feed is not None:
                     feed.finish()

@@ -46,6 +46,8 @@ SIGNATURES = {
     "mda_conv_fwd_bnstats": "ppppp" + "i" * 15 + "p" * 8 + "ff" + "ps",
     "mda_conv_dgrad": "pppp" + "i" * 14 + "s",
     "mda_conv_wgrad": "pppp" + "i" * 13 + "fiiis",
+    "mda_conv_wgrad_nored": "pppp" + "i" * 13 + "fiiis",
+    "mda_wgrad_reduce_multi": "pis",
     "mda_pack_conv_weights_grouped": "ppp" + "i" * 7 + "s",
     "mda_pad_channels": "ippiiis",
     # max pooling (csrc/pool.hip)

@@ -433,14 +433,13 @@ conv_wgrad_glds_kernel(const WgParams p) {
 // per thread (14 us per ResNet-18 layer); this one issues ~8.
 constexpr int WGR_COLS = 16, WGR_SLICES = 16;
 
-__global__ void __launch_bounds__(256)
-wgrad_reduce_kernel(const float* __restrict__ partial, float* __restrict__ grad, int splits,
-                    int Cout, int Cin, int KH, int KW, int Kp, float scale, int accumulate,
-                    int cin_keep, int groups) {
+__device__ __forceinline__ void wgrad_reduce_block(
+    int64_t blk, const float* __restrict__ partial, float* __restrict__ grad, int splits, int Cout,
+    int Cin, int KH, int KW, int Kp, float scale, int accumulate, int cin_keep, int groups) {
   __shared__ float4 red[WGR_SLICES][WGR_COLS];
   const int c = threadIdx.x % WGR_COLS, sl = threadIdx.x / WGR_COLS;
   const int64_t total4 = (int64_t)Cout * Kp / 4;
-  const int64_t e4 = (int64_t)blockIdx.x * WGR_COLS + c;
+  const int64_t e4 = blk * WGR_COLS + c;
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
   if (e4 < total4) {
     const float4* src = (const float4*)partial + e4;
@@ -486,6 +485,38 @@ wgrad_reduce_kernel(const float* __restrict__ partial, float* __restrict__ grad,
     const int64_t dst = ((int64_t)co * cin_w + ciw) * KH * KW + tap;
     grad[dst] = (accumulate ? grad[dst] : 0.f) + scale * v[q];
   }
+}
+
+__global__ void __launch_bounds__(256)
+wgrad_reduce_kernel(const float* __restrict__ partial, float* __restrict__ grad, int splits,
+                    int Cout, int Cin, int KH, int KW, int Kp, float scale, int accumulate,
+                    int cin_keep, int groups) {
+  wgrad_reduce_block(blockIdx.x, partial, grad, splits, Cout, Cin, KH, KW, Kp, scale, accumulate,
+                     cin_keep, groups);
+}
+
+// The split reductions of up to WGRM_MAX layers in ONE launch (the deferred
+// reduces of a captured backward: engine/step.py flushes them once the last
+// weight-gradient GEMM is queued).  Layers passed by value; block b belongs to
+// the layer whose [blk0, blk0 + blocks) range holds it.
+constexpr int WGRM_MAX = 16;
+struct WgrLayer {
+  const float* partial;
+  float* grad;
+  int splits, Cout, Cin, KH, KW, Kp, accumulate, cin_keep, groups, blk0;
+  float scale;
+};
+struct WgrTable {
+  WgrLayer l[WGRM_MAX];
+  int n;
+};
+
+__global__ void __launch_bounds__(256) wgrad_reduce_multi_kernel(const WgrTable t) {
+  int i = 0;
+  while (i + 1 < t.n && (int)blockIdx.x >= t.l[i + 1].blk0) ++i;
+  const WgrLayer& L = t.l[i];
+  wgrad_reduce_block(blockIdx.x - L.blk0, L.partial, L.grad, L.splits, L.Cout, L.Cin, L.KH, L.KW,
+                     L.Kp, L.scale, L.accumulate, L.cin_keep, L.groups);
 }
 
 __global__ void __launch_bounds__(256)
@@ -720,11 +751,11 @@ MDA_API int mda_wgrad_plan(int64_t M, int64_t Cout, int64_t Cin, int64_t KH, int
 }
 
 // partial: splits*Cout*Kp floats.  grad: fp32 OIHW, accumulated when accumulate != 0.
-MDA_API int mda_conv_wgrad(const void* x, const void* dy, float* partial, float* grad, int64_t N,
+static int conv_wgrad_impl(const void* x, const void* dy, float* partial, float* grad, int64_t N,
                            int64_t H, int64_t W, int64_t Cin, int64_t Ho, int64_t Wo, int64_t Cout,
                            int64_t KH, int64_t KW, int64_t stride, int64_t pad, int64_t Kp,
                            int64_t splits, float scale, int64_t accumulate, int64_t cin_keep,
-                           int64_t groups, hipStream_t st) {
+                           int64_t groups, hipStream_t st, bool reduce) {
   if (Cout % 8 || Kp % TK) return (int)hipErrorInvalidValue;
   if (cin_keep <= 0 || cin_keep > Cin) cin_keep = Cin;
   if (groups > 1 && (Cin % groups || Cout % groups)) return (int)hipErrorInvalidValue;
@@ -759,13 +790,63 @@ MDA_API int mda_conv_wgrad(const void* x, const void* dy, float* partial, float*
   else
     hipLaunchKernelGGL(conv_wgrad_kernel<WG_SCALAR>, grid, dim3(256), 0, st, p);
   int rc = (int)hipGetLastError();
-  if (rc) return rc;
+  if (rc || !reduce) return rc;
   const int64_t total4 = Cout * Kp / 4;  // Kp % 64 == 0
   const int blocks = (int)((total4 + WGR_COLS - 1) / WGR_COLS);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, partial, grad,
                      (int)splits, (int)Cout, (int)Cin, (int)KH, (int)KW, (int)Kp, scale,
                      (int)accumulate, (int)cin_keep, (int)(groups > 1 ? groups : 1));
   MDA_CHECK_LAUNCH();
+}
+
+MDA_API int mda_conv_wgrad(const void* x, const void* dy, float* partial, float* grad, int64_t N,
+                           int64_t H, int64_t W, int64_t Cin, int64_t Ho, int64_t Wo, int64_t Cout,
+                           int64_t KH, int64_t KW, int64_t stride, int64_t pad, int64_t Kp,
+                           int64_t splits, float scale, int64_t accumulate, int64_t cin_keep,
+                           int64_t groups, hipStream_t st) {
+  return conv_wgrad_impl(x, dy, partial, grad, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
+                         Kp, splits, scale, accumulate, cin_keep, groups, st, true);
+}
+
+// The weight-gradient GEMM only: its split partials stay in `partial` for a
+// later mda_wgrad_reduce_multi (same arguments; grad / scale / accumulate /
+// cin_keep / groups are checked and then belong to that reduce).
+MDA_API int mda_conv_wgrad_nored(const void* x, const void* dy, float* partial, float* grad,
+                                 int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Ho,
+                                 int64_t Wo, int64_t Cout, int64_t KH, int64_t KW, int64_t stride,
+                                 int64_t pad, int64_t Kp, int64_t splits, float scale,
+                                 int64_t accumulate, int64_t cin_keep, int64_t groups,
+                                 hipStream_t st) {
+  return conv_wgrad_impl(x, dy, partial, grad, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
+                         Kp, splits, scale, accumulate, cin_keep, groups, st, false);
+}
+
+// rows: n x 11 int64 {partial, grad, splits, Cout, Cin, KH, KW, Kp, accumulate, cin_keep,
+// groups} (host memory; scale 1).  Launches ceil(n / 16) multi-layer reduce kernels.
+MDA_API int mda_wgrad_reduce_multi(const int64_t* rows, int64_t n, hipStream_t st) {
+  for (int64_t b0 = 0; b0 < n; b0 += WGRM_MAX) {
+    WgrTable t;
+    t.n = (int)((n - b0) < WGRM_MAX ? (n - b0) : WGRM_MAX);
+    int blk = 0;
+    for (int i = 0; i < t.n; ++i) {
+      const int64_t* r = rows + (b0 + i) * 11;
+      WgrLayer& L = t.l[i];
+      L.partial = (const float*)r[0];
+      L.grad = (float*)r[1];
+      L.splits = (int)r[2]; L.Cout = (int)r[3]; L.Cin = (int)r[4]; L.KH = (int)r[5];
+      L.KW = (int)r[6]; L.Kp = (int)r[7]; L.accumulate = (int)r[8];
+      L.cin_keep = (int)((r[9] <= 0 || r[9] > r[4]) ? r[4] : r[9]);
+      L.groups = (int)(r[10] > 1 ? r[10] : 1);
+      L.scale = 1.f;
+      L.blk0 = blk;
+      if (L.Cout % 8 || L.Kp % 64 || L.splits < 1) return (int)hipErrorInvalidValue;
+      blk += (int)(((int64_t)L.Cout * L.Kp / 4 + WGR_COLS - 1) / WGR_COLS);
+    }
+    hipLaunchKernelGGL(wgrad_reduce_multi_kernel, dim3((unsigned)blk), dim3(256), 0, st, t);
+    const int rc = (int)hipGetLastError();
+    if (rc) return rc;
+  }
+  return 0;
 }
 
 namespace {

@@ -85,6 +85,44 @@ def join_wgrad_stream() -> None:
         torch.cuda.current_stream().wait_stream(s)
 
 
+_WG_DEFER = [None]  # rows of deferred split reductions while armed (a list), else None
+_WG_KEEP: list = []  # their partial buffers, alive until the flush has been queued
+
+
+def set_wgrad_defer(on: bool) -> None:
+    """Arm / disarm deferred weight-gradient reductions: while armed, each
+    native conv backward queues only its wgrad GEMM, and
+    :func:`flush_wgrad_reduces` reduces every layer's split partials into the
+    flat gradient in one multi-layer launch (``mda_wgrad_reduce_multi``)
+    instead of one reduce kernel per layer on the backward's critical path."""
+    _WG_DEFER[0] = [] if on else None
+    _WG_KEEP.clear()
+
+
+def flush_wgrad_reduces() -> None:
+    rows = _WG_DEFER[0]
+    if rows:
+        t = torch.tensor(rows, dtype=torch.int64)
+        _ext.call("mda_wgrad_reduce_multi", t, len(rows))
+        rows.clear()
+    _WG_KEEP.clear()
+
+
+def _conv_wgrad(x, dy, target, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, Kp, sp, direct,
+                cin_keep, groups):
+    """Weight gradient of one conv into ``target`` (accumulated when ``direct``)."""
+    part = torch.empty(sp * Cout * Kp, dtype=torch.float32, device=dy.device)
+    if direct and _WG_DEFER[0] is not None:
+        _ext.call("mda_conv_wgrad_nored", x, dy, part, target, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
+                  stride, pad, Kp, sp, 1.0, 1, cin_keep, groups)
+        _WG_DEFER[0].append([part.data_ptr(), target.data_ptr(), sp, Cout, Cin, KH, KW, Kp, 1,
+                             cin_keep, groups])
+        _WG_KEEP.append(part)
+        return
+    _ext.call("mda_conv_wgrad", x, dy, part, target, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride,
+              pad, Kp, sp, 1.0, 1 if direct else 0, cin_keep, groups)
+
+
 def _wgrad_launch(fn, direct, *tensors):
     """Run ``fn`` (a wgrad launch sequence) on the armed side stream when its
     result goes straight into the flat gradient; inputs are recorded as used
@@ -433,10 +471,8 @@ class _ConvBNActTrain(torch.autograd.Function):
             target = weight.grad if direct_w else torch.empty_like(weight, memory_format=torch.contiguous_format)
 
             def wg():
-                part = torch.empty(sp * Cout * Kp, dtype=torch.float32, device=dev)
-                _ext.call("mda_conv_wgrad", x, dy, part, target, N, H, W, Cin, Ho, Wo, Cout, KH,
-                          KW, stride, pad, Kp, sp, 1.0, 1 if direct_w else 0, ctx.cin_keep,
-                          ctx.groups)
+                _conv_wgrad(x, dy, target, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, Kp, sp,
+                            direct_w, ctx.cin_keep, ctx.groups)
             _wgrad_launch(wg, direct_w, x, dy)
             dw = None if direct_w else target
             if direct_w:
@@ -699,9 +735,8 @@ class _ConvTrain(torch.autograd.Function):
             target = weight.grad if direct_w else torch.empty_like(weight, memory_format=torch.contiguous_format)
 
             def wg():
-                part = torch.empty(sp * Cout * Kp, dtype=torch.float32, device=dev)
-                _ext.call("mda_conv_wgrad", x, dz, part, target, N, H, W, Cin, Ho, Wo, Cout, KH,
-                          KW, stride, pad, Kp, sp, 1.0, 1 if direct_w else 0, ctx.cin_keep, 1)
+                _conv_wgrad(x, dz, target, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, Kp, sp,
+                            direct_w, ctx.cin_keep, 1)
             _wgrad_launch(wg, direct_w, x, dz)
             dw = None if direct_w else target
             if direct_w:

@@ -100,7 +100,7 @@ def test_dgrad_wgrad_kernels_exact_inputs(shape):
         assert rel_x < 1e-2, rel_x
 
 
-@pytest.mark.parametrize("name", ["resnet8x4", "wrn_16_2", "vgg8", "MobileNetV2", "ShuffleV2"])
+@pytest.mark.parametrize("name", ["resnet8x4", "wrn_16_2", "vgg8", "MobileNetV2", "ShuffleV1", "ShuffleV2"])
 def test_student_train_step_uses_native_path(name):
     """A full student training forward/backward through the native path vs an
     fp32 PyTorch reference: its gradient error must be in the same band as the

@@ -641,17 +641,22 @@ class TrainStep:
             out = self._eager(b)
             self.steps_done += 1
             return out
-        for k, v in b.items():
-            static[k].copy_(v, non_blocking=True)
+        # the step's input copies in one multi-tensor launch (each separate copy is a
+        # ~5 us kernel ahead of the graph)
+        dst = [static[k] for k in b]
+        src = [b[k] for k in b]
         if self._pipe is not None:
             g_teach, _ = self._pipe
             nxt = self._static_next["image"]
             if self._x_for is None or self._x_for is not batch.get("image"):
+                torch._foreach_copy_(dst, src)
+                dst, src = [], []
                 nxt.copy_(static["image"], non_blocking=True)  # this batch was not prefetched
                 g_teach.replay()
             if next_batch is not None and next_batch.get("image") is not None \
                     and tuple(next_batch["image"].shape) == tuple(nxt.shape):
-                nxt.copy_(self._prep_image(next_batch["image"]), non_blocking=True)
+                dst.append(nxt)
+                src.append(self._prep_image(next_batch["image"]))
                 self._x_for = next_batch["image"]
                 self._la_misses = 0
             else:
@@ -666,6 +671,8 @@ class TrainStep:
                     out = self._eager(b)
                     self.steps_done += 1
                     return out
+        if dst:
+            torch._foreach_copy_(dst, src)
         if self._dual is not None:
             self._replay_dot_dual()
             self.steps_done += 1

@@ -86,7 +86,6 @@ CFG.RUNTIME.DOT_DUAL_STREAM = True   # DOT: replay the task / KD backwards as co
 CFG.RUNTIME.TEACHER_LOOKAHEAD = "auto"  # auto | on | off: captured steps run the teacher of batch t+1
                                         # beside the student step t (auto: off for >= 128 px feature KD)
 CFG.RUNTIME.WGRAD_DEFER = True       # captured backward: all layers' wgrad split reductions in one launch
-CFG.RUNTIME.BATCH_TORCH_GRADS = False # captured backward: PyTorch-path param grads by one multi-tensor copy
 CFG.RUNTIME.WGRAD_STREAM = "auto"    # auto | on | off: captured-backward wgrads on a forked stream (auto: >= 128 px inputs)
 CFG.RUNTIME.FOLD_TEACHER_BN = True   # fold frozen teacher BN into conv weights
 CFG.RUNTIME.PROFILE = False          # torch.profiler trace + hipEvent step times of a window

@@ -218,13 +218,6 @@ class TrainStep:
         self._wg_auto = False
         self._wg_stream = None
         self.wgrad_defer = self.device.type == "cuda" and bool(cfg.RUNTIME.get("WGRAD_DEFER", True))
-        # params whose gradient reaches them through autograd's AccumulateGrad (the
-        # PyTorch-path layers): found in the first eager step; in captured
-        # backwards their grads are collected with one multi-tensor copy
-        self._torch_grad_params = None
-        import os
-        self.batch_torch_grads = (bool(cfg.RUNTIME.get("BATCH_TORCH_GRADS", False))
-                                  or os.environ.get("MDA_BATCH_TORCH_GRADS", "0") == "1")
 
     def _graph_comm_mode(self, cfg) -> bool:
         """True: the gradient all-reduce is captured inside the step's hipGraph.
@@ -307,17 +300,12 @@ class TrainStep:
         preds, losses = self._fwd(b)
         armed = self._arm_wgrad_stream()
         deferred = (not armed) and self._arm_wgrad_defer()
-        hooks = self._detect_torch_grads()
         try:
             if self.is_dot:
                 self.flat.bind_grads(1)
-                batched = self._unbind_torch_grads()
                 losses["loss_kd"].backward(retain_graph=True)
-                self._collect_torch_grads(batched, 1)
                 self.flat.bind_grads(0)
-                batched = self._unbind_torch_grads()
                 losses["loss_ce"].backward()
-                self._collect_torch_grads(batched, 0)
             else:
                 if overlap_comm:
                     self.reducer.arm()
@@ -325,12 +313,8 @@ class TrainStep:
                 # (no sum node, no per-step fill kernels)
                 terms = [v for v in losses.values() if v.requires_grad]
                 if terms:
-                    batched = self._unbind_torch_grads() if not overlap_comm else False
                     torch.autograd.backward(terms, [self._unit(v) for v in terms])
-                    self._collect_torch_grads(batched, 0)
         finally:
-            for h in hooks:
-                h.remove()
             self._flush_wgrad_defer(deferred)
             self._join_wgrad_stream(armed)
         self._post_backward()
@@ -338,57 +322,6 @@ class TrainStep:
         if feed is not None:
             feed.finish()  # look-ahead: join the next batch's teacher forward
         return preds, losses
-
-    def _detect_torch_grads(self):
-        """First backward on the GPU: hooks note which params receive their
-        gradient through AccumulateGrad (native kernels write theirs straight
-        into the flat buffer and return None, so their hooks never fire)."""
-        if self._torch_grad_params is not None or self.device.type != "cuda" \
-                or not self.batch_torch_grads or torch.cuda.is_current_stream_capturing():
-            return []
-        seen = set()
-        self._torch_grad_params = []
-        hooks = []
-        for p in self.flat.params:
-            def hook(t, _seen=seen):
-                _seen.add(id(t))
-            hooks.append(p.register_post_accumulate_grad_hook(hook))
-        self._tg_seen = seen
-        return hooks
-
-    def _unbind_torch_grads(self):
-        """While capturing: leave the PyTorch-path params' ``.grad`` unset, so
-        AccumulateGrad assigns instead of launching one add kernel per param."""
-        if self.device.type != "cuda" or not torch.cuda.is_current_stream_capturing() \
-                or not self._torch_params():
-            return False
-        for p in self._torch_params():
-            p.grad = None
-        return True
-
-    def _torch_params(self):
-        seen = getattr(self, "_tg_seen", None)
-        if seen is not None:  # finalise the first step's detection
-            self._torch_grad_params = [p for p in self.flat.params if id(p) in seen]
-            self._tg_seen = None
-        return self._torch_grad_params or []
-
-    def _collect_torch_grads(self, batched, k: int) -> None:
-        """... and copy them into gradient set ``k`` with one multi-tensor copy."""
-        if not batched:
-            return
-        g = self.flat.grads[k]
-        idx = {id(q): i for i, q in enumerate(self.flat.params)}
-        dst, src = [], []
-        for p in self._torch_params():
-            o = self.flat.offsets[idx[id(p)]]
-            view = g[o:o + p.numel()].view_as(p)
-            if p.grad is not None:
-                dst.append(view)
-                src.append(p.grad)
-            p.grad = view
-        if dst:
-            torch._foreach_copy_(dst, src)
 
     def _arm_wgrad_defer(self) -> bool:
         """While a backward is being captured (and the wgrads stay on the main
@@ -608,9 +541,7 @@ class TrainStep:
             armed = self._arm_wgrad_stream()
             deferred = (not armed) and self._arm_wgrad_defer()
             try:
-                batched = self._unbind_torch_grads()
                 losses["loss_kd"].backward(retain_graph=True)
-                self._collect_torch_grads(batched, 1)
             finally:
                 self._flush_wgrad_defer(deferred)
                 self._join_wgrad_stream(armed)
@@ -626,9 +557,7 @@ class TrainStep:
                 armed = self._arm_wgrad_stream()
                 deferred = (not armed) and self._arm_wgrad_defer()
                 try:
-                    batched = self._unbind_torch_grads()
                     losses["loss_ce"].backward()
-                    self._collect_torch_grads(batched, 0)
                 finally:
                     self._flush_wgrad_defer(deferred)
                     self._join_wgrad_stream(armed)

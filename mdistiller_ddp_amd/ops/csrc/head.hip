@@ -20,8 +20,8 @@ namespace {
 
 // grid (N, ceil(J / 256)).  Phase 1: the block pools image n into LDS -- 8
 // channels per thread with 16-byte loads, pixel groups reduced through LDS.
-// Phase 2: one thread per logit, dot(pooled, W[j]) with 16-byte weight loads
-// (independent loads, no serial cross-lane reductions).
+// Phase 2: one thread per logit, dot(pooled, W[j]) with 16-byte weight loads,
+// 32 of them in flight per round.
 template <typename T>
 __global__ void __launch_bounds__(256)
 pool_fc_fwd_kernel(const T* __restrict__ x, int HW, int C, const float* __restrict__ W,
@@ -42,6 +42,7 @@ pool_fc_fwd_kernel(const T* __restrict__ x, int HW, int C, const float* __restri
 #pragma unroll
     for (int i = 0; i < V; ++i) acc[i] = 0.f;
     if (pg < P) {
+#pragma unroll 8
       for (int p = pg; p < HW; p += P) {
         const uint4 raw = *reinterpret_cast<const uint4*>(xn + (int64_t)p * C + cg * V);
         const T* e = reinterpret_cast<const T*>(&raw);
@@ -76,20 +77,29 @@ pool_fc_fwd_kernel(const T* __restrict__ x, int HW, int C, const float* __restri
   __syncthreads();
   const int j = blockIdx.y * 256 + tid;
   if (j < J) {
+    // thread per logit; 32 weight float4s in flight per round (a C = 256 row is
+    // two L2 round trips), four independent accumulators
     const float* wj = W + (int64_t)j * C;
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
     int c = 0;
     if ((C & 3) == 0) {
+      for (; c + 128 <= C; c += 128) {
+        float4 w4[32];
+#pragma unroll
+        for (int u = 0; u < 32; ++u) w4[u] = *reinterpret_cast<const float4*>(wj + c + 4 * u);
+#pragma unroll
+        for (int u = 0; u < 32; ++u) {
+          const float4 s4 = *reinterpret_cast<const float4*>(sp + c + 4 * u);
+          a[u & 3] += (s4.x * w4[u].x + s4.y * w4[u].y) + (s4.z * w4[u].z + s4.w * w4[u].w);
+        }
+      }
       for (; c < C; c += 4) {
         const float4 w4 = *reinterpret_cast<const float4*>(wj + c);
-        a0 += sp[c] * w4.x;
-        a1 += sp[c + 1] * w4.y;
-        a2 += sp[c + 2] * w4.z;
-        a3 += sp[c + 3] * w4.w;
+        a[0] += (sp[c] * w4.x + sp[c + 1] * w4.y) + (sp[c + 2] * w4.z + sp[c + 3] * w4.w);
       }
     }
-    for (; c < C; ++c) a0 += sp[c] * wj[c];
-    io<T>::st(logits, (int64_t)n * J + j, ((a0 + a1) + (a2 + a3)) + (bias ? bias[j] : 0.f));
+    for (; c < C; ++c) a[0] += sp[c] * wj[c];
+    io<T>::st(logits, (int64_t)n * J + j, ((a[0] + a[1]) + (a[2] + a[3])) + (bias ? bias[j] : 0.f));
   }
 }
 
@@ -107,8 +117,13 @@ pool_fc_bwd_kernel(const T* __restrict__ dl, const T* __restrict__ dpooled,
     __syncthreads();
     if (dW != nullptr) {
       for (int c = threadIdx.x; c < C; c += blockDim.x) {
-        float acc = 0.f;
-        for (int n = 0; n < N; ++n) acc += sh[n] * io<T>::ld(pooled, (int64_t)n * C + c);
+        float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // 8 loads in flight
+        int n = 0;
+        for (; n + 8 <= N; n += 8)
+#pragma unroll
+          for (int u = 0; u < 8; ++u) a[u] += sh[n + u] * io<T>::ld(pooled, (int64_t)(n + u) * C + c);
+        for (; n < N; ++n) a[0] += sh[n] * io<T>::ld(pooled, (int64_t)n * C + c);
+        const float acc = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
         float* o = dW + (int64_t)j * C + c;
         *o = accum ? *o + acc : acc;
       }
@@ -127,8 +142,14 @@ pool_fc_bwd_kernel(const T* __restrict__ dl, const T* __restrict__ dpooled,
   __syncthreads();
   T* dxn = dx + (int64_t)n * HW * C;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float acc = dpooled ? io<T>::ld(dpooled, (int64_t)n * C + c) : 0.f;
-    for (int j = 0; j < J; ++j) acc += sh[j] * W[(int64_t)j * C + c];
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // 8 loads in flight
+    int j = 0;
+    for (; j + 8 <= J; j += 8)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] += sh[j + u] * W[(int64_t)(j + u) * C + c];
+    for (; j < J; ++j) a[0] += sh[j] * W[(int64_t)j * C + c];
+    const float acc = (dpooled ? io<T>::ld(dpooled, (int64_t)n * C + c) : 0.f) +
+                      (((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7])));
     const float v = acc * inv_hw;
     for (int p = 0; p < HW; ++p) io<T>::st(dxn, (int64_t)p * C + c, v);
   }

@@ -2,7 +2,7 @@
 set -x
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_gpu_head.py -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_head.log 2>&1 ; rc=$?; tail -3 gpurun_out/pytest_head.log; [ $rc -eq 0 ] || exit 1
-timeout -k 10 120 python -u scripts/head_microbench.py > gpurun_out/head_mb.log 2>&1 || { tail -20 gpurun_out/head_mb.log; exit 1; }
+PYTHONPATH=. timeout -k 10 120 python -u scripts/head_microbench.py > gpurun_out/head_mb.log 2>&1 || { tail -20 gpurun_out/head_mb.log; exit 1; }
 cat gpurun_out/head_mb.log
 rm -f gpurun_out/throughput.jsonl
 timeout -k 10 900 python -u benchmarks/throughput.py --steps 100 --warmup 20 --out gpurun_out/throughput.jsonl > gpurun_out/throughput.log 2>&1 || { tail -30 gpurun_out/throughput.log; exit 1; }

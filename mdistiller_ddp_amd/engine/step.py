@@ -29,6 +29,7 @@ import contextlib
 import torch
 
 from ..parallel import GradReducer, get_world_size
+from ..runtime.streams import join_branches
 from .optim import FlatParams, FlatDOT, build_optimizer
 
 
@@ -317,6 +318,7 @@ class TrainStep:
         finally:
             self._flush_wgrad_defer(deferred)
             self._join_wgrad_stream(armed)
+            join_branches()
         self._post_backward()
         feed = self.distiller.__dict__.get("_teacher_feed")
         if feed is not None:
@@ -372,17 +374,27 @@ class TrainStep:
 
     def _fwd(self, b: dict):
         """Zero the gradients, repack the student's weights, forward + losses."""
-        self.flat.zero_grad()
         packs = None
+        zero = [self.flat.grads]
         if self.device.type == "cuda":
             from ..ops.backend import hip_enabled_for
             if hip_enabled_for(self.flat.data):
                 from ..ops import hip_train
+                # every training BN of the step gets a one-shot channel-sum region
+                # of the arena; their zeroing shares the gradient-zeroing launch
+                zero.append(hip_train.bn_step_begin(self.device, zero=False))
+                self._bn_arena = True
                 packs = self._packs
                 if packs is None:
                     packs = self._packs = hip_train.PackCache()
-                packs.pack_all(self.device)
-                hip_train.set_active_packs(packs)
+        if len(zero) > 1 and zero[0].dtype == zero[1].dtype:
+            torch._foreach_zero_(zero)
+        else:
+            for t in zero:
+                t.zero_()
+        if packs is not None:
+            packs.pack_all(self.device)
+            hip_train.set_active_packs(packs)
         try:
             preds, losses = self._forward(b)
         finally:
@@ -408,10 +420,16 @@ class TrainStep:
         self.meters.update(preds, target, losses)
 
     # ------------------------------------------------------------------
+    def _bn_end(self):
+        if getattr(self, "_bn_arena", False):
+            from ..ops import hip_train
+            hip_train.bn_step_end(self.device)
+
     def _eager(self, b: dict):
         preds, losses = self._fwd_bwd(b, overlap_comm=True)
         self._reduce()
         self._update(preds, b["target"], losses)
+        self._bn_end()
         # hand out detached outputs: a caller holding autograd-attached outputs
         # of an eager step across the hipGraph capture crashes the capture
         return preds.detach(), {k: v.detach() for k, v in losses.items()}
@@ -511,6 +529,7 @@ class TrainStep:
             g2 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g2, pool=pool, stream=s):
                 self._update(preds, static["target"], losses)
+        self._bn_end()
         self._graphs = (g1, g2)
         self._static = (static, preds.detach(), {k: v.detach() for k, v in losses.items()})
 
@@ -545,6 +564,7 @@ class TrainStep:
             finally:
                 self._flush_wgrad_defer(deferred)
                 self._join_wgrad_stream(armed)
+                join_branches()
         hip_train.set_ws_tag("dot_ce")
         try:
             with torch.cuda.stream(s):
@@ -561,6 +581,7 @@ class TrainStep:
                 finally:
                     self._flush_wgrad_defer(deferred)
                     self._join_wgrad_stream(armed)
+                    join_branches()
                 if feed is not None:
                     feed.finish()
         finally:
@@ -583,6 +604,7 @@ class TrainStep:
                 self._post_backward()
                 self._update(preds, static["target"], losses)
             g_upd = None
+        self._bn_end()
         self._dual = (g_fwd, g_kd, g_ce, g_opt, g_upd, torch.cuda.Stream(), torch.cuda.Event())
         self._graphs = (None, None)
         self._static = (static, preds.detach(), {k: v.detach() for k, v in losses.items()})

@@ -12,7 +12,8 @@ from __future__ import annotations
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ...ops.nn import conv_bn_act, pool_linear
+from ...ops.nn import conv_bn_act, grad_fork, pool_linear
+from ...runtime.streams import run_branch
 from .._base import ModelBase, PreactStage
 
 
@@ -35,12 +36,24 @@ class BasicBlock(nn.Module):
         self.downsample = downsample
         self.stride = stride
 
+    def _shortcut(self, x, fork=None):
+        return conv_bn_act(x, self.downsample[0], self.downsample[1], "none", fork=fork)[0]
+
     def forward(self, x):
-        h, _ = conv_bn_act(x, self.conv1, self.bn1, "relu")
-        res = x if self.downsample is None else conv_bn_act(
-            x, self.downsample[0], self.downsample[1], "none")[0]
+        # x feeds conv1 and the shortcut: their input gradients are summed in
+        # the second one's dgrad epilogue (GradFork), not by an autograd add
+        fork = grad_fork(x)
+        if self.downsample is None:
+            h, _ = conv_bn_act(x, self.conv1, self.bn1, "relu", fork=fork)
+            res = x
+        else:
+            # projection shortcut on the branch stream, beside conv1 (and, in
+            # the backward, beside the main path's dgrad chain)
+            res = run_branch(x, lambda t: self._shortcut(t, fork))
+            h, _ = conv_bn_act(x, self.conv1, self.bn1, "relu", fork=fork)
+            fork = None
         return conv_bn_act(h, self.conv2, self.bn2, "relu", residual=res,
-                           want_preact=self.is_last and self._need_preact)
+                           want_preact=self.is_last and self._need_preact, res_fork=fork)
 
 
 class Bottleneck(nn.Module):
@@ -60,13 +73,17 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
         self.stride = stride
 
+    def _shortcut(self, x, fork=None):
+        return conv_bn_act(x, self.downsample[0], self.downsample[1], "none", fork=fork)[0]
+
     def forward(self, x):
-        h, _ = conv_bn_act(x, self.conv1, self.bn1, "relu")
+        fork = grad_fork(x)
+        res = x if self.downsample is None else run_branch(x, lambda t: self._shortcut(t, fork))
+        h, _ = conv_bn_act(x, self.conv1, self.bn1, "relu", fork=fork)
         h, _ = conv_bn_act(h, self.conv2, self.bn2, "relu")
-        res = x if self.downsample is None else conv_bn_act(
-            x, self.downsample[0], self.downsample[1], "none")[0]
         return conv_bn_act(h, self.conv3, self.bn3, "relu", residual=res,
-                           want_preact=self.is_last and self._need_preact)
+                           want_preact=self.is_last and self._need_preact,
+                           res_fork=fork if self.downsample is None else None)
 
 
 class Stage(nn.Sequential):

@@ -16,7 +16,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ...ops.nn import MaxPool2d, conv_bn_act, pool_linear
+from ...ops.nn import MaxPool2d, conv_bn_act, grad_fork, pool_linear
+from ...runtime.streams import run_branch
 from .._base import ModelBase, PreactStage
 from ..cifar.resnet import Stage
 
@@ -40,15 +41,22 @@ class BasicBlock(nn.Module):
         self.is_last = False
         self._need_preact = True
 
-    def _res(self, x):
+    def _res(self, x, fork=None):
+        """(residual, residual fork): the projection shortcut runs on the
+        branch stream; x's two consumers sum their gradients in the native
+        backward (ops.hip_train.GradFork)."""
         if self.downsample is None:
-            return x
-        return conv_bn_act(x, self.downsample[0], self.downsample[1], "none")[0]
+            return x, fork
+        res = run_branch(x, lambda t: conv_bn_act(t, self.downsample[0], self.downsample[1],
+                                                  "none", fork=fork)[0])
+        return res, None
 
     def forward(self, x):
-        h, _ = conv_bn_act(x, self.conv1, self.bn1, "relu")
-        return conv_bn_act(h, self.conv2, self.bn2, "relu", residual=self._res(x),
-                           want_preact=self.is_last and self._need_preact)
+        fork = grad_fork(x)
+        res, res_fork = self._res(x, fork)
+        h, _ = conv_bn_act(x, self.conv1, self.bn1, "relu", fork=fork)
+        return conv_bn_act(h, self.conv2, self.bn2, "relu", residual=res,
+                           want_preact=self.is_last and self._need_preact, res_fork=res_fork)
 
 
 class Bottleneck(BasicBlock):
@@ -69,10 +77,12 @@ class Bottleneck(BasicBlock):
         self._need_preact = True
 
     def forward(self, x):
-        h, _ = conv_bn_act(x, self.conv1, self.bn1, "relu")
+        fork = grad_fork(x)
+        res, res_fork = self._res(x, fork)
+        h, _ = conv_bn_act(x, self.conv1, self.bn1, "relu", fork=fork)
         h, _ = conv_bn_act(h, self.conv2, self.bn2, "relu")
-        return conv_bn_act(h, self.conv3, self.bn3, "relu", residual=self._res(x),
-                           want_preact=self.is_last and self._need_preact)
+        return conv_bn_act(h, self.conv3, self.bn3, "relu", residual=res,
+                           want_preact=self.is_last and self._need_preact, res_fork=res_fork)
 
 
 class ResNet(nn.Module, ModelBase):

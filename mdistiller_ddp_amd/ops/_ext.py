@@ -45,6 +45,7 @@ SIGNATURES = {
     "mda_conv_set_stamps": "p",
     "mda_conv_fwd_bnstats": "ppppp" + "i" * 15 + "p" * 8 + "ff" + "ps",
     "mda_conv_dgrad": "pppp" + "i" * 14 + "s",
+    "mda_conv_dgrad_res": "ppppp" + "i" * 14 + "s",
     "mda_conv_wgrad": "pppp" + "i" * 13 + "fiiis",
     "mda_conv_wgrad_nored": "pppp" + "i" * 13 + "fiiis",
     "mda_wgrad_reduce_multi": "pis",
@@ -73,6 +74,12 @@ SIGNATURES = {
     "mda_bn_stats2": "piip" + "pppp" + "pppp" + "ffps",
     "mda_bn_bwd_reduce2": "pppppppp" + "iii" + "pppp" + "s",
     "mda_bn_finalize": "piii" + "pppppppp" + "ffps",
+    # fused BN through a per-stream slot (csrc/bn.hip, csrc/bnslot.h)
+    "mda_bn_region_bytes": "ip",
+    "mda_bn_stats_acc": "piips",
+    "mda_bn_apply_fin": "ppii" + "ppppp" + "ff" + "p" + "ppp" + "i" + "s",
+    "mda_bn_bwd_fused": "ppppp" + "p" + "iii" + "pp" + "pp" + "ppp" + "s",
+    "mda_conv_fwd_bnacc": "ppppp" + "i" * 14 + "s",
     # CRD memory (csrc/crd.hip)
     "mda_crd_scores": "ppppiiifs",
     "mda_crd_grad": "ppppppiiifs",

@@ -549,3 +549,458 @@ MDA_API int mda_bn_finalize(const float* partial, int64_t nblk, int64_t M, int64
                      (float*)nullptr, (float*)nullptr);
   MDA_CHECK_LAUNCH();
 }
+
+// ===========================================================================
+// Fused training BN (round 3): channel sums through a one-shot BnRegion
+// (csrc/bnslot.h) instead of partial rows + a finalize launch.
+//
+//   forward   conv (epilogue adds the block's sum y / sum y^2 into the region,
+//             conv_igemm.hip mda_conv_fwd_bnacc)  or  bn_stats_acc_kernel
+//             -> bn_apply_fin_kernel: every block finalizes the channels
+//                from the region in its prologue (block 0 also writes mean /
+//                rstd / scale / shift for the backward and the running stats),
+//                applies z = y*scale + shift (+ res), act, preact.  2 launches
+//   backward  bn_bwd_fused_kernel: dz = (dout + dout2) * act'(z) (+ dpre),
+//             block sums -> region, grid barrier (<= 1 block per CU, resident
+//             by construction), every block reads the totals, block 0
+//             accumulates dgamma / dbeta into the flat gradient, then
+//             dy = scale*(dz - (sum dz + xhat*sum dz*xhat)/M), dres = dz from
+//             the values still in registers (HOLD) or re-read.  1 launch
+//
+// versus 3 forward (conv, finalize, apply) + 3 backward (reduce, finalize,
+// apply) launches per layer before; dout2 folds the gradient add of a
+// residual fork (two consumers of one activation) into the same pass.
+#include "bnslot.h"
+
+namespace {
+
+struct FinArgs {
+  const float* gamma; const float* beta;
+  float* running_mean; float* running_var;
+  float* stats;          // [4][C]: mean, rstd, scale, shift (written by block 0)
+  float momentum, eps;
+  int64_t* nbt;
+};
+
+// Block sums a[8], b[8] of the thread's channel group -> region shard.
+__device__ __forceinline__ void region_block_add(BnRegion* r, float (&a)[8], float (&b)[8], int C,
+                                                 int rpi) {
+  __shared__ float sm[2][256 * 8];
+  const int tid = threadIdx.x;
+  const int C8 = C / 8;
+  const int cg = tid % C8, r0 = tid / C8;
+  if (r0 < rpi) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      sm[0][r0 * C + cg * 8 + k] = a[k];
+      sm[1][r0 * C + cg * 8 + k] = b[k];
+    }
+  }
+  __syncthreads();
+  const int shard = blockIdx.x % slot_shards(C);
+  for (int t = tid; t < 2 * C; t += blockDim.x) {
+    const int q = t / C, c = t - q * C;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    int rr = 0;
+    for (; rr + 4 <= rpi; rr += 4) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] += sm[q][(rr + u) * C + c];
+    }
+    for (; rr < rpi; ++rr) acc[0] += sm[q][rr * C + c];
+    acc_add(region_acc(r, C, shard, q) + c, (double)((acc[0] + acc[1]) + (acc[2] + acc[3])));
+  }
+}
+
+// Channel c's totals over the SH shards (plain loads when the sums come from
+// an earlier launch, device-coherent ones behind an in-kernel barrier): all
+// 2*SH loads of a channel in flight together.
+template <bool COHERENT>
+__device__ __forceinline__ void region_channel(BnRegion* r, int C, int c, double& t0, double& t1) {
+  const int SH = slot_shards(C);
+  double a[SLOT_SHMAX], b[SLOT_SHMAX];
+#pragma unroll
+  for (int k = 0; k < SLOT_SHMAX; ++k) {
+    const double* pa = region_acc(r, C, k, 0) + c;
+    const double* pb = region_acc(r, C, k, 1) + c;
+    a[k] = k < SH ? (COHERENT ? acc_load(pa) : *pa) : 0.0;
+    b[k] = k < SH ? (COHERENT ? acc_load(pb) : *pb) : 0.0;
+  }
+  t0 = 0.0;
+  t1 = 0.0;
+#pragma unroll
+  for (int k = 0; k < SLOT_SHMAX; ++k) { t0 += a[k]; t1 += b[k]; }
+}
+
+// Standalone statistics pass (y already materialised: depthwise convs,
+// split-K convs, pre-activation BN): sums into the region, no finalize.
+__global__ void __launch_bounds__(256)
+bn_stats_acc_kernel(const bf16_t* __restrict__ y, int M, int C, BnRegion* __restrict__ reg) {
+  const int C8 = C / 8;
+  const int rpi = 256 / C8;
+  const int cg = threadIdx.x % C8, r0 = threadIdx.x / C8;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ss[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (r0 < rpi) {
+    MDA_ROW_LOOP({
+      const uint4 v = *(const uint4*)(y + o);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+_Pragma("unroll")
+      for (int k = 0; k < 4; ++k) {
+        const float f0 = __uint_as_float(w[k] << 16), f1 = __uint_as_float(w[k] & 0xffff0000u);
+        s[2 * k] += f0; ss[2 * k] += f0 * f0;
+        s[2 * k + 1] += f1; ss[2 * k + 1] += f1 * f1;
+      }
+    })
+  }
+  region_block_add(reg, s, ss, C, rpi);
+}
+
+// z = y*scale + shift (+ res); out = act(z); preact = z -- with the finalize
+// of the region's sums in the prologue.  Grid stride is a multiple of C/8
+// when C/8 is a power of two (power-of-two grid) so every thread keeps one
+// channel group.
+constexpr int APPLY_V = 4;  // 16-byte vectors per thread, all loads issued before any math
+
+__device__ __forceinline__ void apply8(const uint4& yv, const uint4& rv, bool has_res, const float* sc,
+                                       const float* sh, int act, uint4& out, uint4& z) {
+  const uint32_t yw[4] = {yv.x, yv.y, yv.z, yv.w};
+  const uint32_t rw[4] = {rv.x, rv.y, rv.z, rv.w};
+  uint32_t zo[4], oo[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float v0 = __uint_as_float(yw[k] << 16) * sc[2 * k] + sh[2 * k];
+    float v1 = __uint_as_float(yw[k] & 0xffff0000u) * sc[2 * k + 1] + sh[2 * k + 1];
+    if (has_res) {
+      v0 += __uint_as_float(rw[k] << 16);
+      v1 += __uint_as_float(rw[k] & 0xffff0000u);
+    }
+    zo[k] = pack_bf16x2(v0, v1);
+    oo[k] = pack_bf16x2(act_f(v0, act), act_f(v1, act));
+  }
+  out = make_uint4(oo[0], oo[1], oo[2], oo[3]);
+  z = make_uint4(zo[0], zo[1], zo[2], zo[3]);
+}
+
+// z = y*scale + shift (+ res); out = act(z); preact = z -- with the finalize
+// of the region's sums in the prologue.  The thread's APPLY_V vectors of y
+// (and res) are loaded BEFORE the prologue, so their latency overlaps the
+// region loads; grids past APPLY_V vectors per thread loop.
+__global__ void __launch_bounds__(256)
+bn_apply_fin_kernel(const bf16_t* __restrict__ y, BnRegion* __restrict__ reg, int64_t M, int C,
+                    FinArgs f, const bf16_t* __restrict__ res, bf16_t* __restrict__ out,
+                    bf16_t* __restrict__ preact, int act) {
+  __shared__ float s_scale[SLOT_CMAX], s_shift[SLOT_CMAX];
+  const int64_t total = M * C / 8;
+  const int c8 = C / 8;
+  const int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  uint4 yv[APPLY_V], rv[APPLY_V];
+#pragma unroll
+  for (int k = 0; k < APPLY_V; ++k) {
+    const int64_t i = i0 + k * stride;
+    const int64_t ii = i < total ? i : 0;
+    yv[k] = ((const uint4*)y)[ii];
+    rv[k] = res ? ((const uint4*)res)[ii] : make_uint4(0, 0, 0, 0);
+  }
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    double t0, t1;
+    region_channel<false>(reg, C, c, t0, t1);
+    const double mean = t0 / (double)M;
+    double var = t1 / (double)M - mean * mean;
+    if (var < 0) var = 0;
+    const float rstd = (float)(1.0 / sqrt(var + (double)f.eps));
+    const float g = f.gamma ? f.gamma[c] : 1.f;
+    const float bb = f.beta ? f.beta[c] : 0.f;
+    const float sc = g * rstd;
+    const float sh = bb - (float)mean * sc;
+    s_scale[c] = sc;
+    s_shift[c] = sh;
+    if (blockIdx.x == 0) {
+      f.stats[c] = (float)mean;
+      f.stats[C + c] = rstd;
+      f.stats[2 * C + c] = sc;
+      f.stats[3 * C + c] = sh;
+      if (f.running_mean) {
+        const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
+        f.running_mean[c] = (1.f - f.momentum) * f.running_mean[c] + f.momentum * (float)mean;
+        f.running_var[c] = (1.f - f.momentum) * f.running_var[c] + f.momentum * (float)unbiased;
+      }
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && f.nbt) f.nbt[0] += 1;
+  __syncthreads();
+  float sc[8], sh[8];
+#pragma unroll
+  for (int k = 0; k < APPLY_V; ++k) {
+    const int64_t i = i0 + k * stride;
+    if (i < total) {
+      const int cc = (int)(i % c8) * 8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { sc[e] = s_scale[cc + e]; sh[e] = s_shift[cc + e]; }
+      uint4 o, z;
+      apply8(yv[k], rv[k], res != nullptr, sc, sh, act, o, z);
+      ((uint4*)out)[i] = o;
+      if (preact) ((uint4*)preact)[i] = z;
+    }
+  }
+  for (int64_t i = i0 + APPLY_V * stride; i < total; i += stride) {
+    const int cc = (int)(i % c8) * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { sc[e] = s_scale[cc + e]; sh[e] = s_shift[cc + e]; }
+    const uint4 y1 = ((const uint4*)y)[i];
+    const uint4 r1 = res ? ((const uint4*)res)[i] : make_uint4(0, 0, 0, 0);
+    uint4 o, z;
+    apply8(y1, r1, res != nullptr, sc, sh, act, o, z);
+    ((uint4*)out)[i] = o;
+    if (preact) ((uint4*)preact)[i] = z;
+  }
+}
+
+struct BwdArgs {
+  const bf16_t* dout; const bf16_t* dout2; const bf16_t* dpre;
+  const bf16_t* y; const bf16_t* res;
+  const float* stats;    // [4][C] mean, rstd, scale, shift
+  bf16_t* dy; bf16_t* dres;
+  float* dgamma; float* dbeta; float* sums;   // accumulated / written by block 0 (each may be null)
+  BnRegion* reg;
+  unsigned* err;
+  int M, C, act;
+};
+
+struct Raw8 { uint4 y, d, d2, p, r; };
+
+__device__ __forceinline__ void bwd_load8(const BwdArgs& a, int64_t o, Raw8& v) {
+  v.y = *(const uint4*)(a.y + o);
+  v.d = a.dout ? *(const uint4*)(a.dout + o) : make_uint4(0, 0, 0, 0);
+  v.d2 = a.dout2 ? *(const uint4*)(a.dout2 + o) : make_uint4(0, 0, 0, 0);
+  v.p = a.dpre ? *(const uint4*)(a.dpre + o) : make_uint4(0, 0, 0, 0);
+  v.r = (a.res && a.act != ACT_NONE) ? *(const uint4*)(a.res + o) : make_uint4(0, 0, 0, 0);
+}
+
+// dz of 8 channels (z recomputed from y: no stored mask)
+__device__ __forceinline__ void bwd_dz8(const BwdArgs& a, const Raw8& v, const float* sc,
+                                        const float* sh, float (&dz)[8]) {
+  const uint32_t yw[4] = {v.y.x, v.y.y, v.y.z, v.y.w}, dw[4] = {v.d.x, v.d.y, v.d.z, v.d.w};
+  const uint32_t d2w[4] = {v.d2.x, v.d2.y, v.d2.z, v.d2.w}, pw[4] = {v.p.x, v.p.y, v.p.z, v.p.w};
+  const uint32_t rw[4] = {v.r.x, v.r.y, v.r.z, v.r.w};
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int w = k >> 1;
+    const bool hi = k & 1;
+    auto f = [&](uint32_t u) { return hi ? __uint_as_float(u & 0xffff0000u) : __uint_as_float(u << 16); };
+    float d = f(dw[w]);
+    if (a.dout2) d += f(d2w[w]);
+    if (a.act != ACT_NONE) {
+      float z = f(yw[w]) * sc[k] + sh[k];
+      if (a.res) z += f(rw[w]);
+      d *= act_grad(z, a.act);
+    }
+    if (a.dpre) d += f(pw[w]);
+    dz[k] = d;
+  }
+}
+
+template <int VPT, bool HOLD>
+__global__ void __launch_bounds__(256)
+bn_bwd_fused_kernel(BwdArgs a) {
+  __shared__ float s_m0[SLOT_CMAX], s_m1[SLOT_CMAX];
+  const int C = a.C, M = a.M;
+  const int C8 = C / 8;
+  const int rpi = 256 / C8;
+  const int cg = threadIdx.x % C8, r0 = threadIdx.x / C8;
+  const bool active = r0 < rpi;
+  const int c0 = cg * 8;
+  float sc[8], sh[8], mu[8], rs[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    mu[k] = a.stats[c0 + k]; rs[k] = a.stats[C + c0 + k];
+    sc[k] = a.stats[2 * C + c0 + k]; sh[k] = a.stats[3 * C + c0 + k];
+  }
+  const int rstride = gridDim.x * rpi;
+  float sdz[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sdzx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float hz[HOLD ? VPT : 1][8];
+  uint4 hy[HOLD ? VPT : 1];
+  auto accum = [&](const float (&dz)[8], const uint4& yv) {
+    const uint32_t yw[4] = {yv.x, yv.y, yv.z, yv.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float yf = (e & 1) ? __uint_as_float(yw[e >> 1] & 0xffff0000u) : __uint_as_float(yw[e >> 1] << 16);
+      sdz[e] += dz[e];
+      sdzx[e] += dz[e] * (yf - mu[e]) * rs[e];
+    }
+  };
+  if (HOLD) {
+    // every load of the thread's rows in flight before any math
+    Raw8 raw[HOLD ? VPT : 1];
+#pragma unroll
+    for (int k = 0; k < VPT; ++k) {
+      const int m = blockIdx.x * rpi + r0 + k * rstride;
+      const bool ok = active && m < M;
+      bwd_load8(a, (int64_t)(ok ? m : 0) * C + c0, raw[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < VPT; ++k) {
+      const int m = blockIdx.x * rpi + r0 + k * rstride;
+      hy[k] = raw[k].y;
+      if (active && m < M) {
+        bwd_dz8(a, raw[k], sc, sh, hz[k]);
+        accum(hz[k], hy[k]);
+      }
+    }
+  } else if (active) {
+    int m = blockIdx.x * rpi + r0;
+    for (; m + rstride < M; m += 2 * rstride) {
+      Raw8 v0, v1;
+      bwd_load8(a, (int64_t)m * C + c0, v0);
+      bwd_load8(a, (int64_t)(m + rstride) * C + c0, v1);
+      float dz[8];
+      bwd_dz8(a, v0, sc, sh, dz);
+      accum(dz, v0.y);
+      bwd_dz8(a, v1, sc, sh, dz);
+      accum(dz, v1.y);
+    }
+    if (m < M) {
+      Raw8 v0;
+      bwd_load8(a, (int64_t)m * C + c0, v0);
+      float dz[8];
+      bwd_dz8(a, v0, sc, sh, dz);
+      accum(dz, v0.y);
+    }
+  }
+  region_block_add(a.reg, sdz, sdzx, C, rpi);
+  region_grid_barrier(a.reg, a.err);
+  {
+    const float invM = 1.f / (float)M;
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      double d0, d1;
+      region_channel<true>(a.reg, C, c, d0, d1);
+      const float t0 = (float)d0, t1 = (float)d1;
+      s_m0[c] = t0 * invM;
+      s_m1[c] = t1 * invM;
+      if (blockIdx.x == 0) {
+        if (a.sums) { a.sums[c] = t0; a.sums[C + c] = t1; }
+        if (a.dbeta) a.dbeta[c] += t0;
+        if (a.dgamma) a.dgamma[c] += t1;
+      }
+    }
+  }
+  __syncthreads();
+  float m0[8], m1[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { m0[k] = s_m0[c0 + k]; m1[k] = s_m1[c0 + k]; }
+  auto emit = [&](int m, const float (&dz)[8], const uint4& yv) {
+    const int64_t o = (int64_t)m * C + c0;
+    const uint32_t yw[4] = {yv.x, yv.y, yv.z, yv.w};
+    uint32_t go[4], ro[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      float g[2], r[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int e = 2 * w + h;
+        const float yf = h ? __uint_as_float(yw[w] & 0xffff0000u) : __uint_as_float(yw[w] << 16);
+        const float xhat = (yf - mu[e]) * rs[e];
+        g[h] = sc[e] * (dz[e] - (m0[e] + xhat * m1[e]));
+        r[h] = dz[e];
+      }
+      go[w] = pack_bf16x2(g[0], g[1]);
+      ro[w] = pack_bf16x2(r[0], r[1]);
+    }
+    *(uint4*)(a.dy + o) = make_uint4(go[0], go[1], go[2], go[3]);
+    if (a.dres) *(uint4*)(a.dres + o) = make_uint4(ro[0], ro[1], ro[2], ro[3]);
+  };
+  if (HOLD) {
+#pragma unroll
+    for (int k = 0; k < VPT; ++k) {
+      const int m = blockIdx.x * rpi + r0 + k * rstride;
+      if (active && m < M) emit(m, hz[k], hy[k]);
+    }
+  } else if (active) {
+    for (int m = blockIdx.x * rpi + r0; m < M; m += rstride) {
+      Raw8 v0;
+      bwd_load8(a, (int64_t)m * C + c0, v0);
+      float dz[8];
+      bwd_dz8(a, v0, sc, sh, dz);
+      emit(m, dz, v0.y);
+    }
+  }
+}
+
+int g_num_cus = 0;
+
+int num_cus() {
+  if (g_num_cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+      g_num_cus = n;
+    else
+      g_num_cus = 256;
+  }
+  return g_num_cus;
+}
+
+// power-of-two block count for the apply kernels
+inline int apply_blocks(int64_t n8, int vpt) {
+  const int64_t want = (n8 + 256 * (int64_t)vpt - 1) / (256 * (int64_t)vpt);
+  int64_t b = 1;
+  while (b < want && b < 1024) b <<= 1;
+  return (int)b;
+}
+
+}  // namespace
+
+// Bytes of the (zeroed, 64-byte aligned) region one BN call needs.
+MDA_API int mda_bn_region_bytes(int64_t C, int64_t* out) {
+  if (C <= 0 || C % 8 || C > SLOT_CMAX) return (int)hipErrorInvalidValue;
+  *out = region_bytes((int)C);
+  return 0;
+}
+
+MDA_API int mda_bn_stats_acc(const void* y, int64_t M, int64_t C, void* region, hipStream_t st) {
+  if (C % 8 || C > SLOT_CMAX || M <= 0 || M >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
+  const int nblk = reduce_blocks(M, C, STATS2_VPT, STATS2_MAXB);
+  hipLaunchKernelGGL(bn_stats_acc_kernel, dim3(nblk), dim3(256), 0, st, (const bf16_t*)y, (int)M,
+                     (int)C, (BnRegion*)region);
+  MDA_CHECK_LAUNCH();
+}
+
+MDA_API int mda_bn_apply_fin(const void* y, void* region, int64_t M, int64_t C, const float* gamma,
+                             const float* beta, float* running_mean, float* running_var,
+                             float* stats, float momentum, float eps, int64_t* nbt,
+                             const void* res, void* out, void* preact, int64_t act,
+                             hipStream_t st) {
+  if (C % 8 || C > SLOT_CMAX || M <= 0 || M >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
+  FinArgs f{gamma, beta, running_mean, running_var, stats, momentum, eps, nbt};
+  const int nb = apply_blocks(M * C / 8, APPLY_V);
+  hipLaunchKernelGGL(bn_apply_fin_kernel, dim3(nb), dim3(256), 0, st, (const bf16_t*)y,
+                     (BnRegion*)region, M, (int)C, f, (const bf16_t*)res, (bf16_t*)out,
+                     (bf16_t*)preact, (int)act);
+  MDA_CHECK_LAUNCH();
+}
+
+// Fused BN backward (one launch) on a fresh (zeroed) region.  dout2
+// (optional) is a second gradient of the BN output added to dout (residual
+// fork); sums (optional) receives [sum dz | sum dz*xhat]; dgamma / dbeta
+// (optional) are accumulated; err (optional) is set on a barrier timeout.
+MDA_API int mda_bn_bwd_fused(const void* dout, const void* dout2, const void* dpre, const void* y,
+                             const void* res, const float* stats, int64_t M, int64_t C,
+                             int64_t act, void* region, void* err, void* dy, void* dres,
+                             float* dgamma, float* dbeta, float* sums, hipStream_t st) {
+  if (C % 8 || C > SLOT_CMAX || M <= 0 || M >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
+  BwdArgs a{(const bf16_t*)dout, (const bf16_t*)dout2, (const bf16_t*)dpre, (const bf16_t*)y,
+            (const bf16_t*)res, stats, (bf16_t*)dy, (bf16_t*)dres, dgamma, dbeta, sums,
+            (BnRegion*)region, (unsigned*)err, (int)M, (int)C, (int)act};
+  const int C8 = (int)C / 8;
+  const int rpi = 256 / C8;
+  const int64_t rows_iter = (M + rpi - 1) / rpi;       // block-iterations of work
+  // at most one block per CU: every block of the grid barrier is resident
+  const int maxb = num_cus();
+  const int nb = (int)std::min<int64_t>(rows_iter, maxb);
+  const int64_t per = (rows_iter + nb - 1) / nb;     // row iterations per thread
+  if (per <= 1) hipLaunchKernelGGL((bn_bwd_fused_kernel<1, true>), dim3(nb), dim3(256), 0, st, a);
+  else if (per <= 2) hipLaunchKernelGGL((bn_bwd_fused_kernel<2, true>), dim3(nb), dim3(256), 0, st, a);
+  else if (per <= 4) hipLaunchKernelGGL((bn_bwd_fused_kernel<4, true>), dim3(nb), dim3(256), 0, st, a);
+  else if (per <= 8) hipLaunchKernelGGL((bn_bwd_fused_kernel<8, true>), dim3(nb), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((bn_bwd_fused_kernel<1, false>), dim3(nb), dim3(256), 0, st, a);
+  MDA_CHECK_LAUNCH();
+}

@@ -33,6 +33,7 @@
 // (Cin % 8 == 0: every 16-byte chunk lies inside one tap), SCALAR (any Cin,
 // e.g. the 3-channel stem).
 #include "common.h"
+#include "bnslot.h"
 #include <stdlib.h>
 
 namespace {
@@ -68,6 +69,9 @@ struct ConvParams {
   // (bf16-rounded) output, stats_part[blockIdx.x][2][Cout] (raw output only:
   // no scale/bias/residual/activation, no split-K)
   float* stats_part;
+  // training BN through a one-shot BnRegion (bnslot.h): the block's channel
+  // sums are added into shard blockIdx.x % slot_shards(Cout) of it instead
+  BnRegion* stats_slot;
   // diagnostics: per-block phase timestamps (s_memrealtime, 100 MHz), null in
   // normal runs (mda_conv_set_stamps)
   uint64_t* stamps;
@@ -240,7 +244,8 @@ __device__ __forceinline__ void epi_prefetch(const ConvParams& p, EpiPre<BM, BN,
   const int c8 = tid % E::TPR, rr = tid / E::TPR;
   const int co = n0 + c8 * 8;
   const bool split = par ? p.zsplits > 1 : gridDim.z > 1;
-  e.have = !split && p.stats_part == nullptr && (p.Cout & 7) == 0 && co < p.Cout;
+  e.have = !split && p.stats_part == nullptr && p.stats_slot == nullptr && (p.Cout & 7) == 0 &&
+           co < p.Cout;
   e.have_res = false;
   if (!e.have) return;
   load_scale_bias8(p, co, e.sc, e.bi);
@@ -290,7 +295,7 @@ __device__ __forceinline__ void conv_epilogue_rows(const ConvParams& p, char* sm
   const int zsplit = has_pc ? (int)blockIdx.z % p.zsplits : (int)blockIdx.z;
   const bool split = has_pc ? p.zsplits > 1 : gridDim.z > 1;
   const int mlim = has_pc ? pc.Mc : p.M;
-  if (p.stats_part != nullptr) {
+  if (p.stats_part != nullptr || p.stats_slot != nullptr) {
     // raw bf16 output + BN statistics partials of this block's rows.  No early
     // return before the barrier: threads past Cout just contribute zeros.
     float s1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, s2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -326,8 +331,13 @@ __device__ __forceinline__ void conv_epilogue_rows(const ConvParams& p, char* sm
         a0 += red[(q * RPP + r) * BN + c];
         a1 += red[(q * RPP + r + 1) * BN + c];
       }
-      if (n0 + c < p.Cout)
-        p.stats_part[((int64_t)blockIdx.x * 2 + q) * p.Cout + n0 + c] = a0 + a1;
+      if (n0 + c < p.Cout) {
+        if (p.stats_slot != nullptr)
+          acc_add(region_acc(p.stats_slot, p.Cout, (int)blockIdx.x % slot_shards(p.Cout), q) + n0 + c,
+                  (double)(a0 + a1));
+        else
+          p.stats_part[((int64_t)blockIdx.x * 2 + q) * p.Cout + n0 + c] = a0 + a1;
+      }
     }
     return;
   }
@@ -1731,6 +1741,7 @@ MDA_API int mda_conv_fwd(const void* x, const void* w, const float* scale, const
   p.par = 0;
   p.zsplits = 1;
   p.stats_part = nullptr;
+  p.stats_slot = nullptr;
   p.stamps = g_stamps;
   int mode = (Cin % BK == 0) ? LOAD_FAST : (Cin % 8 == 0 ? LOAD_VEC8 : LOAD_SCALAR);
   return dispatch(p, mode, tile, splits, st, halo_eligible(p) ? 1 : 0);
@@ -1740,14 +1751,32 @@ MDA_API int mda_conv_fwd(const void* x, const void* w, const float* scale, const
 // sum_{kh,kw,co} dy[N, (ih+pad-kh)/s, (iw+pad-kw)/s, co] * w[co, ci, kh, kw].
 // wt: weights packed [Cin][Kp] with k = (kh*KW + kw)*Cout + co (mda_pack_conv_weights).
 // dy: [N, Ho, Wo, Cout]; requires Cout % 8 == 0.
+MDA_API int mda_conv_dgrad_res(const void* dy, const void* wt, void* dx, float* partial,
+                               const void* res, int64_t N, int64_t H, int64_t W, int64_t Cin,
+                               int64_t Ho, int64_t Wo, int64_t Cout, int64_t KH, int64_t KW,
+                               int64_t stride, int64_t pad, int64_t Kp, int64_t tile,
+                               int64_t splits, hipStream_t st);
+
 MDA_API int mda_conv_dgrad(const void* dy, const void* wt, void* dx, float* partial, int64_t N,
                            int64_t H, int64_t W, int64_t Cin, int64_t Ho, int64_t Wo,
                            int64_t Cout, int64_t KH, int64_t KW, int64_t stride, int64_t pad,
                            int64_t Kp, int64_t tile, int64_t splits, hipStream_t st) {
+  return mda_conv_dgrad_res(dy, wt, dx, partial, nullptr, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
+                            stride, pad, Kp, tile, splits, st);
+}
+
+// dx = dgrad(dy) (+ res): the residual-add epilogue sums the gradient another
+// consumer of the same activation produced (a residual fork), so autograd
+// never launches that add.  res: [N, H, W, Cin] bf16 or null.
+MDA_API int mda_conv_dgrad_res(const void* dy, const void* wt, void* dx, float* partial,
+                               const void* res, int64_t N, int64_t H, int64_t W, int64_t Cin,
+                               int64_t Ho, int64_t Wo, int64_t Cout, int64_t KH, int64_t KW,
+                               int64_t stride, int64_t pad, int64_t Kp, int64_t tile,
+                               int64_t splits, hipStream_t st) {
   if (Cout % 8) return (int)hipErrorInvalidValue;
   ConvParams p;
   p.x = (const bf16_t*)dy; p.w = (const bf16_t*)wt; p.scale = nullptr; p.bias = nullptr;
-  p.res = nullptr; p.y = (bf16_t*)dx; p.preact = nullptr; p.partial = partial;
+  p.res = (const bf16_t*)res; p.y = (bf16_t*)dx; p.preact = nullptr; p.partial = partial;
   // GEMM view: rows = dx pixels, cols = Cin, k = (tap, co); "input" image = dy
   p.N = N; p.H = Ho; p.W = Wo; p.Cin = Cout; p.Ho = H; p.Wo = W; p.Cout = Cin; p.KH = KH;
   p.KW = KW; p.stride = stride; p.pad = pad; p.K = KH * KW * Cout; p.Kp = Kp; p.M = N * H * W;
@@ -1756,6 +1785,7 @@ MDA_API int mda_conv_dgrad(const void* dy, const void* wt, void* dx, float* part
   p.par = 0;
   p.zsplits = 1;
   p.stats_part = nullptr;
+  p.stats_slot = nullptr;
   p.stamps = g_stamps;
   // strided dgrad: one GEMM per output-parity class with only its taps
   if (stride > 1 && mode == LOAD_DGRAD_FAST && use_glds() && use_par_dgrad()) p.par = (int)stride;
@@ -1798,6 +1828,7 @@ MDA_API int mda_conv_fwd_bnstats(const void* x, const void* w, void* y, float* p
   p.par = 0;
   p.zsplits = 1;
   p.stats_part = nullptr;
+  p.stats_slot = nullptr;
   p.stamps = g_stamps;
   if (Cout % 8 || Cout > 2048) return (int)hipErrorInvalidValue;
   int mode = (Cin % BK == 0) ? LOAD_FAST : (Cin % 8 == 0 ? LOAD_VEC8 : LOAD_SCALAR);
@@ -1822,4 +1853,37 @@ MDA_API int mda_conv_fwd_bnstats(const void* x, const void* w, void* y, float* p
                            mean, rstd, scale, shift, momentum, eps, nbt, st);
   return mda_bn_stats2(y, p.M, Cout, bn_partial, gamma, beta, running_mean, running_var, mean,
                        rstd, scale, shift, momentum, eps, nbt, st);
+}
+
+// Training conv whose epilogue adds the BN statistics of its raw bf16 output
+// into a BnRegion (csrc/bnslot.h); the caller follows with mda_bn_apply_fin,
+// whose prologue finalizes them (2 launches per conv + BN instead of 3).
+// Split-K convs (sums only final after the combine) run the conv, then the
+// standalone statistics pass into the same slot.
+extern "C" int mda_bn_stats_acc(const void* y, int64_t M, int64_t C, void* region, hipStream_t st);
+
+MDA_API int mda_conv_fwd_bnacc(const void* x, const void* w, void* y, float* partial, void* region,
+                               int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Ho,
+                               int64_t Wo, int64_t Cout, int64_t KH, int64_t KW, int64_t stride,
+                               int64_t pad, int64_t Kp, int64_t tile, int64_t splits,
+                               hipStream_t st) {
+  ConvParams p;
+  p.x = (const bf16_t*)x; p.w = (const bf16_t*)w; p.scale = nullptr; p.bias = nullptr;
+  p.res = nullptr; p.y = (bf16_t*)y; p.preact = nullptr; p.partial = partial;
+  p.N = N; p.H = H; p.W = W; p.Cin = Cin; p.Ho = Ho; p.Wo = Wo; p.Cout = Cout; p.KH = KH;
+  p.KW = KW; p.stride = stride; p.pad = pad; p.K = KH * KW * Cin; p.Kp = Kp; p.M = N * Ho * Wo;
+  p.act = 0;
+  p.par = 0;
+  p.zsplits = 1;
+  p.stats_part = nullptr;
+  p.stats_slot = nullptr;
+  p.stamps = g_stamps;
+  if (Cout % 8 || Cout > SLOT_CMAX) return (int)hipErrorInvalidValue;
+  int mode = (Cin % BK == 0) ? LOAD_FAST : (Cin % 8 == 0 ? LOAD_VEC8 : LOAD_SCALAR);
+  if (tile == 0 || splits == 0) mda_conv_plan(p.M, p.Cout, p.Kp, &tile, &splits);
+  const int halo = halo_eligible(p) ? 1 : 0;
+  if (splits == 1) p.stats_slot = (BnRegion*)region;
+  int rc = dispatch(p, mode, tile, splits, st, halo);
+  if (rc || splits == 1) return rc;
+  return mda_bn_stats_acc(y, p.M, Cout, region, st);
 }

@@ -33,11 +33,110 @@ _ACT = {"none": 0, "relu": 1, "relu6": 2}
 
 
 class _WS:
-    """Per-device scratch for the BN reductions (partials + arrival counters)."""
+    """Per-stream scratch for the unfused BN reductions (partial rows +
+    arrival counters)."""
 
     def __init__(self, device):
         self.partial = torch.zeros(2 * 2048 * 512, dtype=torch.float32, device=device)
         self.counter = torch.zeros(64, dtype=torch.int32, device=device)
+
+
+_BN_FUSED = [os.environ.get("MDA_BN_FUSED", "1") != "0"]
+
+
+def set_bn_fused(on: bool) -> None:
+    """Fused BN (one-shot channel-sum regions: conv+stats -> apply with the
+    finalize in its prologue; one-launch grid-barrier backward) vs the
+    partial-rows path (A/B)."""
+    _BN_FUSED[0] = bool(on)
+
+
+_REG_BYTES: dict = {}
+
+
+def _region_bytes(C: int) -> int:
+    v = _REG_BYTES.get(C)
+    if v is None:
+        o = ctypes.c_int64(0)
+        _ext.call("mda_bn_region_bytes", C, o)
+        v = _REG_BYTES[C] = (int(o.value) + 255) // 256 * 256
+    return v
+
+
+class _Arena:
+    """Per-device arena of one-shot BN regions (csrc/bnslot.h).
+
+    ``bn_step_begin`` (start of every training step, inside its hipGraph)
+    zeroes the part the previous steps used with ONE memset and hands regions
+    out from offset 0: each training BN call of the step gets its own zeroed
+    region, at the same offset in every step, so captured graphs stay valid.
+    Calls outside a step, or beyond the zeroed part, get a fresh zeroed tensor.
+    """
+
+    CAP = 8 << 20
+
+    def __init__(self, device):
+        # fp32-typed so the step's memset can share one multi-tensor zeroing
+        # launch with the flat fp32 gradient buffer (engine/step.py::_fwd)
+        self.buf32 = torch.zeros(self.CAP // 4, dtype=torch.float32, device=device)
+        self.buf = self.buf32.view(torch.uint8)
+        self.err = torch.zeros(4, dtype=torch.int32, device=device)  # barrier timeouts
+        self.off = 0
+        self.zeroed = 0
+        self.high = 64 << 10
+        self.active = False
+
+
+_ARENAS: dict = {}
+
+
+def _arena(device) -> _Arena:
+    dev = torch.device(device)
+    key = dev.index or 0
+    a = _ARENAS.get(key)
+    if a is None:
+        a = _ARENAS[key] = _Arena(dev)
+    return a
+
+
+def bn_step_begin(device, zero: bool = True):
+    """Start a training step's arena.  ``zero=False``: the caller zeroes the
+    returned fp32 view itself (e.g. in one multi-tensor launch with the
+    gradients) before the step's first BN."""
+    a = _arena(device)
+    n = (min(a.high, a.CAP) + 255) // 256 * 256
+    a.off, a.zeroed, a.active = 0, n, True
+    view = a.buf32[:n // 4]
+    if zero:
+        view.zero_()
+    return view
+
+
+def bn_step_end(device) -> None:
+    a = _ARENAS.get(torch.device(device).index or 0)
+    if a is not None:
+        a.active = False
+
+
+def _region(C: int, device):
+    a = _arena(device)
+    need = _region_bytes(C)
+    if a.active:
+        start = a.off
+        a.off += need
+        a.high = max(a.high, a.off)  # the next step's memset covers the demand
+        if a.off <= a.zeroed:
+            return a.buf[start:a.off]
+    return torch.zeros(need, dtype=torch.uint8, device=device)
+
+
+def _err_word(device):
+    return _arena(device).err
+
+
+def slot_errors() -> int:
+    """Number of devices on which a fused-BN grid barrier timed out (must be 0)."""
+    return sum(int(a.err.max().item() != 0) for a in _ARENAS.values())
 
 
 _WSS: dict = {}
@@ -145,6 +244,30 @@ def _bn_bwd_reduce(dout, dpre, y, res, stats, M, C, act, ws, sums, dg, db):
     combine, ``mda_bn_bwd_reduce``, measured slower: profiles/r2_misc_ab.md)."""
     _ext.call("mda_bn_bwd_reduce2", dout, dpre, y, res, stats[2], stats[3], stats[0], stats[1],
               M, C, act, ws.partial, sums, dg, db)
+
+
+def _bn_bwd(dout, dpre, y, res, stats, gamma, beta, M, C, act, need_res, direct_gb):
+    """BN (+ residual) (+ activation) backward -> (dy, dres or None, sums or
+    None).  Fused: ONE grid-barrier launch (mda_bn_bwd_fused); else the
+    partial-rows reduce + finalize + apply (3 launches).  dgamma / dbeta are
+    accumulated into the parameters' flat-gradient views when ``direct_gb``,
+    else returned through ``sums`` ([sum dz | sum dz*xhat])."""
+    dev = y.device
+    ws = _ws(dev)
+    dg = gamma.grad if direct_gb else None
+    db = beta.grad if direct_gb else None
+    dy = torch.empty_like(y)
+    dres = torch.empty_like(y) if need_res else None
+    if _BN_FUSED[0]:
+        sums = None if direct_gb else torch.empty(2, C, dtype=torch.float32, device=dev)
+        _ext.call("mda_bn_bwd_fused", dout, None, dpre, y, res, stats, M, C, act, _region(C, dev),
+                  _err_word(dev), dy, dres, dg, db, sums)
+        return dy, dres, sums
+    sums = torch.empty(2, C, dtype=torch.float32, device=dev)
+    _bn_bwd_reduce(dout, dpre, y, res, stats, M, C, act, ws, sums, dg, db)
+    _ext.call("mda_bn_bwd_apply", dout, dpre, y, res, stats[2], stats[3], stats[0], stats[1],
+              sums, dy, dres, M, C, act)
+    return dy, dres, sums
 
 
 _WG_PLANS: dict = {}
@@ -365,14 +488,75 @@ def _dw_wgrad_blocks(N, Ho, Wo, C):
     return v
 
 
+class GradFork:
+    """Two consumers of one activation (a residual fork: conv1 and the
+    shortcut conv, or conv1 and the identity residual) whose input gradients
+    are summed INSIDE the native backward instead of by an autograd add.
+
+    Both consumers register in their forward (:meth:`join`); in the backward
+    the first one to run parks its gradient (and an event on its stream) and
+    returns None for the shared input; the second adds the parked gradient in
+    its dgrad's residual epilogue (``mda_conv_dgrad_res``) -- or, if it has no
+    dgrad, with one add -- and returns the sum.  A fork whose second consumer
+    took a non-native path (``members < 2``) is inert: both return their own
+    gradient and autograd adds them as usual.
+    """
+
+    def __init__(self):
+        self.members = 0
+        self.pending = None
+        self.event = None
+
+    def join(self):
+        self.members += 1
+        return self
+
+    @property
+    def armed(self) -> bool:
+        return self.members == 2
+
+    def park(self, g) -> bool:
+        """First arrival: keep ``g`` and return True (caller returns None)."""
+        if not self.armed or self.pending is not None:
+            return False
+        self.pending = g
+        self.event = torch.cuda.Event()
+        self.event.record(torch.cuda.current_stream(g.device))
+        return True
+
+    def take(self):
+        """Second arrival: the parked gradient (ordered on the current stream), or None."""
+        if not self.armed or self.pending is None:
+            return None
+        g, self.pending = self.pending, None
+        cur = torch.cuda.current_stream(g.device)
+        cur.wait_event(self.event)
+        g.record_stream(cur)
+        self.event = None
+        return g
+
+
+def _fork_sum(fork, g):
+    """Autograd-visible gradient of a forked input for a consumer without a
+    dgrad of its own (the identity residual): park it, or add the parked one."""
+    if fork is None or g is None:
+        return g
+    if fork.park(g):
+        return None
+    other = fork.take()
+    return g if other is None else g + other
+
+
 class _ConvBNActTrain(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, gamma, beta, residual, meta, bn, want_preact):
+    def forward(ctx, x, weight, gamma, beta, residual, meta, bn, want_preact, forks=(None, None)):
         stride, pad, act = meta[:3]
         if len(meta) > 3 and meta[3] == "dw":
+            ctx.forks = (None, None)
             return _dw_forward(ctx, x, weight, gamma, beta, residual, stride, pad, act, bn,
                                want_preact)
         ctx.kind = "dense"
+        ctx.forks = tuple(f.join() if f is not None else None for f in forks)
         G = meta[4] if len(meta) > 4 and meta[3] == "grouped" else 1
         ctx.groups = G
         need_dx = ctx.needs_input_grad[0]
@@ -417,15 +601,26 @@ class _ConvBNActTrain(torch.autograd.Function):
                         memory_format=torch.channels_last)
         ws = _ws(dev)
         stats = torch.empty(4, Cout, dtype=torch.float32, device=dev)  # mean, rstd, scale, shift
-        # conv whose epilogue emits the BN statistics partials + finalize (2 launches)
-        _ext.call("mda_conv_fwd_bnstats", x, wf, y, part, ws.partial, ws.partial.numel(), N, H, W,
-                  Cin, Ho, Wo, Cout, KH, KW, stride, pad, Kp, tile, splits, gamma.detach(),
-                  beta.detach(), bn.running_mean, bn.running_var, stats[0], stats[1], stats[2],
-                  stats[3], float(bn.momentum), float(bn.eps), bn.num_batches_tracked)
         res = _cl_bf16(residual) if residual is not None else None
         out = torch.empty_like(y)
         pre = torch.empty_like(y) if want_preact else None
-        _ext.call("mda_bn_apply", y, stats[2], stats[3], res, out, pre, M, Cout, act)
+        if _BN_FUSED[0]:
+            # conv whose epilogue adds the BN sums into the stream's slot, then
+            # apply with the finalize in its prologue (2 launches)
+            reg = _region(Cout, dev)
+            _ext.call("mda_conv_fwd_bnacc", x, wf, y, part, reg, N, H, W, Cin, Ho, Wo, Cout,
+                      KH, KW, stride, pad, Kp, tile, splits)
+            _ext.call("mda_bn_apply_fin", y, reg, M, Cout, gamma.detach(), beta.detach(),
+                      bn.running_mean, bn.running_var, stats, float(bn.momentum), float(bn.eps),
+                      bn.num_batches_tracked, res, out, pre, act)
+        else:
+            # conv whose epilogue emits the BN statistics partials + finalize (2 launches)
+            _ext.call("mda_conv_fwd_bnstats", x, wf, y, part, ws.partial, ws.partial.numel(), N, H,
+                      W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, Kp, tile, splits, gamma.detach(),
+                      beta.detach(), bn.running_mean, bn.running_var, stats[0], stats[1],
+                      stats[2], stats[3], float(bn.momentum), float(bn.eps),
+                      bn.num_batches_tracked)
+            _ext.call("mda_bn_apply", y, stats[2], stats[3], res, out, pre, M, Cout, act)
         ctx.save_for_backward(x, wt, weight, gamma, beta, y, res, stats)
         ctx.meta = (N, Cin, H, W, Cout, Ho, Wo, KH, KW, stride, pad, Kp, KpT, act)
         ctx.has_res = residual is not None
@@ -443,18 +638,14 @@ class _ConvBNActTrain(torch.autograd.Function):
         dev = y.device
         dout = _cl_bf16(dout) if dout is not None else None
         dpre = _cl_bf16(dpre) if dpre is not None else None
-        ws = _ws(dev)
-        sums = torch.empty(2, Cout, dtype=torch.float32, device=dev)
         # dgamma / dbeta straight into existing .grad buffers (flat views), else returned
         direct_gb = gamma.grad is not None and beta.grad is not None
-        dg = gamma.grad if direct_gb else None
-        db = beta.grad if direct_gb else None
-        _bn_bwd_reduce(dout, dpre, y, res, stats, M, Cout, act, ws, sums, dg, db)
         need_res = ctx.has_res and ctx.needs_input_grad[4]
-        dy = torch.empty_like(y)
-        dres = torch.empty_like(y) if need_res else None
-        _ext.call("mda_bn_bwd_apply", dout, dpre, y, res, stats[2], stats[3], stats[0], stats[1],
-                  sums, dy, dres, M, Cout, act)
+        dy, dres, sums = _bn_bwd(dout, dpre, y, res, stats, gamma, beta, M, Cout, act, need_res,
+                                 direct_gb)
+        x_fork, res_fork = ctx.forks
+        if need_res:
+            dres = _fork_sum(res_fork, dres)
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty((N, Cin, H, W), dtype=torch.bfloat16, device=dev,
@@ -462,8 +653,11 @@ class _ConvBNActTrain(torch.autograd.Function):
             from .hip_layers import conv_plan
             tile, splits = conv_plan(N * H * W, Cin, KpT)
             part = torch.empty(splits * N * H * W * Cin, dtype=torch.float32, device=dev) if splits > 1 else None
-            _ext.call("mda_conv_dgrad", dy, wt, dx, part, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
-                      stride, pad, KpT, tile, splits)
+            other = x_fork.take() if x_fork is not None else None
+            _ext.call("mda_conv_dgrad_res", dy, wt, dx, part, other, N, H, W, Cin, Ho, Wo, Cout,
+                      KH, KW, stride, pad, KpT, tile, splits)
+            if other is None and x_fork is not None and x_fork.park(dx):
+                dx = None
         dw = None
         if ctx.needs_input_grad[1]:
             sp = _wgrad_splits(M, Cout, Cin, KH, KW, Kp)
@@ -481,19 +675,26 @@ class _ConvBNActTrain(torch.autograd.Function):
             notify_grad(gamma, beta)
         dgamma = None if direct_gb else sums[1].clone()
         dbeta = None if direct_gb else sums[0].clone()
-        return dx, dw, dgamma, dbeta, dres, None, None, None
+        return dx, dw, dgamma, dbeta, dres, None, None, None, None
 
 
 def _bn_train_forward(y, M, C, gamma, beta, bn, residual, act, want_preact):
     dev = y.device
     ws = _ws(dev)
     stats = torch.empty(4, C, dtype=torch.float32, device=dev)  # mean, rstd, scale, shift
-    _ext.call("mda_bn_stats2", y, M, C, ws.partial, gamma.detach(), beta.detach(),
-              bn.running_mean, bn.running_var, stats[0], stats[1], stats[2], stats[3],
-              float(bn.momentum), float(bn.eps), bn.num_batches_tracked)
     res = _cl_bf16(residual) if residual is not None else None
     out = torch.empty_like(y)
     pre = torch.empty_like(y) if want_preact else None
+    if _BN_FUSED[0]:
+        reg = _region(C, dev)
+        _ext.call("mda_bn_stats_acc", y, M, C, reg)
+        _ext.call("mda_bn_apply_fin", y, reg, M, C, gamma.detach(), beta.detach(),
+                  bn.running_mean, bn.running_var, stats, float(bn.momentum), float(bn.eps),
+                  bn.num_batches_tracked, res, out, pre, act)
+        return out, pre, res, stats
+    _ext.call("mda_bn_stats2", y, M, C, ws.partial, gamma.detach(), beta.detach(),
+              bn.running_mean, bn.running_var, stats[0], stats[1], stats[2], stats[3],
+              float(bn.momentum), float(bn.eps), bn.num_batches_tracked)
     _ext.call("mda_bn_apply", y, stats[2], stats[3], res, out, pre, M, C, act)
     return out, pre, res, stats
 
@@ -501,19 +702,11 @@ def _bn_train_forward(y, M, C, gamma, beta, bn, residual, act, want_preact):
 def _bn_train_backward(ctx, dout, dpre, y, res, stats, gamma, beta, M, C, act):
     """-> (dy, dres, dgamma or None, dbeta or None); dgamma/dbeta go straight
     into bound flat-gradient views when present."""
-    dev = y.device
     dout = _cl_bf16(dout) if dout is not None else None
     dpre = _cl_bf16(dpre) if dpre is not None else None
-    ws = _ws(dev)
-    sums = torch.empty(2, C, dtype=torch.float32, device=dev)
     direct_gb = gamma.grad is not None and beta.grad is not None
-    dg = gamma.grad if direct_gb else None
-    db = beta.grad if direct_gb else None
-    _bn_bwd_reduce(dout, dpre, y, res, stats, M, C, act, ws, sums, dg, db)
-    dy = torch.empty_like(y)
-    dres = torch.empty_like(y) if res is not None else None
-    _ext.call("mda_bn_bwd_apply", dout, dpre, y, res, stats[2], stats[3], stats[0], stats[1],
-              sums, dy, dres, M, C, act)
+    dy, dres, sums = _bn_bwd(dout, dpre, y, res, stats, gamma, beta, M, C, act, res is not None,
+                             direct_gb)
     if direct_gb:
         notify_grad(gamma, beta)
         return dy, dres, None, None
@@ -574,7 +767,7 @@ def _dw_backward(ctx, dout, dpre):
         dw = None if direct_w else target
         if direct_w:
             notify_grad(weight)
-    return dx, dw, dgamma, dbeta, dres, None, None, None
+    return dx, dw, dgamma, dbeta, dres, None, None, None, None
 
 
 def pack_weights(weight, dgrad=True):
@@ -831,12 +1024,18 @@ def conv_trainbn_nograd(x, conv, bn, act, residual, want_preact):
     return out, pre
 
 
-def conv_bn_act_train(x, conv, bn, act, residual, want_preact):
+def conv_bn_act_train(x, conv, bn, act, residual, want_preact, fork=None, res_fork=None):
+    """``fork``: the :class:`GradFork` of ``x`` (another consumer of x sums
+    its gradient into this layer's dgrad, or vice versa); ``res_fork``: the
+    fork of ``residual`` (identity shortcut)."""
     meta = (conv.stride[0], conv.padding[0], _ACT[act])
     if is_depthwise(conv):
         meta = meta + ("dw",)
+        fork = res_fork = None
     elif conv.groups != 1:
         meta = meta + ("grouped", conv.groups)
+    if residual is None:
+        res_fork = None
     out, pre = _ConvBNActTrain.apply(x, conv.weight, bn.weight, bn.bias, residual, meta, bn,
-                                     bool(want_preact))
+                                     bool(want_preact), (fork, res_fork))
     return out, pre

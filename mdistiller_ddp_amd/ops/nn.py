@@ -43,15 +43,20 @@ def _bn(x: torch.Tensor, bn: nn.BatchNorm2d) -> torch.Tensor:
 
 def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d | None = None,
                 act: str = "relu", residual: torch.Tensor | None = None,
-                want_preact: bool = False):
-    """``act(bn(conv(x)) + residual)``; returns ``(out, preact_or_None)``."""
+                want_preact: bool = False, fork=None, res_fork=None):
+    """``act(bn(conv(x)) + residual)``; returns ``(out, preact_or_None)``.
+
+    ``fork`` / ``res_fork`` (:class:`ops.hip_train.GradFork`, optional): x /
+    residual also feed another native layer; their gradients are summed
+    inside the native backward (no autograd add) -- ignored off that path."""
     if hip_enabled_for(x):
         from . import hip_layers
         if hip_layers.conv_supported(x, conv, bn):
             return hip_layers.conv_bn_act(x, conv, bn, act, residual, want_preact)
         from . import hip_train
         if _TRAIN_KERNELS["on"] and hip_train.train_supported(x, conv, bn):
-            return hip_train.conv_bn_act_train(x, conv, bn, act, residual, want_preact)
+            return hip_train.conv_bn_act_train(x, conv, bn, act, residual, want_preact, fork,
+                                               res_fork)
         if _TRAIN_KERNELS["on"] and bn is None and hip_train.conv_train_supported(x, conv):
             return hip_train.conv_act_train(x, conv, act, residual, want_preact)
         if hip_train.trainbn_nograd_supported(x, conv, bn):
@@ -295,3 +300,12 @@ class MaxPool2d(nn.MaxPool2d):
         if self.dilation not in (1, (1, 1)) or self.ceil_mode or self.return_indices:
             return super().forward(x)
         return max_pool2d(x, self.kernel_size, self.stride, self.padding)
+
+
+def grad_fork(x: torch.Tensor):
+    """A :class:`ops.hip_train.GradFork` for an activation with two native
+    consumers (training on the HIP path), else None."""
+    if not (torch.is_grad_enabled() and x.requires_grad and hip_enabled_for(x)):
+        return None
+    from . import hip_train
+    return hip_train.GradFork()

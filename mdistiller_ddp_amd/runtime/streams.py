@@ -14,6 +14,7 @@ as a fork/join in the graph.
 """
 from __future__ import annotations
 
+import os
 import threading
 
 import torch
@@ -172,3 +173,64 @@ class TeacherFeed:
         if self._pending is not None:
             _copy_struct(self.X, self._keep(self._pending.get()))
             self._pending = None
+
+
+# ---------------------------------------------------------------------------
+# Intra-block branch concurrency (round 3).  A residual block's projection
+# shortcut (1x1 conv + BN) is independent of its main path until the
+# residual add, so the student issues it on a BRANCH stream forked from the
+# current one: the forward shortcut runs beside conv1 / conv2, and autograd
+# runs its backward (BN backward, dgrad, wgrad) on the same branch stream,
+# beside the main path's dgrad chain.  Native backward kernels write some
+# gradients straight into the flat buffer (no autograd edge back to the
+# caller), so whoever runs the backward joins every branch stream used
+# (``join_branches``) before reading the gradients; hipGraph records the
+# fork/join as parallel branches of the captured step.
+_branch = {"enabled": os.environ.get("MDA_BRANCH_STREAMS", "1") != "0", "used": set()}
+_branch_streams: dict = {}
+
+
+def set_branches(flag: bool) -> None:
+    _branch["enabled"] = bool(flag)
+
+
+def branch_stream(device) -> "torch.cuda.Stream":
+    idx = torch.device(device).index or 0
+    with _lock:
+        s = _branch_streams.get(idx)
+        if s is None:
+            s = torch.cuda.Stream(device=idx)
+            _branch_streams[idx] = s
+        return s
+
+
+def run_branch(x: torch.Tensor, fn):
+    """``fn(x)`` on the branch stream (training forward on a GPU), joined back
+    into the current stream before the result is returned; otherwise inline."""
+    if not (_branch["enabled"] and x.is_cuda and torch.is_grad_enabled()):
+        return fn(x)
+    cur = torch.cuda.current_stream(x.device)
+    s = branch_stream(x.device)
+    if s.cuda_stream == cur.cuda_stream:
+        return fn(x)
+    s.wait_stream(cur)
+    with torch.cuda.stream(s):
+        out = fn(x)
+    x.record_stream(s)
+    cur.wait_stream(s)
+    for t in _tensors(out, []):
+        t.record_stream(cur)
+    _branch["used"].add(x.device.index or 0)
+    return out
+
+
+def join_branches() -> None:
+    """Make the current stream wait for every branch stream used (gradients
+    the branch's native backward wrote directly)."""
+    if not _branch["used"]:
+        return
+    cur = torch.cuda.current_stream()
+    for idx in list(_branch["used"]):
+        s = _branch_streams.get(idx)
+        if s is not None and s.cuda_stream != cur.cuda_stream:
+            cur.wait_stream(s)

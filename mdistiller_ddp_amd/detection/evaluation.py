@@ -46,6 +46,21 @@ def box_iou_np(a, b):
     return inter / np.maximum(aa[:, None] + ab[None, :] - inter, 1e-12)
 
 
+def _voc_iou(b, gb):
+    """Pascal VOC IoU of one box against many, with the +1 pixel convention of
+    Detectron2's ``voc_eval`` (inclusive integer pixel coordinates)."""
+    ixmin = np.maximum(gb[:, 0], b[0])
+    iymin = np.maximum(gb[:, 1], b[1])
+    ixmax = np.minimum(gb[:, 2], b[2])
+    iymax = np.minimum(gb[:, 3], b[3])
+    iw = np.maximum(ixmax - ixmin + 1.0, 0.0)
+    ih = np.maximum(iymax - iymin + 1.0, 0.0)
+    inter = iw * ih
+    uni = ((b[2] - b[0] + 1.0) * (b[3] - b[1] + 1.0)
+           + (gb[:, 2] - gb[:, 0] + 1.0) * (gb[:, 3] - gb[:, 1] + 1.0) - inter)
+    return inter / np.maximum(uni, 1e-12)
+
+
 def mask_iou_np(a, b):
     """a [N, H, W], b [M, H, W] boolean masks -> [N, M] IoU."""
     if len(a) == 0 or len(b) == 0:
@@ -82,9 +97,11 @@ def _ap_101(tp, conf, n_gt):
     return float(q.mean())
 
 
-def _greedy_match(iou, gign, thr):
+def _greedy_match(iou, gign, thr, crowd=None):
     """COCO greedy matching of score-sorted detections to ground truths
-    (non-ignored first); returns (matched gt index or -1) per detection."""
+    (non-ignored first); returns (matched gt index or -1) per detection.
+    ``crowd``: iscrowd ground truths, which (as in pycocotools
+    ``COCOeval.evaluateImg``) may absorb any number of detections."""
     D, G = iou.shape
     used = np.zeros(G, bool)
     order = np.argsort(gign, kind="mergesort")
@@ -92,7 +109,7 @@ def _greedy_match(iou, gign, thr):
     for d in range(D):
         best, m = min(thr, 1 - 1e-10), -1
         for gi in order:
-            if used[gi]:
+            if used[gi] and not (crowd is not None and crowd[gi]):
                 continue
             if m > -1 and not gign[m] and gign[gi]:
                 break
@@ -139,10 +156,13 @@ def instance_ap(predictions, ground_truths, num_classes, *, iou_type="bbox", max
                 else:
                     not_exh = False
                 gobj = g[key][gm]
+                # the annotation's ``area`` field when present (pycocotools), else
+                # the box / mask area; inclusive upper bound like pycocotools
                 ga = g["areas"][gm] if "areas" in g else _areas({key: gobj, "boxes": gobj}, iou_type)
-                gign = (ga < lo) | (ga >= hi)
-                if "iscrowd" in g:
-                    gign = gign | g["iscrowd"][gm].astype(bool)
+                gign = (ga < lo) | (ga > hi)
+                crowd = g["iscrowd"][gm].astype(bool) if "iscrowd" in g else None
+                if crowd is not None:
+                    gign = gign | crowd
                 n_gt += int((~gign).sum())
                 pm = p["classes"] == c
                 pobj, ps = p[key][pm], p["scores"][pm]
@@ -152,11 +172,15 @@ def instance_ap(predictions, ground_truths, num_classes, *, iou_type="bbox", max
                     continue
                 iou = iou_fn(pobj, gobj) if len(gobj) else np.zeros((len(ps), 0))
                 pa = _areas({key: pobj, "boxes": pobj}, iou_type)
+                if crowd is not None and crowd.any() and len(gobj):
+                    # pycocotools: IoU with a crowd region = intersection / detection area
+                    inter = iou * (pa[:, None] + _areas({key: gobj, "boxes": gobj}, iou_type)[None, :]) / (1 + iou)
+                    iou = np.where(crowd[None, :], inter / np.maximum(pa[:, None], 1e-12), iou)
                 for ti, t in enumerate(ious):
-                    m = _greedy_match(iou, gign, t) if len(gobj) else np.full(len(ps), -1)
+                    m = _greedy_match(iou, gign, t, crowd) if len(gobj) else np.full(len(ps), -1)
                     tp = (m >= 0).astype(np.float64)
                     ign = np.where(m >= 0, gign[np.maximum(m, 0)] if len(gobj) else False,
-                                   (pa < lo) | (pa >= hi) | not_exh)
+                                   (pa < lo) | (pa > hi) | not_exh)
                     keep = ~ign
                     tps[ti].append((tp[keep], ps[keep]))
             for ti in range(len(ious)):
@@ -241,7 +265,7 @@ def voc_class_ap(predictions, ground_truths, c, thr, use_07_metric=True):
     for k, (_, i, b) in enumerate(dets):
         gb, diff, seen = state[i]
         if len(gb):
-            iou = box_iou_np(b[None].astype(np.float64), gb.astype(np.float64))[0]
+            iou = _voc_iou(b.astype(np.float64), gb.astype(np.float64))
             j = int(np.argmax(iou))
             if iou[j] > thr:
                 if diff[j]:
@@ -451,8 +475,10 @@ class SemSegEvaluator(DatasetEvaluator):
         if get_world_size() > 1:
             import torch.distributed as dist
             t = torch.from_numpy(conf)
+            if dist.get_backend() == "nccl":  # RCCL: device tensors only
+                t = t.to(torch.device("cuda", torch.cuda.current_device()))
             dist.all_reduce(t)
-            conf = t.numpy()
+            conf = t.cpu().numpy()
         return {"sem_seg": semseg_metrics(conf, self.class_names)}
 
 

@@ -103,7 +103,11 @@ class OFD(Distiller):
         self.feat_loss_weight = cfg.OFD.LOSS.FEAT_WEIGHT
         self._teacher_train_bn = bool(cfg.OFD.TEACHER_TRAIN_BN)
         # the train-mode teacher BN runs on the native capture-safe kernels, so
-        # the whole step is captured (round 1 had to run this mode eagerly)
+        # the whole step is captured (round 1 had to run this mode eagerly) --
+        # unless a teacher layer fell back to MIOpen's train-mode BN during the
+        # eager warm-up (``graph_capturable`` below; TrainStep re-checks it
+        # right before capturing)
+        self._teacher_fallbacks = 0
         self.init_ofd_modules(self.teacher.get_stage_channels()[1:],
                               self.student.get_stage_channels()[1:],
                               self.teacher.get_bn_before_relu(),
@@ -154,8 +158,16 @@ class OFD(Distiller):
             loss = loss + feat_loss(feature_student[i], t, margins[i]) / 2 ** (n - i - 1)
         return loss
 
+    @property
+    def graph_capturable(self) -> bool:
+        return not (self._teacher_train_bn and self._teacher_fallbacks > 0)
+
     def forward_train(self, image, target, **kwargs):
+        from ..ops.nn import trainbn_fallbacks
+        n0 = trainbn_fallbacks()
         t_out = self.teacher_forward(image)
+        if self._teacher_train_bn:
+            self._teacher_fallbacks += trainbn_fallbacks() - n0
         logits_student, feature_student = self.student(image)
         _, feature_teacher = t_out.get()
         loss_ce = L.ce(logits_student, target, self.ce_loss_weight)

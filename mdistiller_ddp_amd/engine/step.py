@@ -454,6 +454,11 @@ class TrainStep:
             out = self._eager(static)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
+        if not getattr(self.distiller, "graph_capturable", True):
+            # decided by the eager steps (e.g. OFD's train-mode teacher BN fell
+            # back to MIOpen on some layer): stay eager for good
+            self.use_graph = False
+            return out
         if self.is_dot and self.dot_dual and not self.graph_comm:
             return self._capture_dot_dual(static, pool, s, out)
         feed = None
@@ -583,7 +588,10 @@ class TrainStep:
                     self._join_wgrad_stream(armed)
                     join_branches()
                 if feed is not None:
-                    feed.finish()
+                    # join only: the KD-backward graph may still be replaying on the
+                    # main stream; the copy into the teacher-output buffers it was
+                    # built from happens in g_opt, after the two streams joined
+                    feed.finish(copy=False)
         finally:
             hip_train.set_ws_tag(None)
             if feed is not None:
@@ -591,8 +599,10 @@ class TrainStep:
         if self.world > 1:
             # split mode: the bucketed all-reduce runs eagerly between the backward
             # graphs (+ the post-backward hook, if any) and the optimizer graph
-            if getattr(self.distiller, "post_backward", None) is not None:
+            if getattr(self.distiller, "post_backward", None) is not None or feed is not None:
                 with torch.cuda.graph(g_opt, pool=pool, stream=s):
+                    if feed is not None:
+                        feed.commit()
                     self._post_backward()
             else:
                 g_opt = None
@@ -601,6 +611,8 @@ class TrainStep:
                 self._update(preds, static["target"], losses)
         else:
             with torch.cuda.graph(g_opt, pool=pool, stream=s):
+                if feed is not None:
+                    feed.commit()
                 self._post_backward()
                 self._update(preds, static["target"], losses)
             g_upd = None

@@ -21,10 +21,14 @@ def _act_of(m):
     return None
 
 
-def run_seq(seq, x, residual=None, want_preact=False):
+def run_seq(seq, x, residual=None, want_preact=False, final_act=None):
     """Returns ``(out, preact_of_last_group_or_None)``.
 
     ``residual`` is added after the last group's BN, before its activation.
+    ``final_act`` overrides the last group's activation (e.g. "relu" on a
+    linear-bottleneck output whose consumer applies ReLU: one fused launch
+    returns both the activated tensor and, with ``want_preact``, the linear
+    one).
     """
     mods = list(seq)
     i, pre = 0, None
@@ -38,6 +42,8 @@ def run_seq(seq, x, residual=None, want_preact=False):
             if j < n and _act_of(mods[j]) is not None:
                 act, j = _act_of(mods[j]), j + 1
             last = j >= n
+            if last and final_act is not None:
+                act = final_act
             x, pre = conv_bn_act(x, m, bn, act, residual if last else None, want_preact and last)
             i = j
         elif isinstance(m, nn.BatchNorm2d):

@@ -43,14 +43,15 @@ class BasicBlock(nn.Module):
         # x feeds conv1 and the shortcut: their input gradients are summed in
         # the second one's dgrad epilogue (GradFork), not by an autograd add
         fork = grad_fork(x)
+        h, _ = conv_bn_act(x, self.conv1, self.bn1, "relu", fork=fork)
         if self.downsample is None:
-            h, _ = conv_bn_act(x, self.conv1, self.bn1, "relu", fork=fork)
             res = x
         else:
-            # projection shortcut on the branch stream, beside conv1 (and, in
-            # the backward, beside the main path's dgrad chain)
+            # projection shortcut on the branch stream, beside conv2.  Created
+            # after conv1, so autograd issues its backward first: the shorter
+            # branch chain (BN backward + 1x1 dgrad) parks its input gradient
+            # and conv1's dgrad, last on the main chain, adds it in its epilogue
             res = run_branch(x, lambda t: self._shortcut(t, fork))
-            h, _ = conv_bn_act(x, self.conv1, self.bn1, "relu", fork=fork)
             fork = None
         return conv_bn_act(h, self.conv2, self.bn2, "relu", residual=res,
                            want_preact=self.is_last and self._need_preact, res_fork=fork)
@@ -78,8 +79,8 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         fork = grad_fork(x)
-        res = x if self.downsample is None else run_branch(x, lambda t: self._shortcut(t, fork))
         h, _ = conv_bn_act(x, self.conv1, self.bn1, "relu", fork=fork)
+        res = x if self.downsample is None else run_branch(x, lambda t: self._shortcut(t, fork))
         h, _ = conv_bn_act(h, self.conv2, self.bn2, "relu")
         return conv_bn_act(h, self.conv3, self.bn3, "relu", residual=res,
                            want_preact=self.is_last and self._need_preact,

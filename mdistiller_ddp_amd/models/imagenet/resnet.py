@@ -53,8 +53,8 @@ class BasicBlock(nn.Module):
 
     def forward(self, x):
         fork = grad_fork(x)
-        res, res_fork = self._res(x, fork)
         h, _ = conv_bn_act(x, self.conv1, self.bn1, "relu", fork=fork)
+        res, res_fork = self._res(x, fork)  # after conv1: its backward runs first
         return conv_bn_act(h, self.conv2, self.bn2, "relu", residual=res,
                            want_preact=self.is_last and self._need_preact, res_fork=res_fork)
 
@@ -78,8 +78,8 @@ class Bottleneck(BasicBlock):
 
     def forward(self, x):
         fork = grad_fork(x)
-        res, res_fork = self._res(x, fork)
         h, _ = conv_bn_act(x, self.conv1, self.bn1, "relu", fork=fork)
+        res, res_fork = self._res(x, fork)  # after conv1: its backward runs first
         h, _ = conv_bn_act(h, self.conv2, self.bn2, "relu")
         return conv_bn_act(h, self.conv3, self.bn3, "relu", residual=res,
                            want_preact=self.is_last and self._need_preact, res_fork=res_fork)

@@ -550,6 +550,9 @@ def _fork_sum(fork, g):
 class _ConvBNActTrain(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, gamma, beta, residual, meta, bn, want_preact, forks=(None, None)):
+        # an unused output (the pre-activation) must not be materialised as a
+        # zero gradient + layout copy: the kernels take null dout / dpre
+        ctx.set_materialize_grads(False)
         stride, pad, act = meta[:3]
         if len(meta) > 3 and meta[3] == "dw":
             ctx.forks = (None, None)
@@ -855,6 +858,7 @@ class _ConvTrain(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, residual, meta, want_preact):
+        ctx.set_materialize_grads(False)
         stride, pad, act = meta
         need_dx = ctx.needs_input_grad[0]
         cin_w = weight.shape[1]
@@ -962,6 +966,7 @@ class _BNActTrain(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, gamma, beta, residual, bn, act, want_preact):
+        ctx.set_materialize_grads(False)
         y = _cl_bf16(x)
         N, C, H, W = y.shape
         M = N * H * W

@@ -37,7 +37,21 @@ def activate(x: torch.Tensor, act: str) -> torch.Tensor:
     raise ValueError(act)
 
 
+# Train-mode BatchNorms that ran WITHOUT autograd on the PyTorch/MIOpen path
+# (e.g. a frozen teacher kept in train-mode BN by OFD whose layer the native
+# no-grad kernels do not serve).  MIOpen's bf16 train-mode BN replayed from a
+# hipGraph went non-finite (profiles/r1_ofd_graph_ab.md), so a distiller that
+# captures such a teacher checks this counter after its eager warm-up.
+_TRAINBN_FALLBACKS = {"n": 0}
+
+
+def trainbn_fallbacks() -> int:
+    return _TRAINBN_FALLBACKS["n"]
+
+
 def _bn(x: torch.Tensor, bn: nn.BatchNorm2d) -> torch.Tensor:
+    if bn.training and not torch.is_grad_enabled():
+        _TRAINBN_FALLBACKS["n"] += 1
     return bn(x)
 
 
@@ -302,10 +316,20 @@ class MaxPool2d(nn.MaxPool2d):
         return max_pool2d(x, self.kernel_size, self.stride, self.padding)
 
 
+_GRAD_FORKS = {"on": True}
+
+
+def set_grad_forks(flag: bool) -> None:
+    """A/B switch: residual-fork gradients summed in the native dgrad epilogue
+    (default) or by autograd."""
+    _GRAD_FORKS["on"] = bool(flag)
+
+
 def grad_fork(x: torch.Tensor):
     """A :class:`ops.hip_train.GradFork` for an activation with two native
     consumers (training on the HIP path), else None."""
-    if not (torch.is_grad_enabled() and x.requires_grad and hip_enabled_for(x)):
+    if not (_GRAD_FORKS["on"] and torch.is_grad_enabled() and x.requires_grad
+            and hip_enabled_for(x)):
         return None
     from . import hip_train
     return hip_train.GradFork()

@@ -95,6 +95,7 @@ class GradReducer:
         self._pending = []
         self._next = 0
         self._works = {}
+        self._wires = {}
         self._hooks = []
         self._armed = False
         if self.overlap:
@@ -119,6 +120,13 @@ class GradReducer:
             return
         b = self._param_bucket[i]
         self._pending[b] -= 1
+        if self._pending[b] < 0 and b in self._works:
+            # more contributions than the calibration step counted, after the
+            # bucket was already all-reduced: the reduced values are stale
+            raise RuntimeError(
+                f"GradReducer: parameter {i} received a gradient contribution after its "
+                f"bucket {b} was launched (calibrated {self._expected[i] if self._expected else '?'} "
+                "contributions); disable DIST.OVERLAP or keep the backward graph static")
         # strictly in bucket order: every rank issues the same collective
         # sequence even if two buckets complete in a different order
         while self._next < len(self.buckets) and self._pending[self._next] <= 0:
@@ -135,12 +143,20 @@ class GradReducer:
         s, e, _ = self.buckets[b]
         return self.flat.grads[self.flat._bound][s:e]
 
+    def _wire_buf(self, key, n, device):
+        """Persistent bf16 wire buffer (allocated once, reused every step)."""
+        w = self._wires.get(key)
+        if w is None or w.numel() != n or w.device != device:
+            w = self._wires[key] = torch.empty(n, dtype=torch.bfloat16, device=device)
+        return w
+
     def _launch(self, b, async_op):
         t = self._slice(b)
         self.bytes_reduced += t.numel() * (2 if self.wire_bf16 else 4)
         self.calls += 1
         if self.wire_bf16:
-            tb = t.to(torch.bfloat16)
+            tb = self._wire_buf(("b", b), t.numel(), t.device)
+            tb.copy_(t)
             work = dist.all_reduce(tb, group=self.group, async_op=True)
             self._works[b] = (work, t, tb)
         else:
@@ -168,6 +184,10 @@ class GradReducer:
             return
         if self._calib is not None:
             self._expected, self._calib = self._calib, None
+        elif self._armed and any(p < 0 for p in self._pending):
+            raise RuntimeError(f"GradReducer: bucket contribution counts went negative "
+                               f"{self._pending} (a parameter got more gradient writes than "
+                               f"the calibration step counted)")
         for b in range(len(self.buckets)):
             if b not in self._works:
                 self._launch(b, async_op=True)
@@ -201,7 +221,8 @@ class GradReducer:
         self.bytes_reduced += t.numel() * (2 if self.wire_bf16 else 4)
         self.calls += 1
         if self.wire_bf16:
-            tb = t.to(torch.bfloat16)
+            tb = self._wire_buf(("sets", tuple(sets)), t.numel(), t.device)
+            tb.copy_(t)
             dist.all_reduce(tb, group=self.group)
             t.copy_(tb)
         else:

@@ -168,11 +168,27 @@ class TeacherFeed:
         (``"use"`` mode leaves this to the caller, e.g. DOT's CE-backward graph)."""
         self._pending = run_teacher_async(teacher, self.next_image)
 
-    def finish(self) -> None:
-        """End of a pipelined step: join the prefetch and move it into ``X``."""
+    def finish(self, copy: bool = True) -> None:
+        """End of a pipelined step: join the prefetch and move it into ``X``.
+
+        ``copy=False`` only joins the teacher stream and keeps the result for a
+        later :meth:`commit` -- for a caller whose other work may still read
+        ``X`` concurrently (DOT's KD-backward graph replays beside the CE
+        graph that hosts the prefetch; the copy goes after their join)."""
         if self._pending is not None:
-            _copy_struct(self.X, self._keep(self._pending.get()))
+            out = self._keep(self._pending.get())
             self._pending = None
+            if copy:
+                _copy_struct(self.X, out)
+            else:
+                self._joined = out
+
+    def commit(self) -> None:
+        """Copy a result joined by ``finish(copy=False)`` into ``X``."""
+        out = getattr(self, "_joined", None)
+        if out is not None:
+            _copy_struct(self.X, out)
+            self._joined = None
 
 
 # ---------------------------------------------------------------------------
@@ -186,7 +202,9 @@ class TeacherFeed:
 # caller), so whoever runs the backward joins every branch stream used
 # (``join_branches``) before reading the gradients; hipGraph records the
 # fork/join as parallel branches of the captured step.
-_branch = {"enabled": os.environ.get("MDA_BRANCH_STREAMS", "1") != "0", "used": set()}
+# Off by default: measured slower on every CIFAR student (profiles/r3_branch_fork_ab.md):
+# the captured cross-stream edges cost more than the shortcut overlap saves.
+_branch = {"enabled": os.environ.get("MDA_BRANCH_STREAMS", "0") == "1", "used": set()}
 _branch_streams: dict = {}
 
 

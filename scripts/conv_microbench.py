@@ -29,6 +29,8 @@ SHAPES = [  # N, Cin, H, Cout, k, s, p
     (64, 128, 16, 256, 3, 2, 1),
     (64, 256, 8, 256, 3, 1, 1),
     (64, 64, 32, 128, 1, 2, 0),
+    (64, 128, 16, 256, 1, 2, 0),
+    (64, 32, 32, 64, 1, 1, 0),
 ]
 IMAGENET = [  # ResNet-50 teacher at batch 64, ResNet-18 student at batch 32
     (64, 64, 56, 64, 1, 1, 0),
@@ -51,6 +53,19 @@ IMAGENET = [  # ResNet-50 teacher at batch 64, ResNet-18 student at batch 32
 
 
 def timeit(fn, iters):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) * 1000.0 / iters
+
+
+def timeit_eager(fn, iters):
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
@@ -115,16 +130,29 @@ def main():
         with torch.no_grad():
             t_fwd = timeit(lambda: hip_layers.conv_bn_act(x, conv, bn, "relu", None, False), args.iters) if "fwd" in ops else nan
             wb = conv.weight.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-            t_mio = timeit(lambda: F.conv2d(x, wb, stride=s, padding=p), args.iters) if "mio" in ops else nan
+            t_mio = nan
             dy = torch.randn(N, Cout, Ho, Ho, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
             t_wg = timeit(lambda: hip_train.conv_wgrad(x, dy, tuple(conv.weight.shape), s, p), args.iters) if "wgrad" in ops else nan
             t_dg = nan
             if Cin % 8 == 0 and "dgrad" in ops:
                 t_dg = timeit(lambda: hip_train.conv_dgrad(dy, conv.weight, tuple(x.shape), s, p), args.iters)
+        # MIOpen (bf16 channels-last) forward / dgrad / wgrad, timed eagerly
+        # (its solvers are not capturable): event time per call over `iters`
+        t_mio_dg = t_mio_wg = nan
+        if "mio" in ops:
+            wb = conv.weight.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+            t_mio = timeit_eager(lambda: F.conv2d(x, wb, stride=s, padding=p), args.iters)
+            t_mio_dg = timeit_eager(lambda: torch.ops.aten.convolution_backward(
+                dy, x, wb, None, (s, s), (p, p), (1, 1), False, (0, 0), 1, (True, False, False)),
+                args.iters)
+            t_mio_wg = timeit_eager(lambda: torch.ops.aten.convolution_backward(
+                dy, x, wb, None, (s, s), (p, p), (1, 1), False, (0, 0), 1, (False, True, False)),
+                args.iters)
         row = dict(shape=[N, Cin, H, Cout, k, s, p], gflop=flop / 1e9, fwd_us=t_fwd,
                    fwd_tflops=flop / t_fwd / 1e6, miopen_fwd_us=t_mio, dgrad_us=t_dg,
                    wgrad_us=t_wg, wgrad_tflops=flop / t_wg / 1e6, dgrad_tflops=flop / t_dg / 1e6,
-                   miopen_tflops=flop / t_mio / 1e6)
+                   miopen_tflops=flop / t_mio / 1e6, miopen_dgrad_us=t_mio_dg,
+                   miopen_wgrad_us=t_mio_wg)
         rows.append(row)
         print(json.dumps({k_: (round(v, 2) if isinstance(v, float) else v) for k_, v in row.items()}),
               flush=True)

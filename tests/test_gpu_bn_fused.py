@@ -181,8 +181,10 @@ def test_residual_block_grad_fork(inplanes, planes, stride, branch):
     """A CIFAR BasicBlock on the native path: x's two consumers (conv1 and the
     identity / projection shortcut) sum their input gradients in the second
     consumer's dgrad epilogue (GradFork), the projection running on the
-    branch stream -- vs the fp32 PyTorch block."""
+    branch stream -- vs the same native block with autograd's add (tight) and
+    vs the fp32 PyTorch block (bf16 band)."""
     from mdistiller_ddp_amd.models.cifar.resnet import BasicBlock
+    from mdistiller_ddp_amd.ops import nn as mda_nn
     from mdistiller_ddp_amd.ops.backend import use_backend
     from mdistiller_ddp_amd.runtime import streams
     torch.manual_seed(3)
@@ -190,25 +192,36 @@ def test_residual_block_grad_fork(inplanes, planes, stride, branch):
     if stride != 1 or inplanes != planes:
         ds = nn.Sequential(nn.Conv2d(inplanes, planes, 1, stride, bias=False), nn.BatchNorm2d(planes))
     blk = BasicBlock(inplanes, planes, stride, ds).cuda().to(memory_format=torch.channels_last)
-    ref = copy.deepcopy(blk)
+    blk_nf, ref = copy.deepcopy(blk), copy.deepcopy(blk)
     x = torch.randn(32, inplanes, 16, 16, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     g = torch.randn(32, planes, 16 // stride, 16 // stride, device="cuda").to(torch.bfloat16)
-    streams.set_branches(branch)
-    try:
-        x1 = x.clone().requires_grad_(True)
-        with use_backend("hip"), torch.autocast("cuda", dtype=torch.bfloat16):
-            out, _ = blk(x1)
-        out.backward(g)
-        torch.cuda.current_stream().wait_stream(streams.branch_stream(x.device))
-    finally:
-        streams.set_branches(True)
+
+    def run(m, forks):
+        mda_nn.set_grad_forks(forks)
+        streams.set_branches(branch)
+        try:
+            xx = x.clone().requires_grad_(True)
+            with use_backend("hip"), torch.autocast("cuda", dtype=torch.bfloat16):
+                out, _ = m(xx)
+            out.backward(g)
+            torch.cuda.current_stream().wait_stream(streams.branch_stream(x.device))
+        finally:
+            mda_nn.set_grad_forks(True)
+            streams.set_branches(True)
+        return out, xx.grad
+
+    out, dx = run(blk, True)
+    out_nf, dx_nf = run(blk_nf, False)
     x2 = x.float().clone().requires_grad_(True)
     with use_backend("torch"):
         o2, _ = ref(x2)
     o2.backward(g.float())
     torch.cuda.synchronize()
-    rel = lambda a, b: ((a.float() - b).norm() / b.norm()).item()  # noqa: E731
+    rel = lambda a, b: ((a.float() - b.float()).norm() / b.float().norm()).item()  # noqa: E731
+    assert rel(dx, dx_nf) < 1e-2
+    for (n, p), (_, q) in zip(blk.named_parameters(), blk_nf.named_parameters()):
+        assert rel(p.grad, q.grad) < 1e-2, n
     assert rel(out, o2) < 2e-2
-    assert rel(x1.grad, x2.grad) < 5e-2
+    assert rel(dx, x2.grad) < 1e-1
     for (n, p), (_, q) in zip(blk.named_parameters(), ref.named_parameters()):
-        assert rel(p.grad, q.grad) < 5e-2, n
+        assert rel(p.grad, q.grad) < 1e-1, n

@@ -181,6 +181,28 @@ def test_ofd_train_bn_teacher_graph_bf16_tracks_fp32_eager():
     assert abs(losses[0] - losses[1]) / abs(losses[1]) < 2e-2, losses
 
 
+def test_ofd_train_bn_teacher_not_served_natively_stays_eager():
+    """OFD with a VGG13 teacher (conv biases: its train-mode BNs run on MIOpen,
+    not the capture-safe native kernels): the eager warm-up counts the
+    fallbacks and the step is never captured, and it stays finite."""
+    torch.manual_seed(0)
+    cfg = _cfg("OFD")
+    cfg.DISTILLER.TEACHER = "vgg13"
+    cfg.DISTILLER.STUDENT = "vgg8"
+    d = build_distiller(cfg, 100, "cuda")
+    d.train()
+    st = TrainStep(d, cfg, "cuda", use_graph=True, dtype=torch.bfloat16)
+    st.set_epoch(1.0)
+    ld = SyntheticLoader("cifar100", 64, "cuda", steps_per_epoch=6, channels_last=True)
+    for b in ld:
+        st.step(b)
+    torch.cuda.synchronize()
+    assert not d.graph_capturable
+    assert st._graphs is None and not st.use_graph
+    loss = st.meters.summary(reduce=False)["loss"]
+    assert loss == loss and abs(loss) < 1e6
+
+
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("typ", ["KD", "DKD"])
 def test_native_bf16_tracks_fp32_over_300_steps(typ):

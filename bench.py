@@ -140,6 +140,8 @@ def main():
             },
             "replicas_identical": r.get("replicas_identical"),
             "final_loss": round(r["final_loss"], 4),
+            "host_ms_per_step": round(r["host_ms_per_step"], 4),
+            "host_idle_ms_per_step": round(r["host_idle_ms_per_step"], 4),
         }
         print(json.dumps(out), flush=True)
     D.destroy()

@@ -121,6 +121,7 @@ def run(cfg_file: str, per_gpu_batch: int, steps: int, warmup: int, opts=(), use
     t0 = time.perf_counter()
     for _ in range(steps):
         cur = advance(cur)
+    host = time.perf_counter() - t0  # host time to enqueue the K steps (launch-bound if ~el)
     sync()
     D.barrier()
     sync()
@@ -129,6 +130,15 @@ def run(cfg_file: str, per_gpu_batch: int, steps: int, warmup: int, opts=(), use
     if D.is_dist():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
     el = float(t.item())
+    # host cost of enqueueing one step with an idle GPU (no queue back-pressure):
+    # the launch-bound floor of the step
+    hs = []
+    for _ in range(10):
+        sync()
+        h0 = time.perf_counter()
+        cur = advance(cur)
+        hs.append(time.perf_counter() - h0)
+    sync()
     m = step.meters.summary(reduce=True)
     n = info.world_size
     same = None
@@ -143,6 +153,8 @@ def run(cfg_file: str, per_gpu_batch: int, steps: int, warmup: int, opts=(), use
     return {
         "seconds": el,
         "ms_per_step": 1000.0 * el / steps,
+        "host_ms_per_step": 1000.0 * host / steps,
+        "host_idle_ms_per_step": 1000.0 * sorted(hs)[len(hs) // 2],
         "images_per_s": n * per_gpu_batch * steps / el,
         "n_gpus": n,
         "global_batch": n * per_gpu_batch,

@@ -46,6 +46,7 @@ SIGNATURES = {
     "mda_conv_fwd_bnstats": "ppppp" + "i" * 15 + "p" * 8 + "ff" + "ps",
     "mda_conv_dgrad": "pppp" + "i" * 14 + "s",
     "mda_conv_dgrad_res": "ppppp" + "i" * 14 + "s",
+    "mda_conv_dgrad_bnsum": "ppppp" + "i" * 14 + "ppp" + "i" + "p" + "s",
     "mda_conv_wgrad": "pppp" + "i" * 13 + "fiiis",
     "mda_conv_wgrad_nored": "pppp" + "i" * 13 + "fiiis",
     "mda_wgrad_reduce_multi": "pis",
@@ -79,6 +80,7 @@ SIGNATURES = {
     "mda_bn_stats_acc": "piips",
     "mda_bn_apply_fin": "ppii" + "ppppp" + "ff" + "p" + "ppp" + "i" + "s",
     "mda_bn_bwd_fused": "ppppp" + "p" + "iii" + "pp" + "pp" + "ppp" + "s",
+    "mda_bn_bwd_apply_reg": "pppp" + "p" + "iii" + "p" + "pp" + "ppp" + "s",
     "mda_conv_fwd_bnacc": "ppppp" + "i" * 14 + "s",
     # CRD memory (csrc/crd.hip)
     "mda_crd_scores": "ppppiiifs",

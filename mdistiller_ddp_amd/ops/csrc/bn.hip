@@ -925,6 +925,86 @@ bn_bwd_fused_kernel(BwdArgs a) {
   }
 }
 
+// BN backward whose channel sums a producer already added into the region
+// (the dgrad epilogue of the consuming conv, conv_igemm.hip
+// mda_conv_dgrad_bnsum): one streaming pass, no reduction and no grid
+// barrier.  dz = dout * act'(z) (+ dpre), dy = scale*(dz - (sum dz +
+// xhat*sum dz*xhat)/M), dres = dz; block 0 accumulates dgamma / dbeta (and
+// writes sums).  The thread's APPLY_V vectors are loaded before the
+// prologue reads the region, so both latencies overlap.
+__global__ void __launch_bounds__(256)
+bn_bwd_apply_reg_kernel(BwdArgs a) {
+  // per-channel operands in LDS: a thread's channel group changes along the
+  // grid stride when C / 8 is not a power of two (MobileNetV2 widths)
+  __shared__ float s_m0[SLOT_CMAX], s_m1[SLOT_CMAX], s_st[4][SLOT_CMAX];
+  const int C = a.C;
+  const int c8 = C / 8;
+  const int64_t total = (int64_t)a.M * c8;
+  const int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  Raw8 raw[APPLY_V];
+#pragma unroll
+  for (int k = 0; k < APPLY_V; ++k) {
+    const int64_t i = i0 + k * stride;
+    bwd_load8(a, (i < total ? i : 0) * 8, raw[k]);
+  }
+  {
+    const float invM = 1.f / (float)a.M;
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      double d0, d1;
+      region_channel<false>(a.reg, C, c, d0, d1);
+      const float t0 = (float)d0, t1 = (float)d1;
+      s_m0[c] = t0 * invM;
+      s_m1[c] = t1 * invM;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) s_st[q][c] = a.stats[q * C + c];
+      if (blockIdx.x == 0) {
+        if (a.sums) { a.sums[c] = t0; a.sums[C + c] = t1; }
+        if (a.dbeta) a.dbeta[c] += t0;
+        if (a.dgamma) a.dgamma[c] += t1;
+      }
+    }
+  }
+  __syncthreads();
+  auto emit = [&](int64_t i, const Raw8& v) {
+    const int c0 = (int)(i % c8) * 8;
+    float sc[8], sh[8], mu[8], rs[8], dz[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      mu[e] = s_st[0][c0 + e]; rs[e] = s_st[1][c0 + e];
+      sc[e] = s_st[2][c0 + e]; sh[e] = s_st[3][c0 + e];
+    }
+    bwd_dz8(a, v, sc, sh, dz);
+    const uint32_t yw[4] = {v.y.x, v.y.y, v.y.z, v.y.w};
+    uint32_t go[4], ro[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      float g[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int e = 2 * w + h;
+        const float yf = h ? __uint_as_float(yw[w] & 0xffff0000u) : __uint_as_float(yw[w] << 16);
+        const float xhat = (yf - mu[e]) * rs[e];
+        g[h] = sc[e] * (dz[e] - (s_m0[c0 + e] + xhat * s_m1[c0 + e]));
+      }
+      go[w] = pack_bf16x2(g[0], g[1]);
+      ro[w] = pack_bf16x2(dz[2 * w], dz[2 * w + 1]);
+    }
+    *(uint4*)(a.dy + i * 8) = make_uint4(go[0], go[1], go[2], go[3]);
+    if (a.dres) *(uint4*)(a.dres + i * 8) = make_uint4(ro[0], ro[1], ro[2], ro[3]);
+  };
+#pragma unroll
+  for (int k = 0; k < APPLY_V; ++k) {
+    const int64_t i = i0 + k * stride;
+    if (i < total) emit(i, raw[k]);
+  }
+  for (int64_t i = i0 + APPLY_V * stride; i < total; i += stride) {
+    Raw8 v;
+    bwd_load8(a, i * 8, v);
+    emit(i, v);
+  }
+}
+
 int g_num_cus = 0;
 
 int num_cus() {
@@ -1002,5 +1082,20 @@ MDA_API int mda_bn_bwd_fused(const void* dout, const void* dout2, const void* dp
   else if (per <= 4) hipLaunchKernelGGL((bn_bwd_fused_kernel<4, true>), dim3(nb), dim3(256), 0, st, a);
   else if (per <= 8) hipLaunchKernelGGL((bn_bwd_fused_kernel<8, true>), dim3(nb), dim3(256), 0, st, a);
   else hipLaunchKernelGGL((bn_bwd_fused_kernel<1, false>), dim3(nb), dim3(256), 0, st, a);
+  MDA_CHECK_LAUNCH();
+}
+
+// BN backward on sums already in `region` (a dgrad epilogue produced them,
+// conv_igemm.hip mda_conv_dgrad_bnsum): one streaming launch.
+MDA_API int mda_bn_bwd_apply_reg(const void* dout, const void* dpre, const void* y, const void* res,
+                                 const float* stats, int64_t M, int64_t C, int64_t act,
+                                 void* region, void* dy, void* dres, float* dgamma, float* dbeta,
+                                 float* sums, hipStream_t st) {
+  if (C % 8 || C > SLOT_CMAX || M <= 0 || M >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
+  BwdArgs a{(const bf16_t*)dout, nullptr, (const bf16_t*)dpre, (const bf16_t*)y,
+            (const bf16_t*)res, stats, (bf16_t*)dy, (bf16_t*)dres, dgamma, dbeta, sums,
+            (BnRegion*)region, nullptr, (int)M, (int)C, (int)act};
+  const int nb = apply_blocks(M * C / 8, APPLY_V);
+  hipLaunchKernelGGL(bn_bwd_apply_reg_kernel, dim3(nb), dim3(256), 0, st, a);
   MDA_CHECK_LAUNCH();
 }

@@ -75,6 +75,19 @@ struct ConvParams {
   // diagnostics: per-block phase timestamps (s_memrealtime, 100 MHz), null in
   // normal runs (mda_conv_set_stamps)
   uint64_t* stamps;
+  // BN-backward sums (dgrad only): this dgrad's output is the gradient dout of
+  // a training BN layer's output act(y*scale + shift (+ bnb_res)); besides the
+  // bf16 dout the epilogue adds that layer's sum dz and sum dz*xhat
+  // (dz = dout * act'(z), xhat = (y - mean) * rstd) into shard
+  // blockIdx.x % slot_shards(Cout) of bnb_slot, so the BN backward is one
+  // streaming pass (csrc/bn.hip mda_bn_bwd_apply_reg) instead of a
+  // reduction + grid barrier + apply.  bnb_stats: [4][Cout] mean, rstd,
+  // scale, shift of that layer.
+  const bf16_t* bnb_y;
+  const bf16_t* bnb_res;
+  const float* bnb_stats;
+  BnRegion* bnb_slot;
+  int bnb_act;
 };
 
 __device__ __forceinline__ void stamp(const ConvParams& p, int k) {
@@ -244,8 +257,8 @@ __device__ __forceinline__ void epi_prefetch(const ConvParams& p, EpiPre<BM, BN,
   const int c8 = tid % E::TPR, rr = tid / E::TPR;
   const int co = n0 + c8 * 8;
   const bool split = par ? p.zsplits > 1 : gridDim.z > 1;
-  e.have = !split && p.stats_part == nullptr && p.stats_slot == nullptr && (p.Cout & 7) == 0 &&
-           co < p.Cout;
+  e.have = !split && p.stats_part == nullptr && p.stats_slot == nullptr && p.bnb_slot == nullptr &&
+           (p.Cout & 7) == 0 && co < p.Cout;
   e.have_res = false;
   if (!e.have) return;
   load_scale_bias8(p, co, e.sc, e.bi);
@@ -265,6 +278,108 @@ template <int BM, int BN, int NT = 256>
 __device__ __forceinline__ void conv_epilogue_rows(const ConvParams& p, char* smem, int m0, int n0,
                                                    int rows, const ParClass& pc, bool has_pc,
                                                    const EpiPre<BM, BN, NT>& pre);
+
+__device__ __forceinline__ float bnb_act_grad(float z, int act) {
+  if (act == ACT_RELU) return z > 0.f ? 1.f : 0.f;
+  if (act == ACT_RELU6) return (z > 0.f && z < 6.f) ? 1.f : 0.f;
+  return 1.f;
+}
+
+// BN-backward epilogue of a dgrad (see ConvParams::bnb_*): store
+// dout = acc (+ res) in bf16, then sum dz and dz*xhat of the STORED values
+// over the block's rows and add them into the region (what the streaming
+// apply recomputes dz from).  Every load of a thread's rows (C tile, BN
+// input y, its residual, the fork gradient) is issued before any math.
+template <int BM, int BN, int NT>
+__device__ __forceinline__ void conv_epilogue_bnb(const ConvParams& p, float* Cs, int m0, int n0,
+                                                  int rows, const ParClass& pc, bool has_pc) {
+  constexpr int CS = ConvSmem<BM, BN>::CS;
+  constexpr int TPR = BN / 8;
+  constexpr int RPP = NT / TPR;
+  constexpr int RPT = (BM + RPP - 1) / RPP;
+  const int tid = threadIdx.x;
+  const int c8 = tid % TPR, rr = tid / TPR;
+  const int co = n0 + c8 * 8;
+  const int C = p.Cout;
+  const int mlim = has_pc ? pc.Mc : p.M;
+  const bool cok = co < C;
+  const bool zres = p.bnb_res != nullptr && p.bnb_act != ACT_NONE;
+  float mu[8], rs[8], sc[8], sh[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    mu[e] = cok ? p.bnb_stats[co + e] : 0.f;
+    rs[e] = cok ? p.bnb_stats[C + co + e] : 0.f;
+    sc[e] = cok ? p.bnb_stats[2 * C + co + e] : 0.f;
+    sh[e] = cok ? p.bnb_stats[3 * C + co + e] : 0.f;
+  }
+  uint4 yv[RPT], rv[RPT], gv[RPT];
+  int mrow[RPT];
+#pragma unroll
+  for (int k = 0; k < RPT; ++k) {
+    const int r0 = rr + k * RPP;
+    int m = m0 + r0;
+    const bool ok = cok && r0 < rows && m < mlim;
+    if (ok && has_pc) m = par_row(p, pc, m);
+    mrow[k] = ok ? m : -1;
+    const int64_t o = (int64_t)(ok ? m : 0) * C + (cok ? co : 0);
+    yv[k] = ok ? *(const uint4*)(p.bnb_y + o) : make_uint4(0u, 0u, 0u, 0u);
+    rv[k] = (ok && zres) ? *(const uint4*)(p.bnb_res + o) : make_uint4(0u, 0u, 0u, 0u);
+    gv[k] = (ok && p.res) ? *(const uint4*)(p.res + o) : make_uint4(0u, 0u, 0u, 0u);
+  }
+  float s1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, s2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < RPT; ++k) {
+    if (mrow[k] < 0) continue;
+    const int r0 = rr + k * RPP;
+    const float4 lo = *(const float4*)&Cs[r0 * CS + c8 * 8];
+    const float4 hi = *(const float4*)&Cs[r0 * CS + c8 * 8 + 4];
+    float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    const uint32_t gw[4] = {gv[k].x, gv[k].y, gv[k].z, gv[k].w};
+    const uint32_t yw[4] = {yv[k].x, yv[k].y, yv[k].z, yv[k].w};
+    const uint32_t rw[4] = {rv[k].x, rv[k].y, rv[k].z, rv[k].w};
+    uint32_t ow[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      if (p.res) {
+        v[2 * w] += __uint_as_float(gw[w] << 16);
+        v[2 * w + 1] += __uint_as_float(gw[w] & 0xffff0000u);
+      }
+      ow[w] = pack_bf16x2(v[2 * w], v[2 * w + 1]);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int e = 2 * w + h;
+        float d = h ? __uint_as_float(ow[w] & 0xffff0000u) : __uint_as_float(ow[w] << 16);
+        const float yf = h ? __uint_as_float(yw[w] & 0xffff0000u) : __uint_as_float(yw[w] << 16);
+        if (p.bnb_act != ACT_NONE) {
+          float z = yf * sc[e] + sh[e];
+          if (zres) z += h ? __uint_as_float(rw[w] & 0xffff0000u) : __uint_as_float(rw[w] << 16);
+          d *= bnb_act_grad(z, p.bnb_act);
+        }
+        s1[e] += d;
+        s2[e] += d * ((yf - mu[e]) * rs[e]);
+      }
+    }
+    *(uint4*)(p.y + (int64_t)mrow[k] * C + co) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+  }
+  __syncthreads();  // every read of the C tile is done: reuse it for the reduction
+  float* red = Cs;  // [2][RPP][BN]
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[(0 * RPP + rr) * BN + c8 * 8 + e] = s1[e];
+    red[(1 * RPP + rr) * BN + c8 * 8 + e] = s2[e];
+  }
+  __syncthreads();
+  if (tid < 2 * BN) {
+    const int q = tid / BN, c = tid - q * BN;
+    float a0 = 0.f, a1 = 0.f;
+    for (int r = 0; r < RPP; r += 2) {
+      a0 += red[(q * RPP + r) * BN + c];
+      a1 += red[(q * RPP + r + 1) * BN + c];
+    }
+    if (n0 + c < C)
+      acc_add(region_acc(p.bnb_slot, C, (int)blockIdx.x % slot_shards(C), q) + n0 + c, (double)(a0 + a1));
+  }
+}
 
 template <int BM, int BN>
 __device__ __forceinline__ void conv_epilogue(const ConvParams& p, const f32x4 (&acc)[BM / 32][BN / 32],
@@ -295,6 +410,10 @@ __device__ __forceinline__ void conv_epilogue_rows(const ConvParams& p, char* sm
   const int zsplit = has_pc ? (int)blockIdx.z % p.zsplits : (int)blockIdx.z;
   const bool split = has_pc ? p.zsplits > 1 : gridDim.z > 1;
   const int mlim = has_pc ? pc.Mc : p.M;
+  if (p.bnb_slot != nullptr) {
+    conv_epilogue_bnb<BM, BN, NT>(p, Cs, m0, n0, rows, pc, has_pc);
+    return;
+  }
   if (p.stats_part != nullptr || p.stats_slot != nullptr) {
     // raw bf16 output + BN statistics partials of this block's rows.  No early
     // return before the barrier: threads past Cout just contribute zeros.
@@ -1732,7 +1851,7 @@ MDA_API int mda_conv_fwd(const void* x, const void* w, const float* scale, const
                          int64_t H, int64_t W, int64_t Cin, int64_t Ho, int64_t Wo, int64_t Cout,
                          int64_t KH, int64_t KW, int64_t stride, int64_t pad, int64_t Kp,
                          int64_t act, int64_t tile, int64_t splits, hipStream_t st) {
-  ConvParams p;
+  ConvParams p{};
   p.x = (const bf16_t*)x; p.w = (const bf16_t*)w; p.scale = scale; p.bias = bias;
   p.res = (const bf16_t*)res; p.y = (bf16_t*)y; p.preact = (bf16_t*)preact; p.partial = partial;
   p.N = N; p.H = H; p.W = W; p.Cin = Cin; p.Ho = Ho; p.Wo = Wo; p.Cout = Cout; p.KH = KH;
@@ -1757,6 +1876,14 @@ MDA_API int mda_conv_dgrad_res(const void* dy, const void* wt, void* dx, float* 
                                int64_t stride, int64_t pad, int64_t Kp, int64_t tile,
                                int64_t splits, hipStream_t st);
 
+MDA_API int mda_conv_dgrad_bnsum(const void* dy, const void* wt, void* dx, float* partial,
+                                 const void* res, int64_t N, int64_t H, int64_t W, int64_t Cin,
+                                 int64_t Ho, int64_t Wo, int64_t Cout, int64_t KH, int64_t KW,
+                                 int64_t stride, int64_t pad, int64_t Kp, int64_t tile,
+                                 int64_t splits, const void* bn_y, const void* bn_res,
+                                 const float* bn_stats, int64_t bn_act, void* region,
+                                 hipStream_t st);
+
 MDA_API int mda_conv_dgrad(const void* dy, const void* wt, void* dx, float* partial, int64_t N,
                            int64_t H, int64_t W, int64_t Cin, int64_t Ho, int64_t Wo,
                            int64_t Cout, int64_t KH, int64_t KW, int64_t stride, int64_t pad,
@@ -1773,8 +1900,33 @@ MDA_API int mda_conv_dgrad_res(const void* dy, const void* wt, void* dx, float* 
                                int64_t Ho, int64_t Wo, int64_t Cout, int64_t KH, int64_t KW,
                                int64_t stride, int64_t pad, int64_t Kp, int64_t tile,
                                int64_t splits, hipStream_t st) {
+  return mda_conv_dgrad_bnsum(dy, wt, dx, partial, res, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride,
+                              pad, Kp, tile, splits, nullptr, nullptr, nullptr, 0, nullptr, st);
+}
+
+// dx = dgrad(dy) (+ res) that also adds the BN-backward sums of the layer
+// whose output gradient dx is (ConvParams::bnb_*): bn_y = that BN's input
+// [N, H, W, Cin], bn_res = its residual (or null), bn_stats = its [4][Cin]
+// mean / rstd / scale / shift, bn_act its activation, region a fresh zeroed
+// BnRegion for Cin channels.  Requires splits == 1 (the split-K combine has
+// no reduction epilogue) and Cin % 8 == 0.
+MDA_API int mda_conv_dgrad_bnsum(const void* dy, const void* wt, void* dx, float* partial,
+                                 const void* res, int64_t N, int64_t H, int64_t W, int64_t Cin,
+                                 int64_t Ho, int64_t Wo, int64_t Cout, int64_t KH, int64_t KW,
+                                 int64_t stride, int64_t pad, int64_t Kp, int64_t tile,
+                                 int64_t splits, const void* bn_y, const void* bn_res,
+                                 const float* bn_stats, int64_t bn_act, void* region,
+                                 hipStream_t st) {
   if (Cout % 8) return (int)hipErrorInvalidValue;
-  ConvParams p;
+  if (region != nullptr && (splits != 1 || Cin % 8 || Cin > SLOT_CMAX || bn_y == nullptr ||
+                            bn_stats == nullptr))
+    return (int)hipErrorInvalidValue;
+  ConvParams p{};
+  p.bnb_y = (const bf16_t*)bn_y;
+  p.bnb_res = (const bf16_t*)bn_res;
+  p.bnb_stats = bn_stats;
+  p.bnb_slot = (BnRegion*)region;
+  p.bnb_act = (int)bn_act;
   p.x = (const bf16_t*)dy; p.w = (const bf16_t*)wt; p.scale = nullptr; p.bias = nullptr;
   p.res = (const bf16_t*)res; p.y = (bf16_t*)dx; p.preact = nullptr; p.partial = partial;
   // GEMM view: rows = dx pixels, cols = Cin, k = (tap, co); "input" image = dy
@@ -1819,7 +1971,7 @@ MDA_API int mda_conv_fwd_bnstats(const void* x, const void* w, void* y, float* p
                                  const float* beta, float* running_mean, float* running_var,
                                  float* mean, float* rstd, float* scale, float* shift,
                                  float momentum, float eps, int64_t* nbt, hipStream_t st) {
-  ConvParams p;
+  ConvParams p{};
   p.x = (const bf16_t*)x; p.w = (const bf16_t*)w; p.scale = nullptr; p.bias = nullptr;
   p.res = nullptr; p.y = (bf16_t*)y; p.preact = nullptr; p.partial = partial;
   p.N = N; p.H = H; p.W = W; p.Cin = Cin; p.Ho = Ho; p.Wo = Wo; p.Cout = Cout; p.KH = KH;
@@ -1867,7 +2019,7 @@ MDA_API int mda_conv_fwd_bnacc(const void* x, const void* w, void* y, float* par
                                int64_t Wo, int64_t Cout, int64_t KH, int64_t KW, int64_t stride,
                                int64_t pad, int64_t Kp, int64_t tile, int64_t splits,
                                hipStream_t st) {
-  ConvParams p;
+  ConvParams p{};
   p.x = (const bf16_t*)x; p.w = (const bf16_t*)w; p.scale = nullptr; p.bias = nullptr;
   p.res = nullptr; p.y = (bf16_t*)y; p.preact = nullptr; p.partial = partial;
   p.N = N; p.H = H; p.W = W; p.Cin = Cin; p.Ho = Ho; p.Wo = Wo; p.Cout = Cout; p.KH = KH;

@@ -246,7 +246,62 @@ def _bn_bwd_reduce(dout, dpre, y, res, stats, M, C, act, ws, sums, dg, db):
               M, C, act, ws.partial, sums, dg, db)
 
 
-def _bn_bwd(dout, dpre, y, res, stats, gamma, beta, M, C, act, need_res, direct_gb):
+class BnLink:
+    """A training BN layer's output, as seen by the conv that consumes it.
+
+    The consumer's dgrad produces exactly this layer's output gradient, so its
+    epilogue can also add the layer's backward channel sums (sum dz,
+    sum dz*xhat) into a fresh region (``mda_conv_dgrad_bnsum``, :meth:`arm`);
+    the layer's backward then runs ONE streaming pass on them
+    (``mda_bn_bwd_apply_reg``) instead of a reduction + grid barrier + apply.
+    The sums are used only if the gradient the layer receives IS that dgrad
+    output, unmodified (:meth:`take`): if autograd summed another gradient into
+    it (a feature loss on the activation, a second consumer on a non-native
+    path) the tensor differs and the layer falls back to the full backward.
+    The link keeps a reference to the armed tensor, so autograd never
+    accumulates into it in place.
+    """
+
+    __slots__ = ("y", "res", "stats", "act", "M", "C", "dout", "ver", "region")
+
+    def __init__(self, y, res, stats, act, M, C):
+        self.y, self.res, self.stats, self.act, self.M, self.C = y, res, stats, act, M, C
+        self.dout = self.region = None
+        self.ver = -1
+
+    def arm(self, dout, region) -> None:
+        self.dout, self.ver, self.region = dout, dout._version, region
+
+    def take(self, dout):
+        d, r = self.dout, self.region
+        self.dout = self.region = None
+        if d is not None and d is dout and dout._version == self.ver:
+            _BNB_COUNT[0] += 1
+            return r
+        if d is not None:
+            _BNB_COUNT[1] += 1
+        return None
+
+
+_BNB_COUNT = [0, 0]  # BN backwards on dgrad-epilogue sums / armed links that fell back
+_BNB_ON = [os.environ.get("MDA_BN_DGRAD_SUMS", "1") != "0"]
+_LAST_LINK = [None]
+
+
+def set_bn_dgrad_sums(on: bool) -> None:
+    """BN-backward sums in the consumer dgrad's epilogue (BnLink) on / off (A/B)."""
+    _BNB_ON[0] = bool(on)
+
+
+def bn_dgrad_sums_count(reset: bool = False):
+    """(BN backwards that used dgrad-epilogue sums, armed links that fell back)."""
+    v = tuple(_BNB_COUNT)
+    if reset:
+        _BNB_COUNT[0] = _BNB_COUNT[1] = 0
+    return v
+
+
+def _bn_bwd(dout, dpre, y, res, stats, gamma, beta, M, C, act, need_res, direct_gb, link=None):
     """BN (+ residual) (+ activation) backward -> (dy, dres or None, sums or
     None).  Fused: ONE grid-barrier launch (mda_bn_bwd_fused); else the
     partial-rows reduce + finalize + apply (3 launches).  dgamma / dbeta are
@@ -258,6 +313,12 @@ def _bn_bwd(dout, dpre, y, res, stats, gamma, beta, M, C, act, need_res, direct_
     db = beta.grad if direct_gb else None
     dy = torch.empty_like(y)
     dres = torch.empty_like(y) if need_res else None
+    reg = link.take(dout) if link is not None else None
+    if reg is not None and dpre is None:
+        sums = None if direct_gb else torch.empty(2, C, dtype=torch.float32, device=dev)
+        _ext.call("mda_bn_bwd_apply_reg", dout, None, y, res, stats, M, C, act, reg, dy, dres,
+                  dg, db, sums)
+        return dy, dres, sums
     if _BN_FUSED[0]:
         sums = None if direct_gb else torch.empty(2, C, dtype=torch.float32, device=dev)
         _ext.call("mda_bn_bwd_fused", dout, None, dpre, y, res, stats, M, C, act, _region(C, dev),
@@ -565,6 +626,7 @@ class _ConvBNActTrain(torch.autograd.Function):
         need_dx = ctx.needs_input_grad[0]
         cin_w = weight.shape[1]
         chpad = G == 1 and (not need_dx) and needs_channel_pad(cin_w)
+        link_in = getattr(x, "_mda_bnlink", None) if (need_dx and G == 1 and _BNB_ON[0]) else None
         x = pad_channels8(x) if chpad else _cl_bf16(x)
         N, Cin, H, W = x.shape
         Cout, _, KH, KW = weight.shape
@@ -627,6 +689,14 @@ class _ConvBNActTrain(torch.autograd.Function):
         ctx.save_for_backward(x, wt, weight, gamma, beta, y, res, stats)
         ctx.meta = (N, Cin, H, W, Cout, Ho, Wo, KH, KW, stride, pad, Kp, KpT, act)
         ctx.has_res = residual is not None
+        ctx.link_in = link_in if (link_in is not None and link_in.C == Cin
+                                  and link_in.M == N * H * W) else None
+        # this layer's output, for its consumer's dgrad (no pre-activation
+        # output: its gradient would join dz after the consumer's epilogue)
+        ctx.bnlink = None
+        if not want_preact and Cout <= 2048:
+            ctx.bnlink = BnLink(y, res if act != 0 else None, stats, act, M, Cout)
+        _LAST_LINK[0] = ctx.bnlink
         if want_preact:
             return out, pre
         return out, None
@@ -645,7 +715,7 @@ class _ConvBNActTrain(torch.autograd.Function):
         direct_gb = gamma.grad is not None and beta.grad is not None
         need_res = ctx.has_res and ctx.needs_input_grad[4]
         dy, dres, sums = _bn_bwd(dout, dpre, y, res, stats, gamma, beta, M, Cout, act, need_res,
-                                 direct_gb)
+                                 direct_gb, ctx.bnlink)
         x_fork, res_fork = ctx.forks
         if need_res:
             dres = _fork_sum(res_fork, dres)
@@ -657,9 +727,20 @@ class _ConvBNActTrain(torch.autograd.Function):
             tile, splits = conv_plan(N * H * W, Cin, KpT)
             part = torch.empty(splits * N * H * W * Cin, dtype=torch.float32, device=dev) if splits > 1 else None
             other = x_fork.take() if x_fork is not None else None
-            _ext.call("mda_conv_dgrad_res", dy, wt, dx, part, other, N, H, W, Cin, Ho, Wo, Cout,
-                      KH, KW, stride, pad, KpT, tile, splits)
-            if other is None and x_fork is not None and x_fork.park(dx):
+            parks = other is None and x_fork is not None and x_fork.armed
+            link = ctx.link_in
+            if link is not None and not parks and splits == 1:
+                # dx is the whole output gradient of the BN layer that made x:
+                # its backward sums come out of this epilogue (BnLink)
+                reg = _region(Cin, dev)
+                _ext.call("mda_conv_dgrad_bnsum", dy, wt, dx, part, other, N, H, W, Cin, Ho, Wo,
+                          Cout, KH, KW, stride, pad, KpT, tile, splits, link.y, link.res,
+                          link.stats, link.act, reg)
+                link.arm(dx, reg)
+            else:
+                _ext.call("mda_conv_dgrad_res", dy, wt, dx, part, other, N, H, W, Cin, Ho, Wo,
+                          Cout, KH, KW, stride, pad, KpT, tile, splits)
+            if parks and x_fork.park(dx):
                 dx = None
         dw = None
         if ctx.needs_input_grad[1]:
@@ -1041,6 +1122,10 @@ def conv_bn_act_train(x, conv, bn, act, residual, want_preact, fork=None, res_fo
         meta = meta + ("grouped", conv.groups)
     if residual is None:
         res_fork = None
+    _LAST_LINK[0] = None
     out, pre = _ConvBNActTrain.apply(x, conv.weight, bn.weight, bn.bias, residual, meta, bn,
                                      bool(want_preact), (fork, res_fork))
+    link, _LAST_LINK[0] = _LAST_LINK[0], None
+    if link is not None:
+        out._mda_bnlink = link
     return out, pre

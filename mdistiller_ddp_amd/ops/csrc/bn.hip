@@ -925,6 +925,43 @@ bn_bwd_fused_kernel(BwdArgs a) {
   }
 }
 
+// BN-backward channel sums (sum dz, sum dz*xhat) of a large tensor into the
+// region: as many blocks as the reduction wants (no grid barrier, so no
+// one-block-per-CU cap); mda_bn_bwd_apply_reg follows.  Used instead of the
+// grid-barrier kernel when its rows do not fit in registers: that kernel
+// re-read y / dout with 4 waves per CU (70 us for a 64 x 112^2 x 64 layer).
+__global__ void __launch_bounds__(256)
+bn_bwd_sums_kernel(BwdArgs a) {
+  const int C = a.C, M = a.M;
+  const int C8 = C / 8;
+  const int rpi = 256 / C8;
+  const int cg = threadIdx.x % C8, r0 = threadIdx.x / C8;
+  const int c0 = cg * 8;
+  float sc[8], sh[8], mu[8], rs[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    mu[k] = a.stats[c0 + k]; rs[k] = a.stats[C + c0 + k];
+    sc[k] = a.stats[2 * C + c0 + k]; sh[k] = a.stats[3 * C + c0 + k];
+  }
+  float sdz[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sdzx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (r0 < rpi) {
+    MDA_ROW_LOOP({
+      Raw8 v;
+      bwd_load8(a, o, v);
+      float dz[8];
+      bwd_dz8(a, v, sc, sh, dz);
+      const uint32_t yw[4] = {v.y.x, v.y.y, v.y.z, v.y.w};
+_Pragma("unroll")
+      for (int e = 0; e < 8; ++e) {
+        const float yf = (e & 1) ? __uint_as_float(yw[e >> 1] & 0xffff0000u) : __uint_as_float(yw[e >> 1] << 16);
+        sdz[e] += dz[e];
+        sdzx[e] += dz[e] * (yf - mu[e]) * rs[e];
+      }
+    })
+  }
+  region_block_add(a.reg, sdz, sdzx, C, rpi);
+}
+
 // BN backward whose channel sums a producer already added into the region
 // (the dgrad epilogue of the consuming conv, conv_igemm.hip
 // mda_conv_dgrad_bnsum): one streaming pass, no reduction and no grid
@@ -1077,6 +1114,15 @@ MDA_API int mda_bn_bwd_fused(const void* dout, const void* dout2, const void* dp
   const int maxb = num_cus();
   const int nb = (int)std::min<int64_t>(rows_iter, maxb);
   const int64_t per = (rows_iter + nb - 1) / nb;     // row iterations per thread
+  if (per > 8) {
+    // too many rows to hold: sums with a full grid, then one streaming pass
+    const int nbr = reduce_blocks(M, C, BWD2_VPT, BWD2_MAXB);
+    hipLaunchKernelGGL(bn_bwd_sums_kernel, dim3(nbr), dim3(256), 0, st, a);
+    { const int rc_ = (int)hipGetLastError(); if (rc_) return rc_; }
+    a.err = nullptr;
+    hipLaunchKernelGGL(bn_bwd_apply_reg_kernel, dim3(apply_blocks(M * C / 8, APPLY_V)), dim3(256), 0, st, a);
+    MDA_CHECK_LAUNCH();
+  }
   if (per <= 1) hipLaunchKernelGGL((bn_bwd_fused_kernel<1, true>), dim3(nb), dim3(256), 0, st, a);
   else if (per <= 2) hipLaunchKernelGGL((bn_bwd_fused_kernel<2, true>), dim3(nb), dim3(256), 0, st, a);
   else if (per <= 4) hipLaunchKernelGGL((bn_bwd_fused_kernel<4, true>), dim3(nb), dim3(256), 0, st, a);

@@ -790,7 +790,7 @@ def _bn_train_backward(ctx, dout, dpre, y, res, stats, gamma, beta, M, C, act):
     dpre = _cl_bf16(dpre) if dpre is not None else None
     direct_gb = gamma.grad is not None and beta.grad is not None
     dy, dres, sums = _bn_bwd(dout, dpre, y, res, stats, gamma, beta, M, C, act, res is not None,
-                             direct_gb)
+                             direct_gb, getattr(ctx, "bnlink", None))
     if direct_gb:
         notify_grad(gamma, beta)
         return dy, dres, None, None
@@ -821,6 +821,10 @@ def _dw_forward(ctx, x, weight, gamma, beta, residual, stride, pad, act, bn, wan
     ctx.save_for_backward(x, wp, weight, gamma, beta, y, res, stats)
     ctx.meta = (N, C, H, W, Ho, Wo, stride, pad, act)
     ctx.has_res = residual is not None
+    # the depthwise layer's BN output feeds a pointwise conv (MobileNets): its
+    # backward sums can come from that conv's dgrad epilogue (BnLink)
+    ctx.bnlink = None if want_preact else BnLink(y, res if act != 0 else None, stats, act, M, C)
+    _LAST_LINK[0] = ctx.bnlink
     return out, pre
 
 

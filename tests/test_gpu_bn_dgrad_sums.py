@@ -172,3 +172,33 @@ def test_resnet_stack_with_forks(stride):
     assert _rel(dx, dx_off) < 2e-2
     for (n, p), (_, q) in zip(allm.named_parameters(), off.named_parameters()):
         assert _rel(p.grad, q.grad) < 2e-2, n
+
+
+@pytest.mark.parametrize("C,H,stride", [(64, 32, 1), (96, 16, 2), (256, 8, 1)])
+def test_depthwise_to_pointwise(C, H, stride):
+    """MobileNet pair: depthwise conv + BN + ReLU feeding a pointwise conv; the
+    depthwise layer's BN sums come from the pointwise dgrad epilogue."""
+    torch.manual_seed(5)
+    dw = nn.Conv2d(C, C, 3, stride, 1, groups=C, bias=False).cuda()
+    b1 = nn.BatchNorm2d(C).cuda()
+    pw = nn.Conv2d(C, 2 * C, 1, bias=False).cuda()
+    b2 = nn.BatchNorm2d(2 * C).cuda()
+    mods = [(dw, b1), (pw, b2)]
+    mods_off = copy.deepcopy(mods)
+    x = torch.randn(64, C, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    g = torch.randn(64, 2 * C, H // stride, H // stride, device="cuda")
+    hip_train.bn_dgrad_sums_count(reset=True)
+    out, dx = _chain(mods, x, g)
+    assert hip_train.bn_dgrad_sums_count(reset=True) == (1, 0)
+    hip_train.set_bn_dgrad_sums(False)
+    try:
+        out_off, dx_off = _chain(mods_off, x, g)
+    finally:
+        hip_train.set_bn_dgrad_sums(True)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out, out_off, atol=0, rtol=0)
+    assert _rel(dx, dx_off) < 1e-2
+    for m, mo in zip(mods, mods_off):
+        for p, q in zip(list(m[0].parameters()) + list(m[1].parameters()),
+                        list(mo[0].parameters()) + list(mo[1].parameters())):
+            assert _rel(p.grad, q.grad) < 1e-2

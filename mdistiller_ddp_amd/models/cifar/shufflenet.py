@@ -12,7 +12,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ...ops.nn import conv_bn_act, channel_shuffle, pool_linear
+from ...ops.nn import conv_bn_act, channel_gather, channel_shuffle, pool_linear
 from .._base import ModelBase, PreactStage
 from .resnet import Stage
 
@@ -27,7 +27,26 @@ class ShuffleBlock(nn.Module):
 
 
 # ----------------------------------------------------------------------------- V1
+def _ceil8(c: int) -> int:
+    return (c + 7) // 8 * 8
+
+
 class BottleneckV1(nn.Module):
+    """ShuffleNetV1 unit with PHYSICALLY padded groups (round 3).
+
+    The bottleneck width ``mid`` splits into groups of mid/g1 (conv1, g1 = 1 for
+    the first unit) and mid/g (conv3) channels -- 18 or 20 on CIFAR, which the
+    16-byte-vector kernels cannot address.  Each group is padded to a multiple
+    of 8 with zero weight rows / columns and BN gamma = beta = 0: pad channels
+    carry exact zeros forward, get exactly zero gradients (BN scale 0, zero
+    consumer columns, gather maps that never read them), and so stay zero under
+    SGD + weight decay.  The channel shuffle between the two layouts is one
+    gather (``channel_gather``: conv1's padded groups -> shuffled order ->
+    conv3's padded groups), and conv1 / conv3 run as compact grouped GEMMs.
+    ``state_dict`` shows the reference's (unpadded) shapes
+    (`mdistiller/models/cifar/ShuffleNetv1.py:19-63`).
+    """
+
     def __init__(self, in_planes, out_planes, stride, groups, is_last=False):
         super().__init__()
         self.is_last = is_last
@@ -35,20 +54,67 @@ class BottleneckV1(nn.Module):
         self.stride = stride
         mid = int(out_planes / 4)
         g = 1 if in_planes == 24 else groups
-        self.conv1 = nn.Conv2d(in_planes, mid, 1, groups=g, bias=False)
-        self.bn1 = nn.BatchNorm2d(mid)
+        m1, m3 = mid // g, mid // groups
+        m1p, m3p = _ceil8(m1), _ceil8(m3)
+        self.real = dict(mid=mid, g1=g, g3=groups, m1=m1, m3=m3, m1p=m1p, m3p=m3p, out=out_planes)
+        self.conv1 = nn.Conv2d(in_planes, g * m1p, 1, groups=g, bias=False)
+        self.bn1 = nn.BatchNorm2d(g * m1p)
         self.shuffle1 = ShuffleBlock(groups=g)
-        self.conv2 = nn.Conv2d(mid, mid, 3, stride, 1, groups=mid, bias=False)
-        self.bn2 = nn.BatchNorm2d(mid)
-        self.conv3 = nn.Conv2d(mid, out_planes, 1, groups=groups, bias=False)
+        self.conv2 = nn.Conv2d(groups * m3p, groups * m3p, 3, stride, 1, groups=groups * m3p, bias=False)
+        self.bn2 = nn.BatchNorm2d(groups * m3p)
+        self.conv3 = nn.Conv2d(groups * m3p, out_planes, 1, groups=groups, bias=False)
         self.bn3 = nn.BatchNorm2d(out_planes)
         self.shortcut = nn.Sequential()
         if stride == 2:
             self.shortcut = nn.Sequential(nn.AvgPool2d(3, stride=2, padding=1))
+        # conv3-layout channel k*m3p + t  <-  shuffled real channel j = k*m3 + t
+        #                                 <-  conv1-layout channel (j % g)*m1p + j // g
+        fmap = [-1] * (groups * m3p)
+        for k in range(groups):
+            for t in range(m3):
+                j = k * m3 + t
+                fmap[k * m3p + t] = (j % g) * m1p + j // g
+        bmap = [-1] * (g * m1p)
+        for c, src in enumerate(fmap):
+            if src >= 0:
+                bmap[src] = c
+        self.register_buffer("_fmap", torch.tensor(fmap, dtype=torch.int32), persistent=False)
+        self.register_buffer("_bmap", torch.tensor(bmap, dtype=torch.int32), persistent=False)
+        # physical index of every real channel (reference order)
+        self._idx1 = [(r // m1) * m1p + r % m1 for r in range(mid)]
+        self._idx3 = [(j // m3) * m3p + j % m3 for j in range(mid)]
+        self._init_real()
+
+    @torch.no_grad()
+    def _init_real(self):
+        R = self.real
+        # the reference's default init on the reference shapes, then placed
+        ref3 = nn.Conv2d(R["mid"], R["out"], 1, groups=R["g3"], bias=False)
+        self.conv3.weight.zero_()
+        self.conv3.weight[:, :R["m3"]].copy_(ref3.weight)
+        keep1 = torch.zeros(self.conv1.out_channels, dtype=torch.bool)
+        keep1[self._idx1] = True
+        keep3 = torch.zeros(self.conv2.out_channels, dtype=torch.bool)
+        keep3[self._idx3] = True
+        self.conv1.weight[~keep1] = 0
+        self.conv2.weight[~keep3] = 0
+        for bn, keep in ((self.bn1, keep1), (self.bn2, keep3)):
+            bn.weight[~keep] = 0
+            bn.bias[~keep] = 0
+
+    def _pad_specs(self):
+        """state_dict key -> (dim, physical indices of the real entries)."""
+        i1, i3 = self._idx1, self._idx3
+        out = {"conv1.weight": (0, i1), "conv2.weight": (0, i3),
+               "conv3.weight": (1, list(range(self.real["m3"])))}
+        for k in ("weight", "bias", "running_mean", "running_var"):
+            out[f"bn1.{k}"] = (0, i1)
+            out[f"bn2.{k}"] = (0, i3)
+        return out
 
     def forward(self, x):
         out, _ = conv_bn_act(x, self.conv1, self.bn1, "relu")
-        out = self.shuffle1(out)
+        out = channel_gather(out, self._fmap, self._bmap)
         out, _ = conv_bn_act(out, self.conv2, self.bn2, "relu")
         if self.stride == 2:
             out, _ = conv_bn_act(out, self.conv3, self.bn3, "none")
@@ -69,6 +135,40 @@ class ShuffleNet(nn.Module, ModelBase):
         self.layer3 = self._make_layer(out_planes[2], num_blocks[2], groups)
         self.linear = nn.Linear(out_planes[2], num_classes)
         self.stage_channels = [24] + list(out_planes)
+        self._register_state_dict_hook(ShuffleNet._sd_slice)
+        self._register_load_state_dict_pre_hook(self._sd_pad)
+
+    def _pad_entries(self):
+        out = {}
+        for name, m in self.named_modules():
+            if isinstance(m, BottleneckV1):
+                for k, v in m._pad_specs().items():
+                    out[f"{name}.{k}"] = v
+        return out
+
+    @staticmethod
+    def _sd_slice(module, sd, prefix, local_metadata):
+        # physical (group-padded) tensors -> the reference's shapes
+        for k, (dim, idx) in module._pad_entries().items():
+            key = prefix + k
+            if key in sd:
+                t = sd[key]
+                sd[key] = t.index_select(dim, torch.tensor(idx, device=t.device)).clone()
+        return sd
+
+    def _sd_pad(self, sd, prefix, *args):
+        own = dict(self.named_parameters())
+        own.update(dict(self.named_buffers()))
+        for k, (dim, idx) in self._pad_entries().items():
+            key = prefix + k
+            if key not in sd or k not in own or sd[key].shape == own[k].shape:
+                continue
+            t, ref = sd[key], own[k]
+            z = torch.zeros(ref.shape, device=t.device, dtype=t.dtype)
+            if k.endswith("running_var"):
+                z.fill_(1.0)
+            z.index_copy_(dim, torch.tensor(idx, device=t.device), t)
+            sd[key] = z
 
     def _make_layer(self, out_planes, num_blocks, groups):
         layers = []

@@ -47,6 +47,10 @@ SIGNATURES = {
     "mda_conv_dgrad": "pppp" + "i" * 14 + "s",
     "mda_conv_dgrad_res": "ppppp" + "i" * 14 + "s",
     "mda_conv_dgrad_bnsum": "ppppp" + "i" * 14 + "ppp" + "i" + "p" + "s",
+    "mda_conv_dgrad_bnsum_g": "ppppp" + "i" * 14 + "ppp" + "i" + "p" + "i" + "s",
+    "mda_conv_fwd_bnacc_g": "ppppp" + "i" * 14 + "i" + "s",
+    "mda_pack_conv_weights_gc": "ppp" + "i" * 7 + "s",
+    "mda_channel_gather": "ppp" + "iii" + "s",
     "mda_conv_wgrad": "pppp" + "i" * 13 + "fiiis",
     "mda_conv_wgrad_nored": "pppp" + "i" * 13 + "fiiis",
     "mda_wgrad_reduce_multi": "pis",

@@ -88,7 +88,25 @@ struct ConvParams {
   const float* bnb_stats;
   BnRegion* bnb_slot;
   int bnb_act;
+  // grouped conv (glds kernel only): Cin above is the channels of ONE group,
+  // x rows hold ldx channels, each group owns cout_g consecutive output
+  // channels, and a block's N tile never leaves its group (grid.y = groups x
+  // tiles per group).  Dense: ldx = Cin, cout_g = Cout.
+  int ldx, cout_g;
 };
+
+// first output channel past the group of the tile starting at n0
+__device__ __forceinline__ int group_nlim(const ConvParams& p, int n0) {
+  if (p.cout_g >= p.Cout) return p.Cout;
+  const int e = (n0 / p.cout_g + 1) * p.cout_g;
+  return e < p.Cout ? e : p.Cout;
+}
+// N tile -> first output channel of the tile (group-aligned tiles)
+__device__ __forceinline__ int group_n0(const ConvParams& p, int ty, int BN) {
+  if (p.cout_g >= p.Cout) return ty * BN;
+  const int tpg = (p.cout_g + BN - 1) / BN;
+  return (ty / tpg) * p.cout_g + (ty % tpg) * BN;
+}
 
 __device__ __forceinline__ void stamp(const ConvParams& p, int k) {
   if (p.stamps != nullptr && threadIdx.x == 0) {
@@ -258,7 +276,7 @@ __device__ __forceinline__ void epi_prefetch(const ConvParams& p, EpiPre<BM, BN,
   const int co = n0 + c8 * 8;
   const bool split = par ? p.zsplits > 1 : gridDim.z > 1;
   e.have = !split && p.stats_part == nullptr && p.stats_slot == nullptr && p.bnb_slot == nullptr &&
-           (p.Cout & 7) == 0 && co < p.Cout;
+           (p.Cout & 7) == 0 && co < group_nlim(p, n0);
   e.have_res = false;
   if (!e.have) return;
   load_scale_bias8(p, co, e.sc, e.bi);
@@ -302,7 +320,7 @@ __device__ __forceinline__ void conv_epilogue_bnb(const ConvParams& p, float* Cs
   const int co = n0 + c8 * 8;
   const int C = p.Cout;
   const int mlim = has_pc ? pc.Mc : p.M;
-  const bool cok = co < C;
+  const bool cok = co < group_nlim(p, n0);
   const bool zres = p.bnb_res != nullptr && p.bnb_act != ACT_NONE;
   float mu[8], rs[8], sc[8], sh[8];
 #pragma unroll
@@ -376,7 +394,7 @@ __device__ __forceinline__ void conv_epilogue_bnb(const ConvParams& p, float* Cs
       a0 += red[(q * RPP + r) * BN + c];
       a1 += red[(q * RPP + r + 1) * BN + c];
     }
-    if (n0 + c < C)
+    if (n0 + c < group_nlim(p, n0))
       acc_add(region_acc(p.bnb_slot, C, (int)blockIdx.x % slot_shards(C), q) + n0 + c, (double)(a0 + a1));
   }
 }
@@ -418,7 +436,7 @@ __device__ __forceinline__ void conv_epilogue_rows(const ConvParams& p, char* sm
     // raw bf16 output + BN statistics partials of this block's rows.  No early
     // return before the barrier: threads past Cout just contribute zeros.
     float s1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, s2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    const bool cok = co < p.Cout;
+    const bool cok = co < group_nlim(p, n0);
     for (int r0 = rr; r0 < rows; r0 += RPP) {
       const int m = m0 + r0;
       if (m >= mlim || !cok) break;
@@ -450,7 +468,7 @@ __device__ __forceinline__ void conv_epilogue_rows(const ConvParams& p, char* sm
         a0 += red[(q * RPP + r) * BN + c];
         a1 += red[(q * RPP + r + 1) * BN + c];
       }
-      if (n0 + c < p.Cout) {
+      if (n0 + c < group_nlim(p, n0)) {
         if (p.stats_slot != nullptr)
           acc_add(region_acc(p.stats_slot, p.Cout, (int)blockIdx.x % slot_shards(p.Cout), q) + n0 + c,
                   (double)(a0 + a1));
@@ -461,7 +479,7 @@ __device__ __forceinline__ void conv_epilogue_rows(const ConvParams& p, char* sm
     return;
   }
   if ((p.Cout & 7) == 0) {
-    if (co >= p.Cout) return;
+    if (co >= group_nlim(p, n0)) return;
     using E = EpiPre<BM, BN, NT>;
     if (pre.have) {
       // operands already in registers (epi_prefetch); fully unrolled so the
@@ -504,7 +522,7 @@ __device__ __forceinline__ void conv_epilogue_rows(const ConvParams& p, char* sm
       if (m >= mlim) break;
       if (has_pc) m = par_row(p, pc, m);
       for (int e = 0; e < 8; ++e) {
-        if (co + e >= p.Cout) break;
+        if (co + e >= group_nlim(p, n0)) break;
         const float a = Cs[r0 * CS + c8 * 8 + e];
         if (split)
           p.partial[((int64_t)zsplit * p.M + m) * p.Cout + co + e] = a;
@@ -815,7 +833,9 @@ conv_glds_kernel(const ConvParams p) {
   const int wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int m0 = blockIdx.x * BM;
-  const int n0 = blockIdx.y * BN;
+  const int n0 = group_n0(p, blockIdx.y, BN);
+  const int nlim = group_nlim(p, n0);
+  const int xoff = (n0 / p.cout_g) * p.Cin;  // grouped: this group's first x channel
   const int trow = tid >> 3;                              // row within each 32-row slab
   const int chunk = (tid & 7) ^ ((trow >> 1) & 7);        // swizzled k-chunk this lane copies
   const uint32_t wave_off = (uint32_t)__builtin_amdgcn_readfirstlane(wid) * 1024u;
@@ -842,7 +862,7 @@ conv_glds_kernel(const ConvParams p) {
     const int r = mm - n * HoWo;
     const int oh = r / p.Wo;
     const int ow = r - oh * p.Wo;
-    a_img[j] = n * p.H * p.W * p.Cin;
+    a_img[j] = n * p.H * p.W * p.ldx + xoff;
     if (DGRAD) {
       a_ih0[j] = oh + p.pad;
       a_iw0[j] = ow + p.pad;
@@ -857,7 +877,7 @@ conv_glds_kernel(const ConvParams p) {
 #pragma unroll
   for (int j = 0; j < BLOADS; ++j) {
     const int co = n0 + trow + 32 * j;
-    b_ok[j] = (trow + 32 * j < BN) && co < p.Cout;
+    b_ok[j] = (trow + 32 * j < BN) && co < nlim;
     b_row[j] = p.w + (int64_t)(b_ok[j] ? co : 0) * p.Kp + chunk * 8;
   }
 
@@ -909,7 +929,7 @@ conv_glds_kernel(const ConvParams p) {
         iw = a_iw0[j] + kw;
         ok = ok && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
       }
-      const bf16_t* src = ok ? p.x + (a_img[j] + (ih * p.W + iw) * p.Cin + c0) : zero;
+      const bf16_t* src = ok ? p.x + (a_img[j] + (ih * p.W + iw) * p.ldx + c0) : zero;
       glds16(src, abase + (uint32_t)(j * 32 * 128));
     }
     const uint32_t bbase = abase + (uint32_t)(BM * 128);
@@ -1658,7 +1678,10 @@ bool use_glds() {
 
 template <int BM, int BN>
 int launch_tile(const ConvParams& p, int mode, int splits, hipStream_t st) {
-  dim3 grid((p.M + BM - 1) / BM, (p.Cout + BN - 1) / BN, splits);
+  const int ny = p.cout_g < p.Cout ? (p.Cout / p.cout_g) * ((p.cout_g + BN - 1) / BN)
+                                   : (p.Cout + BN - 1) / BN;
+  dim3 grid((p.M + BM - 1) / BM, ny, splits);
+  if (p.cout_g < p.Cout && (mode == LOAD_SCALAR || !use_glds())) return (int)hipErrorInvalidValue;
   if (mode != LOAD_SCALAR && use_glds() && p.steps_per_split <= ring1_max()) {  // short-K blocks
     if (mode == LOAD_FAST)
       hipLaunchKernelGGL((conv_glds_kernel<BM, BN, LOAD_FAST, 1>), grid, dim3(256), 0, st, p);
@@ -1732,7 +1755,15 @@ namespace {
 
 int dispatch(ConvParams& p, int mode, int64_t tile, int64_t splits, hipStream_t st, int halo = 0) {
   if (p.Kp % BK || p.Kp < p.K) return (int)hipErrorInvalidValue;
-  const int64_t xb = (int64_t)p.N * p.H * p.W * p.Cin * 2, wb = (int64_t)p.Cout * p.Kp * 2;
+  if (p.ldx <= 0) p.ldx = p.Cin;
+  if (p.cout_g <= 0) p.cout_g = p.Cout;
+  if (p.cout_g < p.Cout) {  // grouped: group-aligned tiles on the glds kernel only
+    if (p.Cout % p.cout_g || p.ldx != p.Cin * (p.Cout / p.cout_g) || p.cout_g % 8 || p.Cin % 8)
+      return (int)hipErrorInvalidValue;
+    halo = 0;
+    p.par = 0;
+  }
+  const int64_t xb = (int64_t)p.N * p.H * p.W * p.ldx * 2, wb = (int64_t)p.Cout * p.Kp * 2;
   if (xb >= ((int64_t)1 << 31) || wb >= ((int64_t)1 << 31) || (int64_t)p.M * p.Cout >= ((int64_t)1 << 31))
     return (int)hipErrorInvalidValue;  // 32-bit buffer offsets
   p.x_bytes = (int)xb;
@@ -1883,6 +1914,13 @@ MDA_API int mda_conv_dgrad_bnsum(const void* dy, const void* wt, void* dx, float
                                  int64_t splits, const void* bn_y, const void* bn_res,
                                  const float* bn_stats, int64_t bn_act, void* region,
                                  hipStream_t st);
+MDA_API int mda_conv_dgrad_bnsum_g(const void* dy, const void* wt, void* dx, float* partial,
+                                   const void* res, int64_t N, int64_t H, int64_t W, int64_t Cin,
+                                   int64_t Ho, int64_t Wo, int64_t Cout, int64_t KH, int64_t KW,
+                                   int64_t stride, int64_t pad, int64_t Kp, int64_t tile,
+                                   int64_t splits, const void* bn_y, const void* bn_res,
+                                   const float* bn_stats, int64_t bn_act, void* region,
+                                   int64_t groups, hipStream_t st);
 
 MDA_API int mda_conv_dgrad(const void* dy, const void* wt, void* dx, float* partial, int64_t N,
                            int64_t H, int64_t W, int64_t Cin, int64_t Ho, int64_t Wo,
@@ -1917,7 +1955,22 @@ MDA_API int mda_conv_dgrad_bnsum(const void* dy, const void* wt, void* dx, float
                                  int64_t splits, const void* bn_y, const void* bn_res,
                                  const float* bn_stats, int64_t bn_act, void* region,
                                  hipStream_t st) {
-  if (Cout % 8) return (int)hipErrorInvalidValue;
+  return mda_conv_dgrad_bnsum_g(dy, wt, dx, partial, res, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
+                                stride, pad, Kp, tile, splits, bn_y, bn_res, bn_stats, bn_act,
+                                region, 1, st);
+}
+
+// Grouped dgrad (groups > 1): dx[.., g*Cin/G + ci] sums only group g's output
+// channels; wt packed [Cin][KpT] with k = tap * (Cout/G) + co_in_group
+// (mda_pack_conv_weights_gc).  The GEMM runs with group-aligned tiles.
+MDA_API int mda_conv_dgrad_bnsum_g(const void* dy, const void* wt, void* dx, float* partial,
+                                   const void* res, int64_t N, int64_t H, int64_t W, int64_t Cin,
+                                   int64_t Ho, int64_t Wo, int64_t Cout, int64_t KH, int64_t KW,
+                                   int64_t stride, int64_t pad, int64_t Kp, int64_t tile,
+                                   int64_t splits, const void* bn_y, const void* bn_res,
+                                   const float* bn_stats, int64_t bn_act, void* region,
+                                   int64_t groups, hipStream_t st) {
+  if (Cout % 8 || groups < 1 || Cin % groups || Cout % groups) return (int)hipErrorInvalidValue;
   if (region != nullptr && (splits != 1 || Cin % 8 || Cin > SLOT_CMAX || bn_y == nullptr ||
                             bn_stats == nullptr))
     return (int)hipErrorInvalidValue;
@@ -1930,19 +1983,23 @@ MDA_API int mda_conv_dgrad_bnsum(const void* dy, const void* wt, void* dx, float
   p.x = (const bf16_t*)dy; p.w = (const bf16_t*)wt; p.scale = nullptr; p.bias = nullptr;
   p.res = (const bf16_t*)res; p.y = (bf16_t*)dx; p.preact = nullptr; p.partial = partial;
   // GEMM view: rows = dx pixels, cols = Cin, k = (tap, co); "input" image = dy
-  p.N = N; p.H = Ho; p.W = Wo; p.Cin = Cout; p.Ho = H; p.Wo = W; p.Cout = Cin; p.KH = KH;
-  p.KW = KW; p.stride = stride; p.pad = pad; p.K = KH * KW * Cout; p.Kp = Kp; p.M = N * H * W;
+  p.N = N; p.H = Ho; p.W = Wo; p.Cin = Cout / groups; p.Ho = H; p.Wo = W; p.Cout = Cin; p.KH = KH;
+  p.KW = KW; p.stride = stride; p.pad = pad; p.K = KH * KW * p.Cin; p.Kp = Kp; p.M = N * H * W;
   p.act = 0;
-  int mode = (Cout % BK == 0) ? LOAD_DGRAD_FAST : LOAD_DGRAD_VEC8;
+  p.ldx = (int)Cout;
+  p.cout_g = (int)(Cin / groups);
+  int mode = (p.Cin % BK == 0) ? LOAD_DGRAD_FAST : LOAD_DGRAD_VEC8;
   p.par = 0;
   p.zsplits = 1;
   p.stats_part = nullptr;
   p.stats_slot = nullptr;
   p.stamps = g_stamps;
   // strided dgrad: one GEMM per output-parity class with only its taps
-  if (stride > 1 && mode == LOAD_DGRAD_FAST && use_glds() && use_par_dgrad()) p.par = (int)stride;
+  if (stride > 1 && mode == LOAD_DGRAD_FAST && use_glds() && use_par_dgrad() && groups == 1)
+    p.par = (int)stride;
+  if (groups > 1 && (p.Cin % 8 || p.cout_g % 8)) return (int)hipErrorInvalidValue;
   // stride-1 3x3 pad-1 dgrad is a "same" conv of dy with the mirrored taps
-  return dispatch(p, mode, tile, splits, st, halo_eligible(p) ? 2 : 0);
+  return dispatch(p, mode, tile, splits, st, (groups == 1 && halo_eligible(p)) ? 2 : 0);
 }
 
 // Training conv + BN statistics, two launches: the conv writes the raw bf16
@@ -2014,12 +2071,34 @@ MDA_API int mda_conv_fwd_bnstats(const void* x, const void* w, void* y, float* p
 // standalone statistics pass into the same slot.
 extern "C" int mda_bn_stats_acc(const void* y, int64_t M, int64_t C, void* region, hipStream_t st);
 
+MDA_API int mda_conv_fwd_bnacc_g(const void* x, const void* w, void* y, float* partial,
+                                 void* region, int64_t N, int64_t H, int64_t W, int64_t Cin,
+                                 int64_t Ho, int64_t Wo, int64_t Cout, int64_t KH, int64_t KW,
+                                 int64_t stride, int64_t pad, int64_t Kp, int64_t tile,
+                                 int64_t splits, int64_t groups, hipStream_t st);
+
 MDA_API int mda_conv_fwd_bnacc(const void* x, const void* w, void* y, float* partial, void* region,
                                int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Ho,
                                int64_t Wo, int64_t Cout, int64_t KH, int64_t KW, int64_t stride,
                                int64_t pad, int64_t Kp, int64_t tile, int64_t splits,
                                hipStream_t st) {
+  return mda_conv_fwd_bnacc_g(x, w, y, partial, region, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride,
+                              pad, Kp, tile, splits, 1, st);
+}
+
+// Grouped (groups > 1, Cin/G and Cout/G multiples of 8): w packed [Cout][Kp]
+// over the Cin/G channels of each output channel's group (the OIHW weight of
+// a grouped conv packed as if dense, mda_pack_conv_weights with Cin/G).
+MDA_API int mda_conv_fwd_bnacc_g(const void* x, const void* w, void* y, float* partial,
+                                 void* region, int64_t N, int64_t H, int64_t W, int64_t Cin,
+                                 int64_t Ho, int64_t Wo, int64_t Cout, int64_t KH, int64_t KW,
+                                 int64_t stride, int64_t pad, int64_t Kp, int64_t tile,
+                                 int64_t splits, int64_t groups, hipStream_t st) {
+  if (groups < 1 || Cin % groups || Cout % groups) return (int)hipErrorInvalidValue;
   ConvParams p{};
+  p.ldx = (int)Cin;
+  p.cout_g = (int)(Cout / groups);
+  Cin /= groups;
   p.x = (const bf16_t*)x; p.w = (const bf16_t*)w; p.scale = nullptr; p.bias = nullptr;
   p.res = nullptr; p.y = (bf16_t*)y; p.preact = nullptr; p.partial = partial;
   p.N = N; p.H = H; p.W = W; p.Cin = Cin; p.Ho = Ho; p.Wo = Wo; p.Cout = Cout; p.KH = KH;
@@ -2032,8 +2111,9 @@ MDA_API int mda_conv_fwd_bnacc(const void* x, const void* w, void* y, float* par
   p.stamps = g_stamps;
   if (Cout % 8 || Cout > SLOT_CMAX) return (int)hipErrorInvalidValue;
   int mode = (Cin % BK == 0) ? LOAD_FAST : (Cin % 8 == 0 ? LOAD_VEC8 : LOAD_SCALAR);
+  if (groups > 1 && mode == LOAD_SCALAR) return (int)hipErrorInvalidValue;
   if (tile == 0 || splits == 0) mda_conv_plan(p.M, p.Cout, p.Kp, &tile, &splits);
-  const int halo = halo_eligible(p) ? 1 : 0;
+  const int halo = (groups == 1 && halo_eligible(p)) ? 1 : 0;
   if (splits == 1) p.stats_slot = (BnRegion*)region;
   int rc = dispatch(p, mode, tile, splits, st, halo);
   if (rc || splits == 1) return rc;

@@ -563,7 +563,7 @@ pack_kernel(const float* __restrict__ w, bf16_t* __restrict__ wf, bf16_t* __rest
 // zeroed once by the per-layer pack at registration and stay zero.
 // (The previous element-per-thread version scattered 2-byte stores at
 // stride KpT and took 232 us for a ResNet-18.)
-constexpr int PACK_MAX_LAYERS = 128;
+constexpr int PACK_MAX_LAYERS = 256;
 constexpr int PACK_FIELDS = 10;
 constexpr int PACK_LDS_FLOATS = 13056;  // >= max over T of T*(T*KHKW + 1)
 
@@ -882,7 +882,53 @@ pack_grouped_kernel(const float* __restrict__ w, bf16_t* __restrict__ wf, bf16_t
     }
   }
 }
+// Compact operands of a grouped conv (group-aligned GEMM tiles,
+// conv_igemm.hip mda_conv_fwd_bnacc_g / mda_conv_dgrad_bnsum_g): w fp32
+// [Cout, Cin/G, KH, KW] ->
+//   wf bf16 [Cout][Kp]:  k = tap * (Cin/G) + ci            (the group's K only)
+//   wt bf16 [Cin][KpT]:  k = tap * (Cout/G) + co_in_group  (dgrad of the group)
+__global__ void __launch_bounds__(256)
+pack_gc_kernel(const float* __restrict__ w, bf16_t* __restrict__ wf, bf16_t* __restrict__ wt,
+               int Cout, int cin_g, int KH, int KW, int Kp, int KpT, int G) {
+  const int cout_g = Cout / G, KK = KH * KW, K = KK * cin_g;
+  const int64_t total = (int64_t)Cout * Kp;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int co = (int)(i / Kp), k = (int)(i - (i / Kp) * Kp);
+    float v = 0.f;
+    if (k < K) {
+      const int tap = k / cin_g, ci = k - tap * cin_g;
+      v = w[((int64_t)co * cin_g + ci) * KK + tap];
+      if (wt) {
+        const int g = co / cout_g, cog = co - g * cout_g;
+        wt[(int64_t)(g * cin_g + ci) * KpT + tap * cout_g + cog] = f2bf(v);
+      }
+    }
+    wf[i] = f2bf(v);
+  }
+  if (wt) {
+    const int padw = KpT - KK * cout_g;
+    const int64_t rows = (int64_t)cin_g * G;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < rows * padw;
+         i += (int64_t)gridDim.x * blockDim.x) {
+      const int ci = (int)(i / padw), j = (int)(i - (i / padw) * padw);
+      wt[(int64_t)ci * KpT + KK * cout_g + j] = 0;
+    }
+  }
+}
 }  // namespace
+
+MDA_API int mda_pack_conv_weights_gc(const float* w, void* wf, void* wt, int64_t Cout, int64_t cin_g,
+                                     int64_t KH, int64_t KW, int64_t Kp, int64_t KpT, int64_t G,
+                                     hipStream_t st) {
+  if (G < 1 || Cout % G || Kp < KH * KW * cin_g || (wt && KpT < KH * KW * (Cout / G)))
+    return (int)hipErrorInvalidValue;
+  const int64_t total = Cout * Kp;
+  const int blocks = (int)std::min<int64_t>((total + 255) / 256, 2048);
+  hipLaunchKernelGGL(pack_gc_kernel, dim3(blocks), dim3(256), 0, st, w, (bf16_t*)wf, (bf16_t*)wt,
+                     (int)Cout, (int)cin_g, (int)KH, (int)KW, (int)Kp, (int)KpT, (int)G);
+  MDA_CHECK_LAUNCH();
+}
 
 MDA_API int mda_pack_conv_weights_grouped(const float* w, void* wf, void* wt, int64_t Cout, int64_t Cin,
                                           int64_t KH, int64_t KW, int64_t Kp, int64_t KpT, int64_t G,

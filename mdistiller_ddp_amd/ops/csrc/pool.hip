@@ -165,3 +165,42 @@ MDA_API int mda_channel_shuffle(const void* x, void* y, int64_t M, int64_t C, in
                      (bf16_t*)y, M, (int)C, (int)g);
   MDA_CHECK_LAUNCH();
 }
+
+// ---------------------------------------------------------------------------
+// Channel gather on NHWC bf16: y[m, c] = map[c] >= 0 ? x[m, map[c]] : 0, with
+// Cx input and Cy output channels.  ShuffleNetV1 with physically padded groups
+// (models/cifar/shufflenet.py): the channel shuffle between conv1 (groups of
+// mid/g1 channels, each padded to a multiple of 8) and the grouped conv3
+// (groups of mid/g, padded) is one such map; its backward is the inverse map.
+// One thread per 2 output channels (4-byte stores); the map lives in LDS.
+namespace {
+__global__ void __launch_bounds__(256)
+channel_gather_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                      const int* __restrict__ map, int64_t M, int Cx, int Cy) {
+  __shared__ int smap[2048];
+  for (int c = threadIdx.x; c < Cy; c += blockDim.x) smap[c] = map[c];
+  __syncthreads();
+  const int64_t total2 = M * Cy / 2;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total2;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = (i * 2) / Cy;
+    const int c = (int)(i * 2 - m * Cy);
+    const bf16_t* row = x + m * Cx;
+    const int j0 = smap[c], j1 = smap[c + 1];
+    const uint32_t a = j0 >= 0 ? (uint32_t)row[j0] : 0u;
+    const uint32_t b = j1 >= 0 ? (uint32_t)row[j1] : 0u;
+    *(uint32_t*)(y + i * 2) = a | (b << 16);
+  }
+}
+}  // namespace
+
+MDA_API int mda_channel_gather(const void* x, void* y, const int* map, int64_t M, int64_t Cx,
+                               int64_t Cy, hipStream_t st) {
+  if (Cy % 2 || Cy > 2048 || Cx <= 0 || M <= 0) return (int)hipErrorInvalidValue;
+  int64_t blocks = (M * Cy / 2 + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(channel_gather_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
+                     (const bf16_t*)x, (bf16_t*)y, map, M, (int)Cx, (int)Cy);
+  MDA_CHECK_LAUNCH();
+}
+

@@ -371,10 +371,15 @@ class PackCache:
             return None
         return e
 
-    def register(self, weight, wf, wt, Cout, Cin, KH, KW, Kp, KpT):
+    def register(self, weight, wf, wt, Cout, Cin, KH, KW, Kp, KpT, groups=1):
+        """``groups`` > 1: a grouped conv's compact operands (Cin = channels per
+        group), packed as ``groups`` dense sub-layers: group g's OIHW rows are
+        contiguous, and so are its rows of wf ([Cout][Kp]) and of wt
+        ([Cin_total][KpT], k = tap * Cout/G + co)."""
         if torch.cuda.is_current_stream_capturing():
             return
-        self.entries[id(weight)] = dict(weight=weight, wf=wf, wt=wt, meta=(Cout, Cin, KH, KW, Kp, KpT))
+        self.entries[id(weight)] = dict(weight=weight, wf=wf, wt=wt, meta=(Cout, Cin, KH, KW, Kp, KpT),
+                                        groups=groups)
         self._dirty = True
 
     def register_dw(self, weight, wp):
@@ -396,6 +401,18 @@ class PackCache:
                 _ext.call("mda_pack_tiles", Cout, Cin, KH, KW, t)
                 n = t.value  # tiles of this layer (padding stays zero from registration)
             w = e["weight"]
+            G = e.get("groups", 1)
+            if G > 1:
+                cog = Cout // G
+                t = ctypes.c_int64(0)
+                _ext.call("mda_pack_tiles", cog, Cin, KH, KW, t)
+                for g in range(G):
+                    rows.append([w.data_ptr() + 4 * g * cog * Cin * KH * KW,
+                                 e["wf"].data_ptr() + 2 * g * cog * Kp,
+                                 e["wt"].data_ptr() + 2 * g * Cin * KpT if e["wt"] is not None else 0,
+                                 cog, Cin, KH, KW, Kp, KpT, start])
+                    start += t.value
+                continue
             rows.append([w.data_ptr(), e["wf"].data_ptr(), e["wt"].data_ptr() if e["wt"] is not None else 0,
                          Cout, Cin, KH, KW, Kp, KpT, start])
             start += n
@@ -405,7 +422,8 @@ class PackCache:
         self._dirty = False
 
     def pack_all(self, device) -> bool:
-        if not self.entries or len(self.entries) > 128 or any(
+        nrows = sum(e.get("groups", 1) for e in self.entries.values())
+        if not self.entries or nrows > 256 or any(
                 e["meta"][2] * e["meta"][3] > 49 for e in self.entries.values()):
             return False
         capturing = torch.cuda.is_current_stream_capturing()
@@ -478,6 +496,15 @@ def set_grouped_native(on: bool) -> None:
     _GROUPED_NATIVE[0] = bool(on)
 
 
+_GROUPED_COMPACT = [os.environ.get("MDA_GROUPED_COMPACT", "1") != "0"]
+
+
+def set_grouped_compact(on: bool) -> None:
+    """Grouped convs on compact per-group operands (default) vs the dense
+    block-diagonal GEMM (A/B, and the path for unaligned groups)."""
+    _GROUPED_COMPACT[0] = bool(on)
+
+
 def train_supported(x, conv, bn) -> bool:
     if not (x.is_cuda and x.dim() == 4 and isinstance(conv, nn.Conv2d)):
         return False
@@ -492,7 +519,12 @@ def train_supported(x, conv, bn) -> bool:
         # Opt-in (MDA_GROUPED_NATIVE=1): G x the MFMA work plus a per-call pack
         # measured slower than MIOpen's grouped kernels on ShuffleV1 (5.48 vs
         # 5.34 ms/step, profiles/r2_misc_ab.md); the GPU test runs it either way.
-        if conv.in_channels % 8 or conv.out_channels % 8 or not _GROUPED_NATIVE[0]:
+        cig, cog = conv.in_channels // conv.groups, conv.out_channels // conv.groups
+        if conv.in_channels % 8 or conv.out_channels % 8:
+            return False
+        # compact grouped GEMM when every group is 16-byte aligned; the
+        # block-diagonal dense fallback only on request
+        if (cig % 8 or cog % 8) and not _GROUPED_NATIVE[0]:
             return False
     if conv.stride[0] != conv.stride[1] or not isinstance(conv.padding, tuple) or conv.padding[0] != conv.padding[1]:
         return False
@@ -625,6 +657,9 @@ class _ConvBNActTrain(torch.autograd.Function):
         ctx.groups = G
         need_dx = ctx.needs_input_grad[0]
         cin_w = weight.shape[1]
+        # grouped conv with 16-byte aligned groups: compact per-group operands
+        # on group-aligned GEMM tiles (no block-diagonal zeros)
+        gc = G > 1 and cin_w % 8 == 0 and (weight.shape[0] // G) % 8 == 0 and _GROUPED_COMPACT[0]
         chpad = G == 1 and (not need_dx) and needs_channel_pad(cin_w)
         link_in = getattr(x, "_mda_bnlink", None) if (need_dx and G == 1 and _BNB_ON[0]) else None
         x = pad_channels8(x) if chpad else _cl_bf16(x)
@@ -638,9 +673,23 @@ class _ConvBNActTrain(torch.autograd.Function):
         KpT = (KH * KW * Cout + 63) // 64 * 64
         dev = x.device
         ctx.cin_keep = cin_w if chpad else 0
+        ctx.kp_w = Kp  # the weight gradient runs dense over all Cin (keeps each group's block)
         packs = _ACTIVE[0]
-        ent = packs.lookup(weight, need_dx) if (packs is not None and not chpad and G == 1) else None
-        if G > 1:  # block-diagonal dense operands, packed per call (no multi-layer table)
+        if gc:
+            Kp = (KH * KW * cin_w + 63) // 64 * 64
+            KpT = (KH * KW * (Cout // G) + 63) // 64 * 64
+        ent = packs.lookup(weight, need_dx) if (packs is not None and not chpad and (G == 1 or gc)) else None
+        if gc and ent is None:
+            wf = torch.empty(Cout, Kp, dtype=torch.bfloat16, device=dev)
+            wt = torch.empty(Cin, KpT, dtype=torch.bfloat16, device=dev) if need_dx else None
+            wc = weight.detach()
+            if packs is not None and wc.is_contiguous() and wc.dtype == torch.float32:
+                packs.register(weight, wf, wt, Cout, cin_w, KH, KW, Kp, KpT, groups=G)
+            _ext.call("mda_pack_conv_weights_gc", wc.float().contiguous(), wf, wt, Cout, cin_w, KH, KW,
+                      Kp, KpT, G)
+        elif gc:
+            wf, wt = ent["wf"], ent["wt"]
+        elif G > 1:  # block-diagonal dense operands, packed per call (no multi-layer table)
             wf = torch.empty(Cout, Kp, dtype=torch.bfloat16, device=dev)
             wt = torch.empty(Cin, KpT, dtype=torch.bfloat16, device=dev) if need_dx else None
             _ext.call("mda_pack_conv_weights_grouped", weight.detach().float().contiguous(), wf, wt,
@@ -669,12 +718,12 @@ class _ConvBNActTrain(torch.autograd.Function):
         res = _cl_bf16(residual) if residual is not None else None
         out = torch.empty_like(y)
         pre = torch.empty_like(y) if want_preact else None
-        if _BN_FUSED[0]:
+        if _BN_FUSED[0] or gc:
             # conv whose epilogue adds the BN sums into the stream's slot, then
             # apply with the finalize in its prologue (2 launches)
             reg = _region(Cout, dev)
-            _ext.call("mda_conv_fwd_bnacc", x, wf, y, part, reg, N, H, W, Cin, Ho, Wo, Cout,
-                      KH, KW, stride, pad, Kp, tile, splits)
+            _ext.call("mda_conv_fwd_bnacc_g", x, wf, y, part, reg, N, H, W, Cin, Ho, Wo, Cout,
+                      KH, KW, stride, pad, Kp, tile, splits, G if gc else 1)
             _ext.call("mda_bn_apply_fin", y, reg, M, Cout, gamma.detach(), beta.detach(),
                       bn.running_mean, bn.running_var, stats, float(bn.momentum), float(bn.eps),
                       bn.num_batches_tracked, res, out, pre, act)
@@ -688,6 +737,7 @@ class _ConvBNActTrain(torch.autograd.Function):
             _ext.call("mda_bn_apply", y, stats[2], stats[3], res, out, pre, M, Cout, act)
         ctx.save_for_backward(x, wt, weight, gamma, beta, y, res, stats)
         ctx.meta = (N, Cin, H, W, Cout, Ho, Wo, KH, KW, stride, pad, Kp, KpT, act)
+        ctx.gc = gc
         ctx.has_res = residual is not None
         ctx.link_in = link_in if (link_in is not None and link_in.C == Cin
                                   and link_in.M == N * H * W) else None
@@ -729,7 +779,16 @@ class _ConvBNActTrain(torch.autograd.Function):
             other = x_fork.take() if x_fork is not None else None
             parks = other is None and x_fork is not None and x_fork.armed
             link = ctx.link_in
-            if link is not None and not parks and splits == 1:
+            if ctx.gc:
+                reg = _region(Cin, dev) if (link is not None and not parks and splits == 1) else None
+                _ext.call("mda_conv_dgrad_bnsum_g", dy, wt, dx, part, other, N, H, W, Cin, Ho, Wo,
+                          Cout, KH, KW, stride, pad, KpT, tile, splits,
+                          link.y if reg is not None else None, link.res if reg is not None else None,
+                          link.stats if reg is not None else None, link.act if reg is not None else 0,
+                          reg, ctx.groups)
+                if reg is not None:
+                    link.arm(dx, reg)
+            elif link is not None and not parks and splits == 1:
                 # dx is the whole output gradient of the BN layer that made x:
                 # its backward sums come out of this epilogue (BnLink)
                 reg = _region(Cin, dev)
@@ -744,12 +803,13 @@ class _ConvBNActTrain(torch.autograd.Function):
                 dx = None
         dw = None
         if ctx.needs_input_grad[1]:
-            sp = _wgrad_splits(M, Cout, Cin, KH, KW, Kp)
+            Kw = ctx.kp_w
+            sp = _wgrad_splits(M, Cout, Cin, KH, KW, Kw)
             direct_w = weight.grad is not None and weight.grad.is_contiguous()
             target = weight.grad if direct_w else torch.empty_like(weight, memory_format=torch.contiguous_format)
 
             def wg():
-                _conv_wgrad(x, dy, target, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, Kp, sp,
+                _conv_wgrad(x, dy, target, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, Kw, sp,
                             direct_w, ctx.cin_keep, ctx.groups)
             _wgrad_launch(wg, direct_w, x, dy)
             dw = None if direct_w else target

@@ -136,6 +136,45 @@ class _ChannelShuffle(torch.autograd.Function):
         return dx, None
 
 
+class _ChannelGather(torch.autograd.Function):
+    """y[:, c] = x[:, fmap[c]] (0 where fmap[c] < 0) on NHWC bf16 in one pass
+    (csrc/pool.hip mda_channel_gather); backward = the same gather with the
+    inverse map (the maps are injective)."""
+
+    @staticmethod
+    def forward(ctx, x, fmap, bmap):
+        from . import _ext
+        x = x.contiguous(memory_format=torch.channels_last)
+        n, c, h, w = x.shape
+        y = torch.empty((n, fmap.numel(), h, w), dtype=x.dtype, device=x.device,
+                        memory_format=torch.channels_last)
+        _ext.call("mda_channel_gather", x, y, fmap, n * h * w, c, fmap.numel())
+        ctx.maps = (bmap, c)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import _ext
+        bmap, cx = ctx.maps
+        dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        n, c, h, w = dy.shape
+        dx = torch.empty((n, cx, h, w), dtype=dy.dtype, device=dy.device,
+                         memory_format=torch.channels_last)
+        _ext.call("mda_channel_gather", dy, dx, bmap, n * h * w, c, cx)
+        return dx, None, None
+
+
+def channel_gather(x: torch.Tensor, fmap: torch.Tensor, bmap: torch.Tensor) -> torch.Tensor:
+    """Channel gather with zero fill: ``fmap`` (int32, one entry per output
+    channel, -1 = zero) and its inverse ``bmap`` (one entry per input channel)."""
+    if (hip_enabled_for(x) and x.dtype == torch.bfloat16 and fmap.numel() % 2 == 0
+            and bmap.numel() % 2 == 0 and fmap.is_cuda):
+        return _ChannelGather.apply(x, fmap, bmap)
+    idx = fmap.long().clamp_min(0)
+    y = x.index_select(1, idx)
+    return y * (fmap >= 0).to(y.dtype).reshape(1, -1, 1, 1)
+
+
 def channel_shuffle(x: torch.Tensor, groups: int) -> torch.Tensor:
     n, c, h, w = x.shape
     if (hip_enabled_for(x) and x.dtype == torch.bfloat16 and c % groups == 0 and c % 2 == 0

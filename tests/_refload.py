@@ -40,3 +40,29 @@ def load(kind: str, mod: str):
     sys.modules[full] = m
     spec.loader.exec_module(m)
     return m
+
+
+MODELS = os.path.join(REF, "mdistiller", "models")
+
+
+def load_model_module(sub: str, mod: str):
+    """``load_model_module("cifar", "ShuffleNetv1")`` -> the reference model
+    module (its ``from .._base import ...`` resolves to the reference's
+    models/_base.py through synthetic packages)."""
+    root = "_mdaref_models"
+    _pkg(root, MODELS)
+    base_full = f"{root}._base"
+    if base_full not in sys.modules:
+        spec = importlib.util.spec_from_file_location(base_full, os.path.join(MODELS, "_base.py"))
+        m = importlib.util.module_from_spec(spec)
+        sys.modules[base_full] = m
+        spec.loader.exec_module(m)
+    _pkg(f"{root}.{sub}", os.path.join(MODELS, sub))
+    full = f"{root}.{sub}.{mod}"
+    if full in sys.modules:
+        return sys.modules[full]
+    spec = importlib.util.spec_from_file_location(full, os.path.join(MODELS, sub, mod + ".py"))
+    m = importlib.util.module_from_spec(spec)
+    sys.modules[full] = m
+    spec.loader.exec_module(m)
+    return m

@@ -238,25 +238,36 @@ def test_wrn_convs_take_native_training_path():
     assert calls["bn"] == n_bn - sum(1 for b in m.modules() if hasattr(b, "bn2")), calls
 
 
-@pytest.mark.parametrize("N,Cin,H,Cout,G,with_res", [(8, 240, 16, 120, 3, False), (8, 120, 8, 480, 3, True),
-                                                      (4, 480, 8, 240, 3, False), (8, 64, 16, 32, 2, True)])
-def test_grouped_conv_bn_act_train(N, Cin, H, Cout, G, with_res):
-    """Grouped 1x1 conv (ShuffleNetV1) + BN (+res) + ReLU on the native path (dense
-    block-diagonal GEMM) vs fp32 PyTorch: outputs, running stats, all gradients."""
+GROUPED = [(8, 240, 16, 120, 3, False, 1, 1), (8, 120, 8, 480, 3, True, 1, 1),
+           (4, 480, 8, 240, 3, False, 1, 1), (8, 64, 16, 32, 2, True, 1, 1),
+           (64, 72, 16, 240, 3, True, 1, 1),      # ShuffleV1 conv3 (24 -> 80 per group, padded)
+           (64, 240, 16, 72, 3, False, 1, 1),     # ShuffleV1 conv1 (80 -> 24 per group)
+           (16, 48, 16, 96, 2, False, 3, 2)]      # 3x3 stride-2 grouped (strided grouped dgrad)
+
+
+@pytest.mark.parametrize("N,Cin,H,Cout,G,with_res,k,s", GROUPED)
+@pytest.mark.parametrize("compact", [True, False])
+def test_grouped_conv_bn_act_train(N, Cin, H, Cout, G, with_res, k, s, compact):
+    """Grouped conv (ShuffleNetV1) + BN (+res) + ReLU on the native path -- the
+    compact per-group GEMM (group-aligned tiles, default) and the dense
+    block-diagonal GEMM -- vs fp32 PyTorch: outputs, running stats, all gradients."""
     torch.manual_seed(2)
-    conv = nn.Conv2d(Cin, Cout, 1, 1, 0, groups=G, bias=False).cuda()
+    conv = nn.Conv2d(Cin, Cout, k, s, k // 2, groups=G, bias=False).cuda()
     bn = nn.BatchNorm2d(Cout).cuda()
     conv_r, bn_r = copy.deepcopy(conv), copy.deepcopy(bn)
     x = torch.randn(N, Cin, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    res = torch.randn(N, Cout, H, H, device="cuda").to(torch.bfloat16) if with_res else None
+    Ho = (H + 2 * (k // 2) - k) // s + 1
+    res = torch.randn(N, Cout, Ho, Ho, device="cuda").to(torch.bfloat16) if with_res else None
     x1 = x.clone().requires_grad_(True)
     r1 = res.clone().requires_grad_(True) if with_res else None
     hip_train.set_grouped_native(True)
+    hip_train.set_grouped_compact(compact)
     try:
         assert hip_train.train_supported(x1, conv, bn)
         out, _ = hip_train.conv_bn_act_train(x1, conv, bn, "relu", r1, False)
     finally:
         hip_train.set_grouped_native(False)
+        hip_train.set_grouped_compact(True)
     g = torch.randn_like(out.float()).to(torch.bfloat16).float()
     out.float().backward(g)
     x2 = x.float().clone().requires_grad_(True)

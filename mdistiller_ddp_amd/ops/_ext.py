@@ -51,6 +51,8 @@ SIGNATURES = {
     "mda_conv_fwd_bnacc_g": "ppppp" + "i" * 14 + "i" + "s",
     "mda_pack_conv_weights_gc": "ppp" + "i" * 7 + "s",
     "mda_channel_gather": "ppp" + "iii" + "s",
+    "mda_vid_loss": "ppp" + "ii" + "f" + "pp" + "s",
+    "mda_vid_bwd": "pppp" + "p" + "ii" + "f" + "pp" + "s",
     "mda_conv_wgrad": "pppp" + "i" * 13 + "fiiis",
     "mda_conv_wgrad_nored": "pppp" + "i" * 13 + "fiiis",
     "mda_wgrad_reduce_multi": "pis",

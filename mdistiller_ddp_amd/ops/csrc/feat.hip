@@ -173,3 +173,133 @@ MDA_API int mda_at_loss(int64_t dts, int64_t dtt, const void* fs, const void* ft
 #undef AT_L
   MDA_CHECK_LAUNCH();
 }
+
+// ---------------------------------------------------------------------------
+// VID Gaussian NLL (reference distillers/VID.py:16-30) on bf16 NHWC maps:
+//   loss = mean_{m,c} 0.5 * ((pred - ft)^2 / var_c + log var_c),
+//   var_c = softplus(log_scale_c) + eps.
+// Everything the loss and both gradients need is S_c = sum_m (pred - ft)^2:
+//   vid_sums     S_c by 8-channel row loops, block tree in LDS, fp64 atomics
+//   vid_finalize the scalar loss (one block, fixed-order tree)
+//   vid_bwd      dpred = go * (pred - ft) / (var_c M C);  block 0:
+//                dls_c = go * 0.5 (M / var_c - S_c / var_c^2) sigmoid(ls_c) / (M C)
+namespace {
+__device__ __forceinline__ float vid_var(float ls, float eps) {
+  return (ls > 20.f ? ls : log1pf(expf(ls))) + eps;
+}
+
+__global__ void __launch_bounds__(256)
+vid_sums_kernel(const bf16_t* __restrict__ pred, const bf16_t* __restrict__ ft, int M, int C,
+                double* __restrict__ acc) {
+  __shared__ float red[256 * 8];
+  const int C8 = C / 8;
+  const int rpi = 256 / C8;
+  const int cg = threadIdx.x % C8, r0 = threadIdx.x / C8;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (r0 < rpi) {
+    for (int m = blockIdx.x * rpi + r0; m < M; m += gridDim.x * rpi) {
+      const int64_t o = (int64_t)m * C + cg * 8;
+      const uint4 a = *(const uint4*)(pred + o), b = *(const uint4*)(ft + o);
+      const uint32_t aw[4] = {a.x, a.y, a.z, a.w}, bw[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float d0 = __uint_as_float(aw[k] << 16) - __uint_as_float(bw[k] << 16);
+        const float d1 = __uint_as_float(aw[k] & 0xffff0000u) - __uint_as_float(bw[k] & 0xffff0000u);
+        s[2 * k] += d0 * d0;
+        s[2 * k + 1] += d1 * d1;
+      }
+    }
+  }
+  if (r0 < rpi) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[r0 * C + cg * 8 + k] = s[k];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float t = 0.f;
+    for (int r = 0; r < rpi; ++r) t += red[r * C + c];
+    __hip_atomic_fetch_add(acc + c, (double)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__global__ void __launch_bounds__(256)
+vid_finalize_kernel(const double* __restrict__ acc, const float* __restrict__ ls, int M, int C,
+                    float eps, float* __restrict__ loss) {
+  __shared__ double red[256];
+  double t = 0.0;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const double v = (double)vid_var(ls[c], eps);
+    t += acc[c] / v + (double)M * log(v);
+  }
+  red[threadIdx.x] = t;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) loss[0] = (float)(0.5 * red[0] / ((double)M * C));
+}
+
+__global__ void __launch_bounds__(256)
+vid_bwd_kernel(const bf16_t* __restrict__ pred, const bf16_t* __restrict__ ft,
+               const float* __restrict__ ls, const double* __restrict__ acc,
+               const float* __restrict__ go, int M, int C, float eps, bf16_t* __restrict__ dpred,
+               float* __restrict__ dls) {
+  __shared__ float s_k[2048];
+  const float g = go[0];
+  const float inv_mc = 1.f / ((float)M * (float)C);
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const float v = vid_var(ls[c], eps);
+    s_k[c] = g * inv_mc / v;
+    if (blockIdx.x == 0 && dls) {
+      const float sg = 1.f / (1.f + expf(-ls[c]));
+      dls[c] = g * 0.5f * inv_mc * ((float)M / v - (float)acc[c] / (v * v)) * sg;
+    }
+  }
+  __syncthreads();
+  const int c8 = C / 8;
+  const int64_t total = (int64_t)M * c8;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % c8) * 8;
+    const uint4 a = *(const uint4*)(pred + i * 8), b = *(const uint4*)(ft + i * 8);
+    const uint32_t aw[4] = {a.x, a.y, a.z, a.w}, bw[4] = {b.x, b.y, b.z, b.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float d0 = __uint_as_float(aw[k] << 16) - __uint_as_float(bw[k] << 16);
+      const float d1 = __uint_as_float(aw[k] & 0xffff0000u) - __uint_as_float(bw[k] & 0xffff0000u);
+      o[k] = pack_bf16x2(d0 * s_k[c0 + 2 * k], d1 * s_k[c0 + 2 * k + 1]);
+    }
+    *(uint4*)(dpred + i * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+}  // namespace
+
+// acc: [C] fp64, zeroed by the caller; loss: [1] fp32.
+MDA_API int mda_vid_loss(const void* pred, const void* ft, const float* log_scale, int64_t M,
+                         int64_t C, float eps, double* acc, float* loss, hipStream_t st) {
+  if (C % 8 || C > 2048 || M <= 0) return (int)hipErrorInvalidValue;
+  const int C8 = (int)C / 8, rpi = 256 / C8;
+  int nb = (int)std::min<int64_t>((M + 4 * rpi - 1) / (4 * rpi), 512);
+  if (nb < 1) nb = 1;
+  hipLaunchKernelGGL(vid_sums_kernel, dim3(nb), dim3(256), 0, st, (const bf16_t*)pred,
+                     (const bf16_t*)ft, (int)M, (int)C, acc);
+  { const int rc = (int)hipGetLastError(); if (rc) return rc; }
+  hipLaunchKernelGGL(vid_finalize_kernel, dim3(1), dim3(256), 0, st, (const double*)acc, log_scale,
+                     (int)M, (int)C, eps, loss);
+  MDA_CHECK_LAUNCH();
+}
+
+// go: [1] fp32 upstream gradient (device); dls may be null.
+MDA_API int mda_vid_bwd(const void* pred, const void* ft, const float* log_scale, const double* acc,
+                        const float* go, int64_t M, int64_t C, float eps, void* dpred, float* dls,
+                        hipStream_t st) {
+  if (C % 8 || C > 2048 || M <= 0) return (int)hipErrorInvalidValue;
+  const int64_t work = M * C / 8;
+  const int nb = (int)std::min<int64_t>((work + 255) / 256, 2048);
+  hipLaunchKernelGGL(vid_bwd_kernel, dim3(nb), dim3(256), 0, st, (const bf16_t*)pred,
+                     (const bf16_t*)ft, log_scale, acc, go, (int)M, (int)C, eps, (bf16_t*)dpred,
+                     dls);
+  MDA_CHECK_LAUNCH();
+}

@@ -11,6 +11,7 @@ unsupported shapes).
 from __future__ import annotations
 
 import torch
+import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _ext
@@ -342,9 +343,61 @@ def kdsvd_loss(g_s, g_t, k):
 
 
 # ---------------------------------------------------------------- VID
+class _VIDNLL(torch.autograd.Function):
+    """VID Gaussian NLL on the native kernels (csrc/feat.hip mda_vid_loss /
+    mda_vid_bwd): one channel-sum pass + a one-block finalize forward, one
+    elementwise pass backward (+ the per-channel log-scale gradient)."""
+
+    @staticmethod
+    def forward(ctx, pred, f_t, log_scale, eps):
+        N, C, H, W = pred.shape
+        M = N * H * W
+        acc = torch.zeros(C, dtype=torch.float64, device=pred.device)
+        loss = torch.empty(1, dtype=torch.float32, device=pred.device)
+        ls = log_scale.detach().float().contiguous()
+        _ext.call("mda_vid_loss", pred, f_t, ls, M, C, float(eps), acc, loss)
+        ctx.save_for_backward(pred, f_t, ls, acc)
+        ctx.meta = (M, C, float(eps), log_scale.dtype)
+        return loss[0]
+
+    @staticmethod
+    def backward(ctx, go):
+        pred, f_t, ls, acc = ctx.saved_tensors
+        M, C, eps, lsdt = ctx.meta
+        g = go.detach().float().reshape(1).contiguous()
+        dpred = torch.empty_like(pred)
+        dls = torch.empty(C, dtype=torch.float32, device=pred.device) if ctx.needs_input_grad[2] else None
+        _ext.call("mda_vid_bwd", pred, f_t, ls, acc, g, M, C, eps, dpred, dls)
+        return dpred, None, (dls.to(lsdt) if dls is not None else None), None
+
+
+def _vid_native_ok(regressor, f_s, f_t) -> bool:
+    if not (hip_enabled_for(f_s) and f_s.dim() == 4 and f_t.dim() == 4 and f_s.shape[2:] == f_t.shape[2:]):
+        return False
+    convs = [m for m in regressor if isinstance(m, nn.Conv2d)]
+    return (len(convs) == 3 and all(c.bias is None and c.kernel_size == (1, 1) and c.groups == 1
+                                    for c in convs)
+            and all(c.out_channels % 8 == 0 and c.in_channels % 8 == 0 for c in convs)
+            and f_t.shape[1] <= 2048)
+
+
 def vid_loss(regressor, log_scale, f_s, f_t, eps=1e-5):
-    """`distillers/VID.py:16-30`: Gaussian NLL with softplus variance."""
+    """`distillers/VID.py:16-30`: Gaussian NLL with softplus variance.
+
+    On the GPU the 1x1 -> ReLU -> 1x1 -> ReLU -> 1x1 regressor runs as three
+    native conv launches (ReLU in the epilogue) and the NLL on
+    :class:`_VIDNLL`; elsewhere the PyTorch formulation."""
     f_s, f_t = _pool_to_match(f_s, f_t)
+    if _vid_native_ok(regressor, f_s, f_t):
+        from .nn import conv_bn_act
+        c1, c2, c3 = [m for m in regressor if isinstance(m, nn.Conv2d)]
+        x = f_s.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        h, _ = conv_bn_act(x, c1, None, "relu")
+        h, _ = conv_bn_act(h, c2, None, "relu")
+        pred, _ = conv_bn_act(h, c3, None, "none")
+        pred = pred.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        ft = f_t.detach().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        return _VIDNLL.apply(pred, ft, log_scale, eps)
     pred_mean = regressor(f_s).float()
     pred_var = F.softplus(log_scale.float()) + eps
     pred_var = pred_var.view(1, -1, 1, 1)

@@ -660,8 +660,8 @@ class _ConvBNActTrain(torch.autograd.Function):
         # grouped conv with 16-byte aligned groups: compact per-group operands
         # on group-aligned GEMM tiles (no block-diagonal zeros)
         gc = G > 1 and cin_w % 8 == 0 and (weight.shape[0] // G) % 8 == 0 and _GROUPED_COMPACT[0]
+        link_in = getattr(x, "_mda_bnlink", None) if (need_dx and (G == 1 or gc) and _BNB_ON[0]) else None
         chpad = G == 1 and (not need_dx) and needs_channel_pad(cin_w)
-        link_in = getattr(x, "_mda_bnlink", None) if (need_dx and G == 1 and _BNB_ON[0]) else None
         x = pad_channels8(x) if chpad else _cl_bf16(x)
         N, Cin, H, W = x.shape
         Cout, _, KH, KW = weight.shape

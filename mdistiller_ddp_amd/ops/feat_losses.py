@@ -107,7 +107,68 @@ def single_stage_nst_loss(f_s, f_t):
     return kmean(f_t, f_t).detach() + kmean(f_s, f_s) - 2 * kmean(f_s, f_t)
 
 
+class _NSTGram(torch.autograd.Function):
+    """NST on ONE Gram per sample: with W = [F_s | F_t] ([HW, 2C] channel
+    columns), G = W^T W holds all three raw Grams; F.normalize's column norms
+    are sqrt(diag G), so the normalised Grams are G / (r_i r_j) and the loss
+    is (||S||^2 + ||T||^2 - 2||X||^2) / (N C^2) -- no pass over the feature
+    maps besides the one batched GEMM.  Backward in closed form:
+        dot_c = k (sum_d S_cd^2 - sum_d X_cd^2),  k = 4 go / (N C^2)
+        P = D_s (k S - diag(dot)) D_s,  Q = -k D_t X^T D_s,   D = diag(1/r)
+        dF_s = F_s P + F_t Q = W [P; Q]          (one batched GEMM)
+    """
+
+    @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
+    def forward(ctx, w):
+        # w: [N, HW, 2C] fp32 (student channels first); fp32 GEMMs (autocast off)
+        N, _, C2 = w.shape
+        C = C2 // 2
+        g = torch.bmm(w.transpose(1, 2), w)
+        r = g.diagonal(dim1=1, dim2=2).clamp_min(0).sqrt().clamp_min(1e-12)
+        gh = g / (r.unsqueeze(2) * r.unsqueeze(1))
+        S, X, T = gh[:, :C, :C], gh[:, :C, C:], gh[:, C:, C:]
+        loss = (S.square().sum() + T.square().sum() - 2 * X.square().sum()) / (N * C * C)
+        ctx.save_for_backward(w, gh, r)
+        return loss
+
+    @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
+    def backward(ctx, go):
+        w, gh, r = ctx.saved_tensors
+        N, _, C2 = w.shape
+        C = C2 // 2
+        S, X = gh[:, :C, :C], gh[:, :C, C:]
+        k = 4.0 * go / (N * C * C)
+        rs, rt = r[:, :C], r[:, C:]
+        dot = k * (S.square().sum(2) - X.square().sum(2))
+        P = (k * S - torch.diag_embed(dot)) / (rs.unsqueeze(2) * rs.unsqueeze(1))
+        Q = -k * X.transpose(1, 2) / (rt.unsqueeze(2) * rs.unsqueeze(1))
+        dws = torch.bmm(w, torch.cat([P, Q], 1))
+        return torch.cat([dws, torch.zeros_like(dws)], 2)
+
+
+def _nst_cols(f):
+    """[N, HW, C] channel columns: a free view of a channels_last map."""
+    n, c = f.shape[0], f.shape[1]
+    if f.is_contiguous(memory_format=torch.channels_last) and not f.is_contiguous():
+        return f.permute(0, 2, 3, 1).reshape(n, -1, c)
+    return f.reshape(n, c, -1).transpose(1, 2)
+
+
+def single_stage_nst_loss_gram(f_s, f_t):
+    """:func:`single_stage_nst_loss` through :class:`_NSTGram` (one batched
+    Gram forward, one batched product backward)."""
+    f_s, f_t = _pool_to_match(f_s, f_t.detach())
+    if f_s.shape[1] != f_t.shape[1]:
+        return single_stage_nst_loss(f_s, f_t)
+    w = torch.cat([_nst_cols(f_s), _nst_cols(f_t)], 2).float()
+    return _NSTGram.apply(w)
+
+
 def nst_loss(g_s, g_t):
+    if g_s and hip_enabled_for(g_s[0]):
+        return sum(single_stage_nst_loss_gram(f_s, f_t) for f_s, f_t in zip(g_s, g_t))
     return sum(single_stage_nst_loss(f_s, f_t) for f_s, f_t in zip(g_s, g_t))
 
 

@@ -510,7 +510,12 @@ def train_supported(x, conv, bn) -> bool:
         return False
     if bn is None or not bn.training or not bn.track_running_stats or bn.momentum is None:
         return False
-    if conv.dilation != (1, 1) or conv.padding_mode != "zeros" or conv.bias is not None:
+    if conv.dilation != (1, 1) or conv.padding_mode != "zeros":
+        return False
+    # a conv bias in front of a training BN only shifts the batch mean (BN
+    # removes it; its gradient sum_m dy is exactly 0): the conv runs without it
+    # and the running mean takes the shift (_ConvBNActTrain)
+    if conv.bias is not None and (conv.groups != 1 or conv.bias.dtype != torch.float32):
         return False
     if conv.groups != 1:
         if is_depthwise(conv):
@@ -642,7 +647,8 @@ def _fork_sum(fork, g):
 
 class _ConvBNActTrain(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, gamma, beta, residual, meta, bn, want_preact, forks=(None, None)):
+    def forward(ctx, x, weight, gamma, beta, residual, meta, bn, want_preact, forks=(None, None),
+                cbias=None):
         # an unused output (the pre-activation) must not be materialised as a
         # zero gradient + layout copy: the kernels take null dout / dpre
         ctx.set_materialize_grads(False)
@@ -747,6 +753,10 @@ class _ConvBNActTrain(torch.autograd.Function):
         if not want_preact and Cout <= 2048:
             ctx.bnlink = BnLink(y, res if act != 0 else None, stats, act, M, Cout)
         _LAST_LINK[0] = ctx.bnlink
+        ctx.cbias = cbias is not None
+        if cbias is not None:
+            # BN(y + b) == BN(y) in training; the running mean tracks mean(y) + b
+            bn.running_mean.add_(cbias.detach(), alpha=float(bn.momentum))
         if want_preact:
             return out, pre
         return out, None
@@ -819,7 +829,9 @@ class _ConvBNActTrain(torch.autograd.Function):
             notify_grad(gamma, beta)
         dgamma = None if direct_gb else sums[1].clone()
         dbeta = None if direct_gb else sums[0].clone()
-        return dx, dw, dgamma, dbeta, dres, None, None, None, None
+        dcb = torch.zeros(Cout, dtype=torch.float32, device=dev) if (
+            ctx.cbias and ctx.needs_input_grad[9]) else None
+        return dx, dw, dgamma, dbeta, dres, None, None, None, None, dcb
 
 
 def _bn_train_forward(y, M, C, gamma, beta, bn, residual, act, want_preact):
@@ -915,7 +927,7 @@ def _dw_backward(ctx, dout, dpre):
         dw = None if direct_w else target
         if direct_w:
             notify_grad(weight)
-    return dx, dw, dgamma, dbeta, dres, None, None, None, None
+    return dx, dw, dgamma, dbeta, dres, None, None, None, None, None
 
 
 def pack_weights(weight, dgrad=True):
@@ -1188,7 +1200,7 @@ def conv_bn_act_train(x, conv, bn, act, residual, want_preact, fork=None, res_fo
         res_fork = None
     _LAST_LINK[0] = None
     out, pre = _ConvBNActTrain.apply(x, conv.weight, bn.weight, bn.bias, residual, meta, bn,
-                                     bool(want_preact), (fork, res_fork))
+                                     bool(want_preact), (fork, res_fork), conv.bias)
     link, _LAST_LINK[0] = _LAST_LINK[0], None
     if link is not None:
         out._mda_bnlink = link

@@ -91,6 +91,17 @@ def test_nst_loss():
     _grad_pair(lambda a, b: ref.nst_loss([a], [b]), lambda a, b: FL.nst_loss([a], [b]), fs, ft)
 
 
+def test_nst_gram_form_matches_reference():
+    """The closed-form one-Gram NST (used on the GPU) == the reference's
+    broadcast polynomial kernels, value and student gradient."""
+    ref = R.load("distillers", "NST")
+    torch.manual_seed(5)
+    fs = torch.randn(4, 16, 8, 8).contiguous(memory_format=torch.channels_last)
+    ft = torch.randn(4, 16, 8, 8).contiguous(memory_format=torch.channels_last)
+    _grad_pair(lambda a, b: ref.nst_loss([a], [b]),
+               lambda a, b: FL.single_stage_nst_loss_gram(a, b), fs, ft)
+
+
 def test_pkt_loss():
     ref = R.load("distillers", "PKT")
     torch.manual_seed(5)

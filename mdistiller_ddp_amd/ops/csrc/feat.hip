@@ -303,3 +303,109 @@ MDA_API int mda_vid_bwd(const void* pred, const void* ft, const float* log_scale
                      dls);
   MDA_CHECK_LAUNCH();
 }
+
+// ---------------------------------------------------------------------------
+// NST (reference distillers/NST.py:12-35) on the batched Gram of
+// W = [F_s | F_t] (ops/feat_losses.py _NSTGram): g [N, 2C, 2C] fp32 = W^T W,
+// r_i = sqrt(g_ii) (F.normalize's column norms), normalised Grams
+// S = g_ss / (r r), X = g_st / (r r), T = g_tt / (r r).
+//   nst_fwd  per-sample ||S||^2 + ||T||^2 - 2||X||^2 (one block per sample)
+//   nst_bwd  PQ [N, 2C, C]: rows c < C:  P_cd = (k S_cd - [c==d] dot_c) / (r_c r_d)
+//                           rows C + c:  Q_cd = -k g_{C+c,d} / (r_d^2 r_{C+c}^2)
+//            dot_c = k (sum_d S_cd^2 - sum_d X_cd^2), k = 4 go / (N C^2);
+//            dF_s = W PQ (one batched GEMM by the caller).
+namespace {
+constexpr int NST_CMAX = 1024;
+
+__device__ __forceinline__ float nst_r(const float* g, int C2, int i) {
+  return fmaxf(sqrtf(fmaxf(g[(int64_t)i * C2 + i], 0.f)), 1e-12f);
+}
+
+__global__ void __launch_bounds__(256)
+nst_fwd_kernel(const float* __restrict__ g, int C, float* __restrict__ part) {
+  __shared__ float rr[2 * NST_CMAX];
+  __shared__ float red[256];
+  const int C2 = 2 * C;
+  const float* gn = g + (int64_t)blockIdx.x * C2 * C2;
+  for (int i = threadIdx.x; i < C2; i += blockDim.x) rr[i] = 1.f / nst_r(gn, C2, i);
+  __syncthreads();
+  float acc = 0.f;
+  // ss (+1), tt (+1), st (-2) blocks
+  for (int64_t e = threadIdx.x; e < (int64_t)3 * C * C; e += blockDim.x) {
+    const int blk = (int)(e / ((int64_t)C * C));
+    const int rem = (int)(e - (int64_t)blk * C * C);
+    const int i = rem / C, j = rem - (rem / C) * C;
+    const int gi = blk == 1 ? C + i : i;
+    const int gj = blk == 0 ? j : C + j;
+    const float v = gn[(int64_t)gi * C2 + gj] * rr[gi] * rr[gj];
+    acc += (blk == 2 ? -2.f : 1.f) * v * v;
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+// grid (N, 2C / 8): 8 rows of PQ per block, one wave per row pair
+__global__ void __launch_bounds__(256)
+nst_bwd_kernel(const float* __restrict__ g, int N, int C, const float* __restrict__ go,
+               float* __restrict__ pq) {
+  __shared__ float rr[2 * NST_CMAX];
+  __shared__ float red[8][32];
+  const int C2 = 2 * C;
+  const int n = blockIdx.x;
+  const float* gn = g + (int64_t)n * C2 * C2;
+  for (int i = threadIdx.x; i < C2; i += blockDim.x) rr[i] = nst_r(gn, C2, i);
+  __syncthreads();
+  const float k = 4.f * go[0] / ((float)N * (float)C * (float)C);
+  const int sub = threadIdx.x / 32, lane = threadIdx.x % 32;  // 8 rows x 32 threads
+  const int row = blockIdx.y * 8 + sub;
+  float dot = 0.f;
+  if (row < C) {
+    float a = 0.f;
+    for (int d = lane; d < C; d += 32) {
+      const float s = gn[(int64_t)row * C2 + d] / (rr[row] * rr[d]);
+      const float x = gn[(int64_t)row * C2 + C + d] / (rr[row] * rr[C + d]);
+      a += s * s - x * x;
+    }
+    red[sub][lane] = a;
+  }
+  __syncthreads();
+  if (row < C) {
+    float a = 0.f;
+    for (int l = 0; l < 32; ++l) a += red[sub][l];
+    dot = k * a;
+  }
+  if (row < C2) {
+    float* out = pq + ((int64_t)n * C2 + row) * C;
+    for (int d = lane; d < C; d += 32) {
+      float v;
+      if (row < C) {
+        const float s = gn[(int64_t)row * C2 + d] / (rr[row] * rr[d]);
+        v = (k * s - (row == d ? dot : 0.f)) / (rr[row] * rr[d]);
+      } else {
+        const float rd = rr[d], rc = rr[row];
+        v = -k * gn[(int64_t)row * C2 + d] / (rd * rd * rc * rc);
+      }
+      out[d] = v;
+    }
+  }
+}
+}  // namespace
+
+MDA_API int mda_nst_fwd(const float* g, int64_t N, int64_t C, float* part, hipStream_t st) {
+  if (C <= 0 || C > NST_CMAX || N <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(nst_fwd_kernel, dim3((unsigned)N), dim3(256), 0, st, g, (int)C, part);
+  MDA_CHECK_LAUNCH();
+}
+
+MDA_API int mda_nst_bwd(const float* g, int64_t N, int64_t C, const float* go, float* pq,
+                        hipStream_t st) {
+  if (C <= 0 || C > NST_CMAX || N <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(nst_bwd_kernel, dim3((unsigned)N, (unsigned)((2 * C + 7) / 8)), dim3(256), 0, st,
+                     g, (int)N, (int)C, go, pq);
+  MDA_CHECK_LAUNCH();
+}

@@ -116,36 +116,52 @@ class _NSTGram(torch.autograd.Function):
         dot_c = k (sum_d S_cd^2 - sum_d X_cd^2),  k = 4 go / (N C^2)
         P = D_s (k S - diag(dot)) D_s,  Q = -k D_t X^T D_s,   D = diag(1/r)
         dF_s = F_s P + F_t Q = W [P; Q]          (one batched GEMM)
+    On the GPU the Gram algebra runs in csrc/feat.hip (mda_nst_fwd /
+    mda_nst_bwd); elsewhere in PyTorch ops.
     """
 
     @staticmethod
     @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
-    def forward(ctx, w):
-        # w: [N, HW, 2C] fp32 (student channels first); fp32 GEMMs (autocast off)
+    def forward(ctx, fs_cols, ft_cols):
+        # [N, HW, C] each; fp32 GEMMs (autocast off)
+        w = torch.cat([fs_cols, ft_cols], 2).float()
         N, _, C2 = w.shape
         C = C2 // 2
         g = torch.bmm(w.transpose(1, 2), w)
-        r = g.diagonal(dim1=1, dim2=2).clamp_min(0).sqrt().clamp_min(1e-12)
-        gh = g / (r.unsqueeze(2) * r.unsqueeze(1))
-        S, X, T = gh[:, :C, :C], gh[:, :C, C:], gh[:, C:, C:]
-        loss = (S.square().sum() + T.square().sum() - 2 * X.square().sum()) / (N * C * C)
-        ctx.save_for_backward(w, gh, r)
+        native = g.is_cuda and hip_enabled_for(g) and C <= 1024
+        if native:
+            part = torch.empty(N, dtype=torch.float32, device=g.device)
+            _ext.call("mda_nst_fwd", g, N, C, part)
+            loss = part.sum() / (N * C * C)
+        else:
+            r = g.diagonal(dim1=1, dim2=2).clamp_min(0).sqrt().clamp_min(1e-12)
+            gh = g / (r.unsqueeze(2) * r.unsqueeze(1))
+            S, X, T = gh[:, :C, :C], gh[:, :C, C:], gh[:, C:, C:]
+            loss = (S.square().sum() + T.square().sum() - 2 * X.square().sum()) / (N * C * C)
+        ctx.save_for_backward(w, g)
+        ctx.native = native
         return loss
 
     @staticmethod
     @torch.amp.custom_bwd(device_type="cuda")
     def backward(ctx, go):
-        w, gh, r = ctx.saved_tensors
+        w, g = ctx.saved_tensors
         N, _, C2 = w.shape
         C = C2 // 2
-        S, X = gh[:, :C, :C], gh[:, :C, C:]
-        k = 4.0 * go / (N * C * C)
-        rs, rt = r[:, :C], r[:, C:]
-        dot = k * (S.square().sum(2) - X.square().sum(2))
-        P = (k * S - torch.diag_embed(dot)) / (rs.unsqueeze(2) * rs.unsqueeze(1))
-        Q = -k * X.transpose(1, 2) / (rt.unsqueeze(2) * rs.unsqueeze(1))
-        dws = torch.bmm(w, torch.cat([P, Q], 1))
-        return torch.cat([dws, torch.zeros_like(dws)], 2)
+        if ctx.native:
+            pq = torch.empty(N, C2, C, dtype=torch.float32, device=g.device)
+            _ext.call("mda_nst_bwd", g, N, C, go.detach().float().reshape(1).contiguous(), pq)
+        else:
+            r = g.diagonal(dim1=1, dim2=2).clamp_min(0).sqrt().clamp_min(1e-12)
+            gh = g / (r.unsqueeze(2) * r.unsqueeze(1))
+            S, X = gh[:, :C, :C], gh[:, :C, C:]
+            k = 4.0 * go / (N * C * C)
+            rs, rt = r[:, :C], r[:, C:]
+            dot = k * (S.square().sum(2) - X.square().sum(2))
+            P = (k * S - torch.diag_embed(dot)) / (rs.unsqueeze(2) * rs.unsqueeze(1))
+            Q = -k * X.transpose(1, 2) / (rt.unsqueeze(2) * rs.unsqueeze(1))
+            pq = torch.cat([P, Q], 1)
+        return torch.bmm(w, pq), None
 
 
 def _nst_cols(f):
@@ -162,8 +178,7 @@ def single_stage_nst_loss_gram(f_s, f_t):
     f_s, f_t = _pool_to_match(f_s, f_t.detach())
     if f_s.shape[1] != f_t.shape[1]:
         return single_stage_nst_loss(f_s, f_t)
-    w = torch.cat([_nst_cols(f_s), _nst_cols(f_t)], 2).float()
-    return _NSTGram.apply(w)
+    return _NSTGram.apply(_nst_cols(f_s), _nst_cols(f_t))
 
 
 def nst_loss(g_s, g_t):

@@ -75,7 +75,8 @@ def main():
             row = {"config": name, "images_per_s": round(r["images_per_s"], 1),
                    "ms_per_step": round(r["ms_per_step"], 3), "per_gpu_batch": bs,
                    "n_gpus": r["n_gpus"], "graph": r["graph"], "dtype": r["dtype"],
-                   "final_loss": round(r["final_loss"], 4)}
+                   "final_loss": round(r["final_loss"], 4),
+                   "host_ms_per_step": round(r["host_ms_per_step"], 3)}
             if name in BASELINE_MS and r["n_gpus"] == 1 and bs == 64:
                 row["baseline_ms"] = BASELINE_MS[name]
                 row["speedup_vs_baseline"] = round(BASELINE_MS[name] / r["ms_per_step"], 2)

@@ -13,6 +13,8 @@ slowest rank's time is reported.
 """
 from __future__ import annotations
 
+import gc
+import os
 import time
 
 import torch
@@ -68,8 +70,19 @@ def run(cfg_file: str, per_gpu_batch: int, steps: int, warmup: int, opts=(), use
 
     set_backend(backend)
     streams.set_enabled(teacher_stream)
+    # release the graphs of an earlier run in this process first: a live graph
+    # keeps its internal parallel streams (and their hardware queues), which
+    # changes how the next step's concurrent streams share queues
+    gc.collect()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
     info = D.init_distributed() if not D.is_dist() else D.info()
     dev = info.device
+    # diagnostics: shift the position of the framework's streams in the stream
+    # pool (their hardware-queue assignment) by allocating k pool streams first
+    for _ in range(int(os.environ.get("MDA_DEBUG_SKIP_STREAMS", "0"))):
+        torch.cuda.Stream(device=dev)
     if dev.type == "cuda":
         torch.backends.cudnn.benchmark = True
     cfg = get_cfg()
@@ -115,6 +128,14 @@ def run(cfg_file: str, per_gpu_batch: int, steps: int, warmup: int, opts=(), use
 
     for _ in range(warmup):
         cur = advance(cur)
+    # the set-up objects (models, graphs, earlier configs in this process) move to
+    # the permanent generation: the timed loop's generation-2 collections no longer
+    # walk them.  Launch-bound steps (DOT's five graph replays) otherwise slow down
+    # with the process history (1.33 -> 1.60 ms/step after two other configs)
+    gc_frozen = os.environ.get("MDA_GC_FREEZE", "1") != "0"
+    if gc_frozen:
+        gc.collect()
+        gc.freeze()
     sync()
     D.barrier()
     sync()
@@ -139,6 +160,8 @@ def run(cfg_file: str, per_gpu_batch: int, steps: int, warmup: int, opts=(), use
         cur = advance(cur)
         hs.append(time.perf_counter() - h0)
     sync()
+    if gc_frozen:
+        gc.unfreeze()
     m = step.meters.summary(reduce=True)
     n = info.world_size
     same = None

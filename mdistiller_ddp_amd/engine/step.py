@@ -161,6 +161,9 @@ class TrainStep:
         self.distiller = distiller
         self.cfg = cfg
         self.device = torch.device(device)
+        if self.device.type == "cuda":
+            from ..runtime import streams as _streams
+            _streams.renew(self.device)  # same stream layout as a fresh process
         self.trainer = trainer
         self.is_dot = trainer in ("dot", "crd_dot")
         self.dtype = dtype

@@ -42,6 +42,21 @@ def side_stream(device) -> "torch.cuda.Stream":
         return s
 
 
+def renew(device) -> None:
+    """Forget this device's cached teacher and branch streams: the next use
+    takes fresh ones from the stream pool.  Called when a training step is
+    built, so every step gets its streams in the same relative order as in a
+    fresh process.  (HIP assigns a stream's hardware queue at creation; with
+    the 4 queues of a process, which of a step's concurrently replayed streams
+    share a queue decides whether they overlap -- DOT's dual-stream step ran
+    1.33 ms/step alone and 1.59-1.60 after another DOT or two other configs
+    in the same process, `profiles/r3_dot_history.md`.)"""
+    idx = torch.device(device).index or 0
+    with _lock:
+        _streams.pop(idx, None)
+        _branch_streams.pop(idx, None)
+
+
 def _tensors(obj, out):
     if isinstance(obj, torch.Tensor):
         out.append(obj)

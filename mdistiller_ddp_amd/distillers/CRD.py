@@ -118,10 +118,45 @@ class ContrastMemory(nn.Module):
         return out_v1, out_v2
 
     def apply_pending(self):
+        """After backward: world 1 applies the bank update; world > 1 packs the
+        rank's (index, v1, v2) rows into a persistent buffer for
+        :meth:`exchange` (eager, between the captured graphs) and
+        :meth:`apply_exchange` (inside the update graph)."""
         pend = getattr(self, "_pending", None)
-        if pend is not None:
-            self._pending = None
-            self.update(*pend)
+        if pend is None:
+            return
+        self._pending = None
+        v1, v2, y = pend
+        if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+            self.update(v1, v2, y)
+            return
+        ws = dist.get_world_size()
+        B, D = v1.shape
+        xl = getattr(self, "_xlocal", None)
+        if xl is None or xl.shape != (B, 1 + 2 * D) or xl.device != v1.device:
+            # (eager steps only: a capture reuses the warm-up's buffers)
+            self._xlocal = torch.empty(B, 1 + 2 * D, dtype=torch.float64, device=v1.device)
+            self._xall = torch.empty(ws * B, 1 + 2 * D, dtype=torch.float64, device=v1.device)
+        self._xlocal[:, 0].copy_(y)
+        self._xlocal[:, 1:1 + D].copy_(v1)
+        self._xlocal[:, 1 + D:].copy_(v2)
+        self._xdim = D
+
+    def exchange(self):
+        """The memory-update all-gather (a collective: never inside a capture
+        in split mode; TrainStep calls it between the graphs)."""
+        if getattr(self, "_xlocal", None) is not None:
+            dist.all_gather_into_tensor(self._xall, self._xlocal)
+
+    @torch.no_grad()
+    def apply_exchange(self):
+        xa = getattr(self, "_xall", None)
+        if xa is None:
+            return
+        D = self._xdim
+        y = xa[:, 0].long()
+        CO.update(self.memory_v1, y, xa[:, 1:1 + D].float(), self.momentum)
+        CO.update(self.memory_v2, y, xa[:, 1 + D:].float(), self.momentum)
 
     @torch.no_grad()
     def update(self, v1, v2, y):
@@ -141,7 +176,8 @@ class ContrastMemory(nn.Module):
 
 class CRD(Distiller):
     teacher_needs = ("pooled",)
-    collective_in_forward = True  # memory-update exchange (keeps hipGraph off for world > 1)
+    # the memory-update exchange runs between the captured graphs (exchange /
+    # apply_exchange), so CRD keeps hipGraphs at world > 1
 
     def __init__(self, student, teacher, cfg, num_data):
         super().__init__(student, teacher)
@@ -159,8 +195,17 @@ class CRD(Distiller):
         return n + sum(b.numel() for b in self.contrast.buffers())
 
     def post_backward(self):
-        """Apply this step's memory-bank update (called by the trainer after backward)."""
+        """Apply (world 1) or stage (world > 1) this step's memory-bank update
+        (called by the trainer after backward)."""
         self.contrast.apply_pending()
+
+    def exchange(self):
+        """world > 1: all-gather the staged updates (eager, between graphs)."""
+        self.contrast.exchange()
+
+    def apply_exchange(self):
+        """world > 1: apply every rank's update in rank order (in the update graph)."""
+        self.contrast.apply_exchange()
 
     def crd_loss(self, f_s, f_t, idx, contrast_idx):
         f_s = self.embed_s(f_s)

@@ -411,14 +411,25 @@ class TrainStep:
         return preds, losses
 
     def _reduce(self):
+        """The step's collectives: the gradient all-reduce, then any exchange the
+        distiller staged after its backward (CRD's memory-update all-gather).
+        Eager between the fwd+bwd and update graphs (split mode), captured in
+        the one graph in ``DIST.GRAPH_COMM=capture`` mode."""
         if self.world <= 1:
             return
         if self.is_dot:
             self.reducer.reduce_sets((0, 1))
         else:
             self.reducer.finish()
+        exchange = getattr(self.distiller, "exchange", None)
+        if exchange is not None:
+            exchange()
 
     def _update(self, preds, target, losses):
+        if self.world > 1:
+            apply = getattr(self.distiller, "apply_exchange", None)
+            if apply is not None:
+                apply()
         self.opt.step()
         self.meters.update(preds, target, losses)
 

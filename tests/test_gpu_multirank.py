@@ -8,6 +8,8 @@ test exercises the same multi-rank code paths on the single-GPU box:
   all-reduce -> optimizer graph) replays 20 steps and the replicas stay
   bit-identical, for the base trainer (native bf16 conv/BN kernels, DKD) and
   for DOT (both gradient sets in one reduction, bf16 wire);
+* CRD keeps hipGraphs at world > 1: its memory-update all-gather runs between
+  the fwd+bwd and update graphs, and the banks stay identical across ranks;
 * the all-reduced gradients equal the mean of the per-rank gradients.
 """
 import os
@@ -43,7 +45,7 @@ def _worker(rank, world, port, scenario, outdir):
     _ext.load(required=True)
     D.init_distributed("gloo", 120.0, device="cuda")
     dev = torch.device("cuda", 0)
-    typ, trainer = {"dkd": ("DKD", "base"), "dot": ("KD", "dot")}[scenario]
+    typ, trainer = {"dkd": ("DKD", "base"), "dot": ("KD", "dot"), "crd": ("CRD", "crd")}[scenario]
     cfg = get_cfg()
     cfg.DISTILLER.TYPE = typ
     cfg.DISTILLER.TEACHER = "resnet32x4"
@@ -54,17 +56,25 @@ def _worker(rank, world, port, scenario, outdir):
     cfg.DIST.GRAPH_COMM = "split"
     if scenario == "dot":
         cfg.DIST.GRAD_DTYPE = "bf16"
+    cfg.CRD.NCE.K = 256
     torch.manual_seed(1000 + rank)  # different init per rank
-    d = build_distiller(cfg, 100, dev)
+    d = build_distiller(cfg, 100, dev, num_data=1000)
     d.train()
-    st = TrainStep(d, cfg, dev, trainer=trainer, use_graph=True, dtype=torch.bfloat16)
+    keys = ("image", "target", "index", "contrastive_index") if typ == "CRD" else ("image", "target")
+    st = TrainStep(d, cfg, dev, trainer=trainer, use_graph=True, dtype=torch.bfloat16,
+                   batch_keys=keys)
     c0 = state_checksum(d, st.flat, buffers=True)
     allc = [torch.empty_like(c0) for _ in range(world)]
     dist.all_gather(allc, c0)
     out = {"init_equal": all(torch.equal(allc[0], a) for a in allc)}
     st.set_epoch(1.0)
     init = st.flat.data.clone()
-    ld = SyntheticLoader("cifar100", 32, dev, steps_per_epoch=20, channels_last=True, seed=rank)
+    ld = SyntheticLoader("cifar100", 32, dev, steps_per_epoch=20, channels_last=True, seed=rank,
+                         crd_k=256, num_data=1000)
+    if typ == "CRD":  # distinct dataset indices across ranks (a sharded sampler's guarantee)
+        for i, b in enumerate(ld.batches):
+            b["index"] = (torch.arange(32, device=dev) + 32 * (2 * i + rank)) % 1000
+            b["contrastive_index"][:, 0] = b["index"]
     for b in ld:
         st.step(b)
     torch.cuda.synchronize()
@@ -81,6 +91,11 @@ def _worker(rank, world, port, scenario, outdir):
     out["moved"] = float((flat - init).norm() / init.norm())
     m = st.meters.summary(reduce=True)
     out["loss"] = m["loss"]
+    if typ == "CRD":  # the memory banks stay identical: the exchange ran between the graphs
+        mem = torch.cat([d.contrast.memory_v1.reshape(-1), d.contrast.memory_v2.reshape(-1)])
+        allm = [torch.empty_like(mem) for _ in range(world)]
+        dist.all_gather(allm, mem)
+        out["memory_equal"] = all(torch.equal(allm[0], a) for a in allm)
     if scenario == "dkd":
         # reduced grad == mean of the local grads (one eager fwd+bwd)
         st.flat.zero_grad()
@@ -106,7 +121,7 @@ def _spawn(scenario, world=2):
 
 
 @pytest.mark.timeout(400)
-@pytest.mark.parametrize("scenario", ["dkd", "dot"])
+@pytest.mark.parametrize("scenario", ["dkd", "dot", "crd"])
 def test_two_ranks_one_gpu_graph_replicas(scenario):
     res = _spawn(scenario)
     for r in res:
@@ -118,3 +133,5 @@ def test_two_ranks_one_gpu_graph_replicas(scenario):
         assert r["loss"] == r["loss"] and abs(r["loss"]) < 1e6
     if scenario == "dkd":
         assert res[0]["grad_rel"] < 1e-5, res[0]
+    if scenario == "crd":
+        assert all(r["memory_equal"] for r in res), res

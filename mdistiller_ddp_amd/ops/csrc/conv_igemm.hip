@@ -93,6 +93,7 @@ struct ConvParams {
   // channels, and a block's N tile never leaves its group (grid.y = groups x
   // tiles per group).  Dense: ldx = Cin, cout_g = Cout.
   int ldx, cout_g;
+  int xcd;  // glds kernel: XCD-aware tile order (MDA_CONV_XCD, default on)
 };
 
 // first output channel past the group of the tile starting at n0
@@ -473,7 +474,7 @@ __device__ __forceinline__ void conv_epilogue_rows(const ConvParams& p, char* sm
           acc_add(region_acc(p.stats_slot, p.Cout, (int)blockIdx.x % slot_shards(p.Cout), q) + n0 + c,
                   (double)(a0 + a1));
         else
-          p.stats_part[((int64_t)blockIdx.x * 2 + q) * p.Cout + n0 + c] = a0 + a1;
+          p.stats_part[((int64_t)(m0 / rows) * 2 + q) * p.Cout + n0 + c] = a0 + a1;
       }
     }
     return;
@@ -832,8 +833,21 @@ conv_glds_kernel(const ConvParams p) {
   const int lane = tid & 63;
   const int wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  const int m0 = blockIdx.x * BM;
-  const int n0 = group_n0(p, blockIdx.y, BN);
+  // XCD-aware tile order: blocks b, b + 8, ... share an XCD (and its L2); each
+  // XCD gets a contiguous run of tiles in (m, n) order, so the N tiles of one
+  // block of rows -- which read the same A rows -- run on one L2 (bijective
+  // for any tile count; cdna_hip_programming.md T1)
+  int mt = blockIdx.x, nt = blockIdx.y;
+  if (p.xcd) {
+    const int nwg = gridDim.x * gridDim.y;
+    const int bid = blockIdx.x + gridDim.x * blockIdx.y;
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    mt = wg / gridDim.y;
+    nt = wg - mt * gridDim.y;
+  }
+  const int m0 = mt * BM;
+  const int n0 = group_n0(p, nt, BN);
   const int nlim = group_nlim(p, n0);
   const int xoff = (n0 / p.cout_g) * p.Cin;  // grouped: this group's first x channel
   const int trow = tid >> 3;                              // row within each 32-row slab
@@ -1641,6 +1655,14 @@ bool use_halo1() {
   return on;
 }
 
+bool use_xcd_remap() {
+  static const bool on = [] {
+    const char* e = getenv("MDA_CONV_XCD");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 bool use_par_dgrad() {
   static const bool on = [] {
     const char* e = getenv("MDA_DGRAD_PARITY");
@@ -1757,6 +1779,7 @@ int dispatch(ConvParams& p, int mode, int64_t tile, int64_t splits, hipStream_t 
   if (p.Kp % BK || p.Kp < p.K) return (int)hipErrorInvalidValue;
   if (p.ldx <= 0) p.ldx = p.Cin;
   if (p.cout_g <= 0) p.cout_g = p.Cout;
+  p.xcd = use_xcd_remap() ? 1 : 0;
   if (p.cout_g < p.Cout) {  // grouped: group-aligned tiles on the glds kernel only
     if (p.Cout % p.cout_g || p.ldx != p.Cin * (p.Cout / p.cout_g) || p.cout_g % 8 || p.Cin % 8)
       return (int)hipErrorInvalidValue;

@@ -1,7 +1,11 @@
 set -o pipefail
-mkdir -p gpurun_out; export PYTHONPATH=$PWD TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 180 --timeout-method thread > gpurun_out/full_gpu.log 2>&1; rc=$?; tail -3 gpurun_out/full_gpu.log; [ $rc -ne 0 ] && { grep -E "Error|assert|FAILED" gpurun_out/full_gpu.log | head -20; exit $rc; }
-timeout -k 10 200 python bench.py --steps 300 --warmup 20 > gpurun_out/flag300.log 2>&1 || exit 1
-tail -1 gpurun_out/flag300.log | cut -c1-200
-timeout -k 10 900 python benchmarks/throughput.py --configs all --steps 60 --warmup 15 --out gpurun_out/r3_tp_all.jsonl > gpurun_out/tp_all.log 2>&1 || exit 1
-PROF="configs/cifar100/dkd/res32x4_res8x4.yaml:r3_flagship;configs/imagenet/r50_mv1/dkd.yaml:r3_r50_mv1;configs/cifar100/dkd/vgg13_mv2.yaml:r3_vgg13_mv2;configs/cifar100/dkd/res32x4_shuv1.yaml:r3_shuv1" bash scripts/gpu_run.sh
+mkdir -p gpurun_out; export PYTHONPATH=$PWD
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+i=0
+for grp in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE" "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU" "SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_INSTS_VMEM_WR" "TCC_HIT_sum TCC_EA0_WRREQ_sum" "TCC_EA0_RDREQ_sum TCC_MISS_sum"; do
+  i=$((i+1))
+  timeout -s KILL 90 rocprofv3 --output-format csv --pmc $grp -d gpurun_out/pmc1_g$i -o run -- python scripts/conv_microbench.py --set imagenet --iters 10 --shape 1 --ops fwd > gpurun_out/pmc1_g$i.log 2>&1 || { tail -5 gpurun_out/pmc1_g$i.log; exit 1; }
+  MDA_CONV_GLDS=0 timeout -s KILL 90 rocprofv3 --output-format csv --pmc $grp -d gpurun_out/pmc1_r$i -o run -- python scripts/conv_microbench.py --set imagenet --iters 10 --shape 1 --ops fwd > gpurun_out/pmc1_r$i.log 2>&1 || { tail -5 gpurun_out/pmc1_r$i.log; exit 1; }
+done
+python scripts/pmc_summary.py gpurun_out "pmc1_g*" conv_glds
+python scripts/pmc_summary.py gpurun_out "pmc1_r*" conv_fwd

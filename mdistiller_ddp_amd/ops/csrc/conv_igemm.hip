@@ -1655,6 +1655,15 @@ bool use_halo1() {
   return on;
 }
 
+// MDA_REG1X1_MIN_M: smallest M of a 1x1 forward conv sent to the register-staged kernel
+int reg1x1_min_m() {
+  static const int v = [] {
+    const char* e = getenv("MDA_REG1X1_MIN_M");
+    return e ? atoi(e) : 32768;
+  }();
+  return v;
+}
+
 bool use_xcd_remap() {
   static const bool on = [] {
     const char* e = getenv("MDA_CONV_XCD");
@@ -1704,7 +1713,12 @@ int launch_tile(const ConvParams& p, int mode, int splits, hipStream_t st) {
                                    : (p.Cout + BN - 1) / BN;
   dim3 grid((p.M + BM - 1) / BM, ny, splits);
   if (p.cout_g < p.Cout && (mode == LOAD_SCALAR || !use_glds())) return (int)hipErrorInvalidValue;
-  if (mode != LOAD_SCALAR && use_glds() && p.steps_per_split <= ring1_max()) {  // short-K blocks
+  // large-M 1x1 forward convs are output-bandwidth bound: the register-staged
+  // kernel streams them 1.2-1.4x faster than the LDS-DMA one
+  // (profiles/r3_conv1x1_imagenet.md)
+  const bool reg1x1 = p.KH == 1 && p.KW == 1 && p.cout_g >= p.Cout && p.M >= reg1x1_min_m() &&
+                      (mode == LOAD_FAST || mode == LOAD_VEC8);
+  if (mode != LOAD_SCALAR && use_glds() && !reg1x1 && p.steps_per_split <= ring1_max()) {  // short-K blocks
     if (mode == LOAD_FAST)
       hipLaunchKernelGGL((conv_glds_kernel<BM, BN, LOAD_FAST, 1>), grid, dim3(256), 0, st, p);
     else if (mode == LOAD_VEC8)
@@ -1715,7 +1729,7 @@ int launch_tile(const ConvParams& p, int mode, int splits, hipStream_t st) {
       hipLaunchKernelGGL((conv_glds_kernel<BM, BN, LOAD_DGRAD_VEC8, 1>), grid, dim3(256), 0, st, p);
     return (int)hipGetLastError();
   }
-  if (mode != LOAD_SCALAR && use_glds()) {
+  if (mode != LOAD_SCALAR && use_glds() && !reg1x1) {
     if (mode == LOAD_FAST)
       hipLaunchKernelGGL((conv_glds_kernel<BM, BN, LOAD_FAST>), grid, dim3(256), 0, st, p);
     else if (mode == LOAD_VEC8)

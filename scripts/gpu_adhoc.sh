@@ -1,11 +1,11 @@
 set -o pipefail
-mkdir -p gpurun_out; export PYTHONPATH=$PWD
-cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-i=0
-for grp in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE" "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU" "SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_INSTS_VMEM_WR" "TCC_HIT_sum TCC_EA0_WRREQ_sum" "TCC_EA0_RDREQ_sum TCC_MISS_sum"; do
-  i=$((i+1))
-  timeout -s KILL 90 rocprofv3 --output-format csv --pmc $grp -d gpurun_out/pmc1_g$i -o run -- python scripts/conv_microbench.py --set imagenet --iters 10 --shape 1 --ops fwd > gpurun_out/pmc1_g$i.log 2>&1 || { tail -5 gpurun_out/pmc1_g$i.log; exit 1; }
-  MDA_CONV_GLDS=0 timeout -s KILL 90 rocprofv3 --output-format csv --pmc $grp -d gpurun_out/pmc1_r$i -o run -- python scripts/conv_microbench.py --set imagenet --iters 10 --shape 1 --ops fwd > gpurun_out/pmc1_r$i.log 2>&1 || { tail -5 gpurun_out/pmc1_r$i.log; exit 1; }
+mkdir -p gpurun_out; export PYTHONPATH=$PWD TMPDIR=/tmp
+run() { tag=$1; shift; timeout -k 10 200 "$@" > gpurun_out/q_$tag.log 2>&1 || { tail -5 gpurun_out/q_$tag.log; exit 1; }; echo "$tag $(tail -1 gpurun_out/q_$tag.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"])')"; }
+for v in 32768 999999999; do
+MDA_REG1X1_MIN_M=$v timeout -k 10 120 python scripts/conv_microbench.py --set cifar --shape 9 --ops fwd --graph --iters 30 > gpurun_out/cv.log 2>&1 || exit 1
+echo "cifar1x1 $v $(grep shape gpurun_out/cv.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["fwd_us"])')"
+MDA_REG1X1_MIN_M=$v run r50_$v python bench.py --steps 30 --warmup 10 --cfg configs/imagenet/r50_mv1/dkd.yaml
+MDA_REG1X1_MIN_M=$v run flag_$v python bench.py --steps 300 --warmup 20
+MDA_REG1X1_MIN_M=$v run mv2_$v python bench.py --steps 100 --warmup 20 --cfg configs/cifar100/dkd/vgg13_mv2.yaml
 done
-python scripts/pmc_summary.py gpurun_out "pmc1_g*" conv_glds
-python scripts/pmc_summary.py gpurun_out "pmc1_r*" conv_fwd
+timeout -k 10 300 python -u -m pytest tests/test_gpu_conv.py tests/test_gpu_train_layers.py -x -q --timeout 150 --timeout-method thread > gpurun_out/t_c.log 2>&1; rc=$?; tail -2 gpurun_out/t_c.log; exit $rc

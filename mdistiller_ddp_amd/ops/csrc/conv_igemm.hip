@@ -1716,7 +1716,9 @@ int launch_tile(const ConvParams& p, int mode, int splits, hipStream_t st) {
   // large-M 1x1 forward convs are output-bandwidth bound: the register-staged
   // kernel streams them 1.2-1.4x faster than the LDS-DMA one
   // (profiles/r3_conv1x1_imagenet.md)
-  const bool reg1x1 = p.KH == 1 && p.KW == 1 && p.cout_g >= p.Cout && p.M >= reg1x1_min_m() &&
+  // (also every short-K one: the CIFAR shortcuts, flagship 0.92-0.93 -> 0.913 ms)
+  const bool reg1x1 = p.KH == 1 && p.KW == 1 && p.cout_g >= p.Cout &&
+                      (p.M >= reg1x1_min_m() || p.Kp <= 4 * BK) &&
                       (mode == LOAD_FAST || mode == LOAD_VEC8);
   if (mode != LOAD_SCALAR && use_glds() && !reg1x1 && p.steps_per_split <= ring1_max()) {  // short-K blocks
     if (mode == LOAD_FAST)

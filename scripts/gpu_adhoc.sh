@@ -2,15 +2,8 @@ set -o pipefail
 mkdir -p gpurun_out; export PYTHONPATH=$PWD TMPDIR=/tmp
 run() { tag=$1; shift; timeout -k 10 200 "$@" > gpurun_out/q_$tag.log 2>&1 || { tail -3 gpurun_out/q_$tag.log; return 0; }; echo "$tag $(tail -1 gpurun_out/q_$tag.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"])')"; }
 run base python bench.py --steps 300 --warmup 20
-run glds0 env MDA_CONV_GLDS=0 python bench.py --steps 300 --warmup 20
-run ring8 env MDA_HALO_RING=8 python bench.py --steps 300 --warmup 20
-run tgt128 env MDA_CONV_TARGET=128 python bench.py --steps 300 --warmup 20
-run tgt512 env MDA_CONV_TARGET=512 python bench.py --steps 300 --warmup 20
-run r1max8 env MDA_GLDS_RING1_MAX=8 python bench.py --steps 300 --warmup 20
-run narrow0 env MDA_HALO_NARROW=0 python bench.py --steps 300 --warmup 20
-run halo2off env MDA_CONV_HALO2=0 python bench.py --steps 300 --warmup 20
-run branch1 env MDA_BRANCH_STREAMS=1 python bench.py --steps 300 --warmup 20
-run wgstream python bench.py --steps 300 --warmup 20 RUNTIME.WGRAD_STREAM on
-run nodefer python bench.py --steps 300 --warmup 20 RUNTIME.WGRAD_DEFER False
-run reg1x1all env MDA_REG1X1_MIN_M=0 python bench.py --steps 300 --warmup 20
 run base2 python bench.py --steps 300 --warmup 20
+run r50 python bench.py --steps 30 --warmup 10 --cfg configs/imagenet/r50_mv1/dkd.yaml
+run r34 python bench.py --steps 30 --warmup 10 --batch 32 --cfg configs/imagenet/r34_r18/reviewkd.yaml
+run mv2 python bench.py --steps 100 --warmup 20 --cfg configs/cifar100/dkd/vgg13_mv2.yaml
+run shuv1 python bench.py --steps 100 --warmup 20 --cfg configs/cifar100/dkd/res32x4_shuv1.yaml

@@ -431,22 +431,30 @@ conv_wgrad_glds_kernel(const WgParams p) {
 // and the 16 slice sums combine in a fixed order (deterministic).  With up to
 // 128 sets per layer the earlier 4-slice version walked ~30 dependent loads
 // per thread (14 us per ResNet-18 layer); this one issues ~8.
-constexpr int WGR_COLS = 16, WGR_SLICES = 16;
+// Slices per block adapt to the split count (round 3): S = 1 for <= 8 sets
+// (each thread sums all sets of ONE float4 column: 256 columns per block),
+// up to 16 for > 64 sets (16 columns per block, as before).  The flagship's
+// deferred multi-layer reduce was 18,944 blocks of 64 elements each: 29 us.
+__host__ __device__ __forceinline__ int wgr_slices(int splits) {
+  return splits <= 8 ? 1 : splits <= 16 ? 2 : splits <= 32 ? 4 : splits <= 64 ? 8 : 16;
+}
+__host__ __device__ __forceinline__ int wgr_cols(int splits) { return 256 / wgr_slices(splits); }
 
 __device__ __forceinline__ void wgrad_reduce_block(
     int64_t blk, const float* __restrict__ partial, float* __restrict__ grad, int splits, int Cout,
     int Cin, int KH, int KW, int Kp, float scale, int accumulate, int cin_keep, int groups) {
-  __shared__ float4 red[WGR_SLICES][WGR_COLS];
-  const int c = threadIdx.x % WGR_COLS, sl = threadIdx.x / WGR_COLS;
+  __shared__ float4 red[256];
+  const int S = wgr_slices(splits), CP = 256 / S;
+  const int c = threadIdx.x % CP, sl = threadIdx.x / CP;
   const int64_t total4 = (int64_t)Cout * Kp / 4;
-  const int64_t e4 = blk * WGR_COLS + c;
+  const int64_t e4 = blk * CP + c;
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
   if (e4 < total4) {
     const float4* src = (const float4*)partial + e4;
     float4 b = a;
     int s = sl;
-    for (; s + WGR_SLICES < splits; s += 2 * WGR_SLICES) {
-      const float4 u0 = src[(int64_t)s * total4], u1 = src[(int64_t)(s + WGR_SLICES) * total4];
+    for (; s + S < splits; s += 2 * S) {
+      const float4 u0 = src[(int64_t)s * total4], u1 = src[(int64_t)(s + S) * total4];
       a.x += u0.x; a.y += u0.y; a.z += u0.z; a.w += u0.w;
       b.x += u1.x; b.y += u1.y; b.z += u1.z; b.w += u1.w;
     }
@@ -456,14 +464,18 @@ __device__ __forceinline__ void wgrad_reduce_block(
     }
     a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
   }
-  red[sl][c] = a;
-  __syncthreads();
-  if (sl != 0 || e4 >= total4) return;
-  float v[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int q = 0; q < WGR_SLICES; ++q) {
-    const float4 r = red[q][c];
-    v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
+  float v[4] = {a.x, a.y, a.z, a.w};
+  if (S > 1) {
+    red[sl * CP + c] = a;
+    __syncthreads();
+    if (sl != 0 || e4 >= total4) return;
+    v[0] = v[1] = v[2] = v[3] = 0.f;
+    for (int q = 0; q < S; ++q) {
+      const float4 r = red[q * CP + c];
+      v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
+    }
+  } else if (e4 >= total4) {
+    return;
   }
   const int K = Cin * KH * KW;
 #pragma unroll
@@ -792,7 +804,8 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* partial, float*
   int rc = (int)hipGetLastError();
   if (rc || !reduce) return rc;
   const int64_t total4 = Cout * Kp / 4;  // Kp % 64 == 0
-  const int blocks = (int)((total4 + WGR_COLS - 1) / WGR_COLS);
+  const int cp = wgr_cols((int)splits);
+  const int blocks = (int)((total4 + cp - 1) / cp);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, partial, grad,
                      (int)splits, (int)Cout, (int)Cin, (int)KH, (int)KW, (int)Kp, scale,
                      (int)accumulate, (int)cin_keep, (int)(groups > 1 ? groups : 1));
@@ -840,7 +853,8 @@ MDA_API int mda_wgrad_reduce_multi(const int64_t* rows, int64_t n, hipStream_t s
       L.scale = 1.f;
       L.blk0 = blk;
       if (L.Cout % 8 || L.Kp % 64 || L.splits < 1) return (int)hipErrorInvalidValue;
-      blk += (int)(((int64_t)L.Cout * L.Kp / 4 + WGR_COLS - 1) / WGR_COLS);
+      const int cp = wgr_cols(L.splits);
+      blk += (int)(((int64_t)L.Cout * L.Kp / 4 + cp - 1) / cp);
     }
     hipLaunchKernelGGL(wgrad_reduce_multi_kernel, dim3((unsigned)blk), dim3(256), 0, st, t);
     const int rc = (int)hipGetLastError();

@@ -54,6 +54,7 @@ SIGNATURES = {
     "mda_vid_loss": "ppp" + "ii" + "f" + "pp" + "s",
     "mda_vid_bwd": "pppp" + "p" + "ii" + "f" + "pp" + "s",
     "mda_nst_fwd": "p" + "ii" + "p" + "s",
+    "mda_dw_fwd_bnacc": "pppp" + "i" * 10 + "s",
     "mda_nst_bwd": "p" + "ii" + "pp" + "s",
     "mda_conv_wgrad": "pppp" + "i" * 13 + "fiiis",
     "mda_conv_wgrad_nored": "pppp" + "i" * 13 + "fiiis",

@@ -20,6 +20,7 @@
 // loads); folded teacher weights are packed once on the host.  3x3 kernels,
 // stride 1 or 2 (every depthwise layer of the model zoo); others use PyTorch.
 #include "common.h"
+#include "bnslot.h"
 
 namespace {
 
@@ -96,6 +97,11 @@ struct DwParams {
   bf16_t* y;            // output
   bf16_t* preact;       // or null
   int N, H, W, C, Ho, Wo, KH, KW, stride, pad, act;
+  // training BN after the conv (round 3): the block's sum y / sum y^2 of the
+  // stored bf16 output go into this region (csrc/bnslot.h) instead of a
+  // separate statistics pass; needs a grid stride that is a multiple of C / V
+  // (every thread keeps one channel group), see launch_fwd
+  BnRegion* stats_slot;
 };
 
 template <int V, int S>
@@ -104,6 +110,9 @@ __global__ void __launch_bounds__(256) dw_fwd_kernel(const DwParams p) {
   const int CG = p.C / V;
   const int WT = (p.Wo + OWT - 1) / OWT;
   const int64_t total = (int64_t)p.N * p.Ho * WT * CG;
+  float st1[V], st2[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) st1[v] = st2[v] = 0.f;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int cg = (int)(i % CG);
@@ -116,6 +125,7 @@ __global__ void __launch_bounds__(256) dw_fwd_kernel(const DwParams p) {
     const int wo0 = wt * OWT;
     const int iw0 = wo0 * S - p.pad;
     float wv[KS * KS][V];
+    (void)c0;
 #pragma unroll
     for (int t = 0; t < KS * KS; ++t) ld_w<V>(p.w + t * p.C + c0, wv[t]);
     typename vec<V>::t raw[KS][NCOLS];
@@ -171,7 +181,37 @@ __global__ void __launch_bounds__(256) dw_fwd_kernel(const DwParams p) {
 #pragma unroll
       for (int v = 0; v < V; ++v) t[v] = act_fn(t[v], p.act);
       st_vec<V>(p.y + o, t);
+      if (p.stats_slot) {
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          const float q = bf2f(f2bf(t[v]));  // the stored value
+          st1[v] += q;
+          st2[v] += q * q;
+        }
+      }
     }
+  }
+  if (p.stats_slot == nullptr) return;
+  // block sums per channel, deterministic: thread t always held channel group
+  // (blockIdx.x * 256 + t) % CG; channel c sums the threads of its group in order
+  __shared__ float red[256][2 * V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    red[threadIdx.x][v] = st1[v];
+    red[threadIdx.x][V + v] = st2[v];
+  }
+  __syncthreads();
+  const int base = (int)(((int64_t)blockIdx.x * blockDim.x) % CG);
+  const int shard = (int)blockIdx.x % slot_shards(p.C);
+  for (int c = threadIdx.x; c < p.C; c += blockDim.x) {
+    const int g = c / V, e = c - g * V;
+    float a = 0.f, b = 0.f;
+    for (int t = ((g - base) % CG + CG) % CG; t < (int)blockDim.x; t += CG) {
+      a += red[t][e];
+      b += red[t][V + e];
+    }
+    acc_add(region_acc(p.stats_slot, p.C, shard, 0) + c, (double)a);
+    acc_add(region_acc(p.stats_slot, p.C, shard, 1) + c, (double)b);
   }
 }
 
@@ -426,7 +466,19 @@ inline int grid_for(int64_t work) {
 int launch_fwd(const DwParams& p, hipStream_t st) {
   const int V = vwidth(p.C);
   const int64_t work = (int64_t)p.N * p.Ho * ((p.Wo + OWT - 1) / OWT) * (p.C / V);
-  const dim3 g(grid_for(work));
+  int nb = grid_for(work);
+  if (p.stats_slot) {
+    // grid stride a multiple of CG (each thread keeps its channel group); at most
+    // 256 blocks per region shard, so each region address sees few atomics
+    const int CG = p.C / V;
+    int a = CG, b = 256;
+    while (b) { const int t = a % b; a = b; b = t; }
+    const int unit = CG / a;  // blocks per stride period
+    const int cap = 256 * slot_shards(p.C);
+    nb = nb < cap ? nb : cap;
+    nb = (nb + unit - 1) / unit * unit;
+  }
+  const dim3 g(nb);
 #define DW_FWD(VV, SS) hipLaunchKernelGGL((dw_fwd_kernel<VV, SS>), g, dim3(256), 0, st, p)
   if (p.stride == 1) {
     if (V == 8) DW_FWD(8, 1); else if (V == 4) DW_FWD(4, 1); else if (V == 2) DW_FWD(2, 1); else DW_FWD(1, 1);
@@ -522,3 +574,17 @@ MDA_API int mda_dw_wgrad(const void* x, const void* dy, float* partial, float* g
                      partial, (int)nblk, (int)(KH * KW), (int)C, grad, (int)accumulate);
   MDA_CHECK_LAUNCH();
 }
+
+// Training depthwise conv whose blocks add the BN statistics of the stored
+// output into `region` (the caller follows with mda_bn_apply_fin).
+MDA_API int mda_dw_fwd_bnacc(const void* x, const float* w, void* y, void* region, int64_t N,
+                             int64_t H, int64_t W, int64_t C, int64_t Ho, int64_t Wo, int64_t KH,
+                             int64_t KW, int64_t stride, int64_t pad, hipStream_t st) {
+  if (KH != KS || KW != KS || stride < 1 || stride > 2 || C > SLOT_CMAX || region == nullptr)
+    return (int)hipErrorInvalidValue;
+  DwParams p{(const bf16_t*)x, w, nullptr, nullptr, nullptr, (bf16_t*)y, nullptr, (int)N, (int)H,
+             (int)W, (int)C, (int)Ho, (int)Wo, (int)KH, (int)KW, (int)stride, (int)pad, 0,
+             (BnRegion*)region};
+  return launch_fwd(p, st);
+}
+

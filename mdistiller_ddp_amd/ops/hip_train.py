@@ -834,16 +834,19 @@ class _ConvBNActTrain(torch.autograd.Function):
         return dx, dw, dgamma, dbeta, dres, None, None, None, None, dcb
 
 
-def _bn_train_forward(y, M, C, gamma, beta, bn, residual, act, want_preact):
+def _bn_train_forward(y, M, C, gamma, beta, bn, residual, act, want_preact, reg=None):
+    """``reg``: a region the producer (the depthwise conv) already filled with
+    the batch sums -- then no statistics pass."""
     dev = y.device
     ws = _ws(dev)
     stats = torch.empty(4, C, dtype=torch.float32, device=dev)  # mean, rstd, scale, shift
     res = _cl_bf16(residual) if residual is not None else None
     out = torch.empty_like(y)
     pre = torch.empty_like(y) if want_preact else None
-    if _BN_FUSED[0]:
-        reg = _region(C, dev)
-        _ext.call("mda_bn_stats_acc", y, M, C, reg)
+    if _BN_FUSED[0] or reg is not None:
+        if reg is None:
+            reg = _region(C, dev)
+            _ext.call("mda_bn_stats_acc", y, M, C, reg)
         _ext.call("mda_bn_apply_fin", y, reg, M, C, gamma.detach(), beta.detach(),
                   bn.running_mean, bn.running_var, stats, float(bn.momentum), float(bn.eps),
                   bn.num_batches_tracked, res, out, pre, act)
@@ -886,10 +889,17 @@ def _dw_forward(ctx, x, weight, gamma, beta, residual, stride, pad, act, bn, wan
             packs.register_dw(weight, wp)
     y = torch.empty((N, C, Ho, Wo), dtype=torch.bfloat16, device=x.device,
                     memory_format=torch.channels_last)
-    _ext.call("mda_dw_fwd", x, wp, None, None, None, y, None, N, H, W, C, Ho, Wo, 3, 3, stride,
-              pad, 0)
     M = N * Ho * Wo
-    out, pre, res, stats = _bn_train_forward(y, M, C, gamma, beta, bn, residual, act, want_preact)
+    reg = None
+    if _BN_FUSED[0]:
+        # the depthwise kernel adds the BN batch sums of its output (no stats pass)
+        reg = _region(C, x.device)
+        _ext.call("mda_dw_fwd_bnacc", x, wp, y, reg, N, H, W, C, Ho, Wo, 3, 3, stride, pad)
+    else:
+        _ext.call("mda_dw_fwd", x, wp, None, None, None, y, None, N, H, W, C, Ho, Wo, 3, 3,
+                  stride, pad, 0)
+    out, pre, res, stats = _bn_train_forward(y, M, C, gamma, beta, bn, residual, act, want_preact,
+                                             reg)
     ctx.save_for_backward(x, wp, weight, gamma, beta, y, res, stats)
     ctx.meta = (N, C, H, W, Ho, Wo, stride, pad, act)
     ctx.has_res = residual is not None

@@ -274,6 +274,10 @@ def test_teacher_lookahead_matches_inline_teacher(typ, trainer):
     ref = outs[1][0].norm()
     spread = ((outs[2][0] - outs[1][0]).norm() / ref).item()
     rel = ((outs[0][0] - outs[1][0]).norm() / ref).item()
-    assert rel <= 10 * spread + 1e-5, (rel, spread)
+    # a fully native step is run-to-run deterministic (spread 0): then the
+    # look-ahead must match to 1e-5; with a PyTorch / MIOpen layer in the loss
+    # path (ReviewKD's ABF) it must stay within 3x that layer's own spread
+    assert rel <= 3 * spread + 1e-5, (rel, spread)
     assert abs(outs[0][1]["loss"] - outs[1][1]["loss"]) <= max(
-        1e-4 * abs(outs[1][1]["loss"]), 10 * abs(outs[2][1]["loss"] - outs[1][1]["loss"]))
+        1e-4 * abs(outs[1][1]["loss"]), 3 * abs(outs[2][1]["loss"] - outs[1][1]["loss"]))
+    print(f"lookahead {typ}: rel {rel:.3g} spread {spread:.3g}")

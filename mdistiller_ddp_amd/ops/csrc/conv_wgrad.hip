@@ -511,13 +511,45 @@ wgrad_reduce_kernel(const float* __restrict__ partial, float* __restrict__ grad,
 // reduces of a captured backward: engine/step.py flushes them once the last
 // weight-gradient GEMM is queued).  Layers passed by value; block b belongs to
 // the layer whose [blk0, blk0 + blocks) range holds it.
-constexpr int WGRM_MAX = 16;
+constexpr int WGRM_MAX = 32;
 struct WgrLayer {
   const float* partial;
   float* grad;
   int splits, Cout, Cin, KH, KW, Kp, accumulate, cin_keep, groups, blk0;
   float scale;
+  int dw;  // depthwise layer: partial [splits][KH*KW][Cout] -> grad [Cout][KH*KW]
 };
+
+// Depthwise split sums (csrc/dwconv.hip dw_wgrad_finalize_kernel's reduction,
+// same order: 8 slices x 32 elements, fp64), so a captured backward can defer
+// them into the one multi-layer reduce as well.
+__device__ __forceinline__ void dw_reduce_block(int64_t blk, const float* __restrict__ partial,
+                                                int nblk, int KK, int C, float* __restrict__ grad,
+                                                int accumulate) {
+  __shared__ double dred[8][32];
+  const int64_t V = (int64_t)KK * C;
+  const int e = threadIdx.x & 31, sl = threadIdx.x >> 5;
+  const int64_t i = blk * 32 + e;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  if (i < V) {
+    int b = sl;
+    for (; b + 24 < nblk; b += 32) {
+      s0 += (double)partial[(int64_t)(b + 0) * V + i];
+      s1 += (double)partial[(int64_t)(b + 8) * V + i];
+      s2 += (double)partial[(int64_t)(b + 16) * V + i];
+      s3 += (double)partial[(int64_t)(b + 24) * V + i];
+    }
+    for (; b < nblk; b += 8) s0 += (double)partial[(int64_t)b * V + i];
+  }
+  dred[sl][e] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (sl != 0 || i >= V) return;
+  const double sum = ((dred[0][e] + dred[1][e]) + (dred[2][e] + dred[3][e])) +
+                     ((dred[4][e] + dred[5][e]) + (dred[6][e] + dred[7][e]));
+  const int t = (int)(i / C), c = (int)(i - (int64_t)t * C);
+  float* o = grad + (int64_t)c * KK + t;
+  *o = accumulate ? *o + (float)sum : (float)sum;
+}
 struct WgrTable {
   WgrLayer l[WGRM_MAX];
   int n;
@@ -527,6 +559,11 @@ __global__ void __launch_bounds__(256) wgrad_reduce_multi_kernel(const WgrTable 
   int i = 0;
   while (i + 1 < t.n && (int)blockIdx.x >= t.l[i + 1].blk0) ++i;
   const WgrLayer& L = t.l[i];
+  if (L.dw) {
+    dw_reduce_block(blockIdx.x - L.blk0, L.partial, L.splits, L.KH * L.KW, L.Cout, L.grad,
+                    L.accumulate);
+    return;
+  }
   wgrad_reduce_block(blockIdx.x - L.blk0, L.partial, L.grad, L.splits, L.Cout, L.Cin, L.KH, L.KW,
                      L.Kp, L.scale, L.accumulate, L.cin_keep, L.groups);
 }
@@ -850,8 +887,14 @@ MDA_API int mda_wgrad_reduce_multi(const int64_t* rows, int64_t n, hipStream_t s
       L.KW = (int)r[6]; L.Kp = (int)r[7]; L.accumulate = (int)r[8];
       L.cin_keep = (int)((r[9] <= 0 || r[9] > r[4]) ? r[4] : r[9]);
       L.groups = (int)(r[10] > 1 ? r[10] : 1);
+      L.dw = r[10] == -1;  // groups = -1 marks a depthwise row (Cout = C, KH x KW taps)
       L.scale = 1.f;
       L.blk0 = blk;
+      if (L.dw) {
+        if (L.splits < 1 || L.Cout < 1) return (int)hipErrorInvalidValue;
+        blk += (int)(((int64_t)L.KH * L.KW * L.Cout + 31) / 32);
+        continue;
+      }
       if (L.Cout % 8 || L.Kp % 64 || L.splits < 1) return (int)hipErrorInvalidValue;
       const int cp = wgr_cols(L.splits);
       blk += (int)(((int64_t)L.Cout * L.Kp / 4 + cp - 1) / cp);

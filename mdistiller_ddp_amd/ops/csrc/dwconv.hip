@@ -570,6 +570,7 @@ MDA_API int mda_dw_wgrad(const void* x, const void* dy, float* partial, float* g
     if (V == 8) DW_WG(8, 2); else if (V == 4) DW_WG(4, 2); else if (V == 2) DW_WG(2, 2); else DW_WG(1, 2);
   }
 #undef DW_WG
+  if (grad == nullptr) MDA_CHECK_LAUNCH();  // partials only (a deferred multi-layer reduce sums them)
   hipLaunchKernelGGL(dw_wgrad_finalize_kernel, dim3((unsigned)((KH * KW * C + 31) / 32)), dim3(256), 0, st,
                      partial, (int)nblk, (int)(KH * KW), (int)C, grad, (int)accumulate);
   MDA_CHECK_LAUNCH();

@@ -931,6 +931,14 @@ def _dw_backward(ctx, dout, dpre):
 
         def wg():
             part = torch.empty(nblk * 9 * C, dtype=torch.float32, device=y.device)
+            if direct_w and _WG_DEFER[0] is not None:
+                # partials now, their sum in the backward's one multi-layer reduce
+                _ext.call("mda_dw_wgrad", x, dy, part, None, N, H, W, C, Ho, Wo, 3, 3, stride,
+                          pad, nblk, 1)
+                _WG_DEFER[0].append([part.data_ptr(), target.data_ptr(), nblk, C, 1, 3, 3, 0, 1,
+                                     0, -1])
+                _WG_KEEP.append(part)
+                return
             _ext.call("mda_dw_wgrad", x, dy, part, target, N, H, W, C, Ho, Wo, 3, 3, stride, pad,
                       nblk, 1 if direct_w else 0)
         _wgrad_launch(wg, direct_w, x, dy)

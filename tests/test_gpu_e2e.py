@@ -132,12 +132,17 @@ def test_validation_sees_updated_weights(tmp_path):
     assert abs(v2[0] - v2_ref[0]) <= 3.0, (v2, v2_ref)
 
 
-@pytest.mark.parametrize("trainer", ["base", "dot"])
-def test_native_bf16_graph_matches_eager(trainer):
+@pytest.mark.parametrize("trainer,student", [("base", "resnet8x4"), ("dot", "resnet8x4"),
+                                             ("base", "MobileNetV2"), ("base", "ShuffleV1")])
+def test_native_bf16_graph_matches_eager(trainer, student):
     """20 steps of the NATIVE bf16 path (HIP conv/BN/loss/optimizer kernels):
-    hipGraph replay vs eager launches of the same kernels."""
+    hipGraph replay vs eager launches of the same kernels (the captured step
+    defers every dense and depthwise weight-gradient reduction into one
+    multi-layer launch; MobileNetV2 / ShuffleV1 cover the depthwise, grouped
+    and channel-gather kernels)."""
     torch.manual_seed(0)
     cfg = _cfg("DKD" if trainer == "base" else "KD", trainer)
+    cfg.DISTILLER.STUDENT = student
     d1 = build_distiller(cfg, 100, "cuda")
     d2 = copy.deepcopy(d1)
     outs = []

@@ -34,6 +34,7 @@ CONFIGS = {
     "pkt_cifar_res32x4_res8x4": ("configs/cifar100/pkt.yaml", 64, [], None),
     "sp_cifar_res32x4_res8x4": ("configs/cifar100/sp.yaml", 64, [], None),
     "vid_cifar_res32x4_res8x4": ("configs/cifar100/vid.yaml", 64, [], None),
+    "kdsvd_cifar_res32x4_res8x4": ("configs/cifar100/kdsvd.yaml", 64, [], None),
     "vanilla_cifar_res8x4": ("configs/cifar100/vanilla.yaml", 64,
                              ["DISTILLER.STUDENT", "resnet8x4"], None),
     "dkd_cifar_vgg13_vgg8": ("configs/cifar100/dkd/vgg13_vgg8.yaml", 64, [], None),

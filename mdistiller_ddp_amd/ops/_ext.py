@@ -88,8 +88,8 @@ SIGNATURES = {
     "mda_bn_region_bytes": "ip",
     "mda_bn_stats_acc": "piips",
     "mda_bn_apply_fin": "ppii" + "ppppp" + "ff" + "p" + "ppp" + "i" + "s",
-    "mda_bn_bwd_fused": "ppppp" + "p" + "iii" + "pp" + "pp" + "ppp" + "s",
-    "mda_bn_bwd_apply_reg": "pppp" + "p" + "iii" + "p" + "pp" + "ppp" + "s",
+    "mda_bn_bwd_fused": "ppppp" + "p" + "iii" + "pp" + "pp" + "ppp" + "ppp" + "s",
+    "mda_bn_bwd_apply_reg": "pppp" + "p" + "iii" + "p" + "pp" + "ppp" + "ppp" + "s",
     "mda_conv_fwd_bnacc": "ppppp" + "i" * 14 + "s",
     # CRD memory (csrc/crd.hip)
     "mda_crd_scores": "ppppiiifs",
@@ -98,6 +98,8 @@ SIGNATURES = {
     # classifier head + metrics (csrc/head.hip)
     "mda_pool_fc_fwd": "ipppppiiiis",
     "mda_pool_fc_bwd": "ippppppp" + "iiiii" + "s",
+    "mda_sym_eig": "piiipp" + "s",
+    "mda_pool_fc_bwd_bn": "ippppppp" + "iiiii" + "pppip" + "s",
     "mda_meters_update": "ippii" + "pppp" + "ips",
     # ReviewKD HCL + ABF (csrc/reviewkd.hip)
     "mda_hcl_loss": "piiipfpfps",

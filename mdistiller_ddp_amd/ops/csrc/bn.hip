@@ -764,7 +764,27 @@ struct BwdArgs {
   BnRegion* reg;
   unsigned* err;
   int M, C, act;
+  // optional: the residual came from another training BN with no activation
+  // (a projection shortcut): its dout IS dres, so this pass also adds that
+  // layer's sum dres and sum dres*xhat_r (ry = its BN input, rstats = its
+  // [4][C] stats) into rreg -- its backward is then one streaming pass too
+  const bf16_t* ry; const float* rstats; BnRegion* rreg;
 };
+
+// res-producer sums of one 8-channel vector (dz = the stored dres values)
+__device__ __forceinline__ void rsum_add8(const BwdArgs& a, int64_t o, int c0, const uint32_t (&ro)[4],
+                                          float (&r1)[8], float (&r2)[8]) {
+  const uint4 yv = *(const uint4*)(a.ry + o);
+  const uint32_t yw[4] = {yv.x, yv.y, yv.z, yv.w};
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int w = e >> 1;
+    const float d = (e & 1) ? __uint_as_float(ro[w] & 0xffff0000u) : __uint_as_float(ro[w] << 16);
+    const float yf = (e & 1) ? __uint_as_float(yw[w] & 0xffff0000u) : __uint_as_float(yw[w] << 16);
+    r1[e] += d;
+    r2[e] += d * ((yf - a.rstats[c0 + e]) * a.rstats[a.C + c0 + e]);
+  }
+}
 
 struct Raw8 { uint4 y, d, d2, p, r; };
 
@@ -887,6 +907,7 @@ bn_bwd_fused_kernel(BwdArgs a) {
   float m0[8], m1[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { m0[k] = s_m0[c0 + k]; m1[k] = s_m1[c0 + k]; }
+  float r1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, r2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   auto emit = [&](int m, const float (&dz)[8], const uint4& yv) {
     const int64_t o = (int64_t)m * C + c0;
     const uint32_t yw[4] = {yv.x, yv.y, yv.z, yv.w};
@@ -907,6 +928,7 @@ bn_bwd_fused_kernel(BwdArgs a) {
     }
     *(uint4*)(a.dy + o) = make_uint4(go[0], go[1], go[2], go[3]);
     if (a.dres) *(uint4*)(a.dres + o) = make_uint4(ro[0], ro[1], ro[2], ro[3]);
+    if (a.rreg) rsum_add8(a, o, c0, ro, r1, r2);
   };
   if (HOLD) {
 #pragma unroll
@@ -922,6 +944,10 @@ bn_bwd_fused_kernel(BwdArgs a) {
       bwd_dz8(a, v0, sc, sh, dz);
       emit(m, dz, v0.y);
     }
+  }
+  if (a.rreg) {
+    __syncthreads();  // the phase-1 reduction's shared buffer is reused
+    region_block_add(a.rreg, r1, r2, C, rpi);
   }
 }
 
@@ -1003,6 +1029,7 @@ bn_bwd_apply_reg_kernel(BwdArgs a) {
     }
   }
   __syncthreads();
+  float r1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, r2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   auto emit = [&](int64_t i, const Raw8& v) {
     const int c0 = (int)(i % c8) * 8;
     float sc[8], sh[8], mu[8], rs[8], dz[8];
@@ -1029,6 +1056,7 @@ bn_bwd_apply_reg_kernel(BwdArgs a) {
     }
     *(uint4*)(a.dy + i * 8) = make_uint4(go[0], go[1], go[2], go[3]);
     if (a.dres) *(uint4*)(a.dres + i * 8) = make_uint4(ro[0], ro[1], ro[2], ro[3]);
+    if (a.rreg) rsum_add8(a, i * 8, c0, ro, r1, r2);  // (the host checks: fixed channel group)
   };
 #pragma unroll
   for (int k = 0; k < APPLY_V; ++k) {
@@ -1040,6 +1068,7 @@ bn_bwd_apply_reg_kernel(BwdArgs a) {
     bwd_load8(a, i * 8, v);
     emit(i, v);
   }
+  if (a.rreg) region_block_add(a.rreg, r1, r2, C, 256 / c8);
 }
 
 int g_num_cus = 0;
@@ -1102,11 +1131,16 @@ MDA_API int mda_bn_apply_fin(const void* y, void* region, int64_t M, int64_t C, 
 MDA_API int mda_bn_bwd_fused(const void* dout, const void* dout2, const void* dpre, const void* y,
                              const void* res, const float* stats, int64_t M, int64_t C,
                              int64_t act, void* region, void* err, void* dy, void* dres,
-                             float* dgamma, float* dbeta, float* sums, hipStream_t st) {
+                             float* dgamma, float* dbeta, float* sums, const void* ry,
+                             const float* rstats, void* rregion, hipStream_t st) {
   if (C % 8 || C > SLOT_CMAX || M <= 0 || M >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
+  if (rregion != nullptr && (dres == nullptr || ry == nullptr || rstats == nullptr ||
+                             256 % (C / 8) != 0))
+    return (int)hipErrorInvalidValue;
   BwdArgs a{(const bf16_t*)dout, (const bf16_t*)dout2, (const bf16_t*)dpre, (const bf16_t*)y,
             (const bf16_t*)res, stats, (bf16_t*)dy, (bf16_t*)dres, dgamma, dbeta, sums,
-            (BnRegion*)region, (unsigned*)err, (int)M, (int)C, (int)act};
+            (BnRegion*)region, (unsigned*)err, (int)M, (int)C, (int)act, (const bf16_t*)ry,
+            rstats, (BnRegion*)rregion};
   const int C8 = (int)C / 8;
   const int rpi = 256 / C8;
   const int64_t rows_iter = (M + rpi - 1) / rpi;       // block-iterations of work
@@ -1136,12 +1170,17 @@ MDA_API int mda_bn_bwd_fused(const void* dout, const void* dout2, const void* dp
 MDA_API int mda_bn_bwd_apply_reg(const void* dout, const void* dpre, const void* y, const void* res,
                                  const float* stats, int64_t M, int64_t C, int64_t act,
                                  void* region, void* dy, void* dres, float* dgamma, float* dbeta,
-                                 float* sums, hipStream_t st) {
+                                 float* sums, const void* ry, const float* rstats, void* rregion,
+                                 hipStream_t st) {
   if (C % 8 || C > SLOT_CMAX || M <= 0 || M >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
   BwdArgs a{(const bf16_t*)dout, nullptr, (const bf16_t*)dpre, (const bf16_t*)y,
             (const bf16_t*)res, stats, (bf16_t*)dy, (bf16_t*)dres, dgamma, dbeta, sums,
-            (BnRegion*)region, nullptr, (int)M, (int)C, (int)act};
+            (BnRegion*)region, nullptr, (int)M, (int)C, (int)act, (const bf16_t*)ry, rstats,
+            (BnRegion*)rregion};
   const int nb = apply_blocks(M * C / 8, APPLY_V);
+  if (rregion != nullptr && (dres == nullptr || ry == nullptr || rstats == nullptr ||
+                             256 % (C / 8) != 0))
+    return (int)hipErrorInvalidValue;  // a thread must keep one channel group
   hipLaunchKernelGGL(bn_bwd_apply_reg_kernel, dim3(nb), dim3(256), 0, st, a);
   MDA_CHECK_LAUNCH();
 }

@@ -1,0 +1,126 @@
+// Batched symmetric eigendecomposition of small Gram matrices, for KDSVD
+// (reference distillers/KDSVD.py:8-35 takes torch.svd of each sample's
+// (C*H) x W feature view and uses the right singular vectors V and the
+// singular values).  V and sigma^2 are the eigenvectors / eigenvalues of the
+// W x W Gram G = X^T X, so the SVD reduces to a tiny eigenproblem per sample.
+//
+// rocSOLVER's batched SVD / syevd check their info word on the host, which
+// breaks hipGraph capture; this kernel has no host interaction:
+//
+//   * one workgroup per matrix (n <= 63), the matrix (fp64) and the
+//     accumulated rotations (fp32) live in LDS (< 64 KB); odd n gets a zero row / column (its
+//     rotations are exactly the identity, so it never mixes and is dropped);
+//   * parallel cyclic Jacobi: each step applies n/2 disjoint rotations
+//     (round-robin tournament pairing, n-1 steps per sweep), a fixed number of
+//     sweeps (quadratic convergence: 8 sweeps reach fp64 round-off for n <= 64;
+//     rotations of already-zero pairs are the identity);
+//   * eigenvalues sorted descending (rank by comparison, ties by index),
+//     each eigenvector's sign fixed so its largest-magnitude component is
+//     positive (LAPACK's sign is arbitrary; this one is deterministic).
+//
+// Output: vals [B][n] (descending), vecs [B][n][n] row-major with the
+// eigenvectors as COLUMNS (V[:, j] pairs with vals[j]), fp32.
+#include "common.h"
+
+namespace {
+
+constexpr int EIG_NMAX = 64;
+
+__global__ void __launch_bounds__(256) sym_eig_kernel(const float* __restrict__ g, int n0,
+                                                      int sweeps, float* __restrict__ vals,
+                                                      float* __restrict__ vecs) {
+  __shared__ double A[EIG_NMAX][EIG_NMAX + 1];
+  __shared__ float V[EIG_NMAX][EIG_NMAX + 1];  // rotations accumulated in fp32
+  __shared__ double cs[EIG_NMAX / 2][2];
+  __shared__ int pp[EIG_NMAX / 2], qq[EIG_NMAX / 2];  // this step's pairs
+  __shared__ double lam[EIG_NMAX];
+  __shared__ int order[EIG_NMAX];
+  const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  const float* gb = g + (int64_t)b * n0 * n0;
+  const int n = n0 + (n0 & 1);
+  for (int e = tid; e < n * n; e += nt) {
+    const int i = e / n, j = e % n;
+    // symmetrise (G is symmetric up to the GEMM's rounding)
+    A[i][j] = (i < n0 && j < n0) ? 0.5 * ((double)gb[i * n0 + j] + (double)gb[j * n0 + i]) : 0.0;
+    V[i][j] = i == j ? 1.f : 0.f;
+  }
+  const int m = n - 1, half = n / 2;
+  __syncthreads();
+  for (int sw = 0; sw < sweeps; ++sw) {
+    for (int r = 0; r < m; ++r) {
+      // round-robin pairing: (m, r) and ((r+k) % m, (r-k+m) % m), k = 1..half-1
+      if (tid < half) {
+        int p, q;
+        if (tid == 0) {
+          p = r; q = m;
+        } else {
+          p = (r + tid) % m; q = (r - tid + m) % m;
+        }
+        if (p > q) { const int t = p; p = q; q = t; }
+        const double apq = A[p][q];
+        double c = 1.0, s = 0.0;
+        if (apq != 0.0) {
+          const double theta = (A[q][q] - A[p][p]) / (2.0 * apq);
+          const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+          c = 1.0 / sqrt(t * t + 1.0);
+          s = t * c;
+        }
+        cs[tid][0] = c; cs[tid][1] = s;
+        pp[tid] = p; qq[tid] = q;
+      }
+      __syncthreads();
+      // rows, in place per pair: A <- J^T A
+      for (int e = tid; e < half * n; e += nt) {
+        const int k = e / n, j = e % n, p = pp[k], q = qq[k];
+        const double c = cs[k][0], s = cs[k][1], ap = A[p][j], aq = A[q][j];
+        A[p][j] = c * ap - s * aq;
+        A[q][j] = s * ap + c * aq;
+      }
+      __syncthreads();
+      // columns, in place per pair: A <- A J, V <- V J
+      for (int e = tid; e < half * n; e += nt) {
+        const int k = e / n, i = e % n, p = pp[k], q = qq[k];
+        const double c = cs[k][0], s = cs[k][1], ap = A[i][p], aq = A[i][q];
+        A[i][p] = c * ap - s * aq;
+        A[i][q] = s * ap + c * aq;
+        const float cf = (float)c, sf = (float)s, vp = V[i][p], vq = V[i][q];
+        V[i][p] = cf * vp - sf * vq;
+        V[i][q] = sf * vp + cf * vq;
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = tid; i < n0; i += nt) lam[i] = A[i][i];
+  __syncthreads();
+  for (int i = tid; i < n0; i += nt) {
+    int rank = 0;
+    for (int j = 0; j < n0; ++j) rank += (lam[j] > lam[i]) || (lam[j] == lam[i] && j < i);
+    order[rank] = i;
+  }
+  __syncthreads();
+  float* vb = vecs + (int64_t)b * n0 * n0;
+  for (int jj = tid; jj < n0; jj += nt) {
+    const int j = order[jj];
+    vals[(int64_t)b * n0 + jj] = (float)lam[j];
+    int im = 0;
+    double best = -1.0;
+    for (int i = 0; i < n0; ++i) {
+      const double a = fabsf(V[i][j]);
+      if (a > best) { best = a; im = i; }
+    }
+    const double sg = V[im][j] < 0.0 ? -1.0 : 1.0;
+    for (int i = 0; i < n0; ++i) vb[i * n0 + jj] = (float)(sg * V[i][j]);
+  }
+}
+
+}  // namespace
+
+// g: [B][n][n] fp32 symmetric (n <= 63); vals [B][n], vecs [B][n][n] fp32 (see above).
+MDA_API int mda_sym_eig(const float* g, int64_t B, int64_t n, int64_t sweeps, float* vals,
+                        float* vecs, hipStream_t st) {
+  if (B <= 0 || B > 65535 || n < 2 || n >= EIG_NMAX || sweeps < 1 || sweeps > 64)
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(sym_eig_kernel, dim3((unsigned)B), dim3(256), 0, st, g, (int)n, (int)sweeps,
+                     vals, vecs);
+  return (int)hipGetLastError();
+}

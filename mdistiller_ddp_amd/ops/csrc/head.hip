@@ -15,6 +15,12 @@
 //    single launch (reference: utils.accuracy + per-iteration all-reduces,
 //    engine/utils.py:125-136, trainer.py:277-281).
 #include "common.h"
+#include "bnslot.h"
+
+// optional BN-backward sums of the pooled map's producer (pool_fc_bwd_kernel)
+struct HeadBn {
+  const bf16_t* y; const bf16_t* res; const float* stats; BnRegion* reg; int act;
+};
 
 namespace {
 
@@ -108,7 +114,7 @@ __global__ void __launch_bounds__(256)
 pool_fc_bwd_kernel(const T* __restrict__ dl, const T* __restrict__ dpooled,
                    const T* __restrict__ pooled, const float* __restrict__ W,
                    float* __restrict__ dW, float* __restrict__ db, T* __restrict__ dx, int N,
-                   int HW, int C, int J, float inv_hw, int accum) {
+                   int HW, int C, int J, float inv_hw, int accum, HeadBn bn) {
   extern __shared__ float sh[];
   if ((int)blockIdx.x < J) {
     // ---- dW[j, :] = sum_n dl[n, j] * pooled[n, :];  db[j] = sum_n dl[n, j]
@@ -152,6 +158,28 @@ pool_fc_bwd_kernel(const T* __restrict__ dl, const T* __restrict__ dpooled,
                       (((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7])));
     const float v = acc * inv_hw;
     for (int p = 0; p < HW; ++p) io<T>::st(dxn, (int64_t)p * C + c, v);
+    if (bn.reg != nullptr) {
+      // dx is the whole output gradient of the training BN that produced the
+      // pooled map: its sum dz / sum dz*xhat over this sample's pixels
+      const float d = io<T>::ld(dxn, c);  // the stored (rounded) value
+      const float mu = bn.stats[c], rs = bn.stats[C + c], sc = bn.stats[2 * C + c],
+                  shf = bn.stats[3 * C + c];
+      float s1 = 0.f, s2 = 0.f;
+      const bf16_t* yn = bn.y + (int64_t)n * HW * C;
+      const bf16_t* rn = bn.res ? bn.res + (int64_t)n * HW * C : nullptr;
+      for (int p = 0; p < HW; ++p) {
+        const float yv = bf2f(yn[(int64_t)p * C + c]);
+        float z = yv * sc + shf;
+        if (rn) z += bf2f(rn[(int64_t)p * C + c]);
+        const float g = bn.act == 1 ? (z > 0.f ? d : 0.f)
+                        : bn.act == 2 ? ((z > 0.f && z < 6.f) ? d : 0.f) : d;
+        s1 += g;
+        s2 += g * ((yv - mu) * rs);
+      }
+      const int shard = n % slot_shards(C);
+      acc_add(region_acc(bn.reg, C, shard, 0) + c, (double)s1);
+      acc_add(region_acc(bn.reg, C, shard, 1) + c, (double)s2);
+    }
   }
 }
 
@@ -337,10 +365,32 @@ MDA_API int mda_pool_fc_fwd(int64_t dt, const void* x, const float* W, const flo
 
 // dl [N, J]; dpooled [N, C] or null; pooled [N, C]; W [J, C] fp32; dW [J, C] fp32 or
 // null; db [J] fp32 or null; dx [N, HW, C].  accum: dW/db += instead of =.
+MDA_API int mda_pool_fc_bwd_bn(int64_t dt, const void* dl, const void* dpooled, const void* pooled,
+                               const float* W, float* dW, float* db, void* dx, int64_t N,
+                               int64_t HW, int64_t C, int64_t J, int64_t accum, const void* bn_y,
+                               const void* bn_res, const float* bn_stats, int64_t bn_act,
+                               void* bn_region, hipStream_t st);
+
 MDA_API int mda_pool_fc_bwd(int64_t dt, const void* dl, const void* dpooled, const void* pooled,
                             const float* W, float* dW, float* db, void* dx, int64_t N, int64_t HW,
                             int64_t C, int64_t J, int64_t accum, hipStream_t st) {
+  return mda_pool_fc_bwd_bn(dt, dl, dpooled, pooled, W, dW, db, dx, N, HW, C, J, accum, nullptr,
+                            nullptr, nullptr, 0, nullptr, st);
+}
+
+// mda_pool_fc_bwd that also adds the BN backward sums of the layer whose
+// output was pooled (bn_*: its input, residual, [4][C] stats, activation and a
+// fresh region; bf16 only, small heads only -- the caller checks
+// mda_pool_fc_bwd_bn_ok).
+MDA_API int mda_pool_fc_bwd_bn(int64_t dt, const void* dl, const void* dpooled, const void* pooled,
+                               const float* W, float* dW, float* db, void* dx, int64_t N,
+                               int64_t HW, int64_t C, int64_t J, int64_t accum, const void* bn_y,
+                               const void* bn_res, const float* bn_stats, int64_t bn_act,
+                               void* bn_region, hipStream_t st) {
   if (N <= 0 || C <= 0 || J <= 0 || N > 16384 || J > 16384) return (int)hipErrorInvalidValue;
+  HeadBn bn{(const bf16_t*)bn_y, (const bf16_t*)bn_res, bn_stats, (BnRegion*)bn_region, (int)bn_act};
+  if (bn_region != nullptr && (dt == DT_F32 || (int64_t)J * C > (1 << 16) || C > SLOT_CMAX))
+    return (int)hipErrorInvalidValue;
   if ((int64_t)J * C > (1 << 16)) {  // large head: tiled GEMM blocks
     const int ct = (int)((C + HB_TC - 1) / HB_TC);
     const int nW = (int)((J + HB_TJ - 1) / HB_TJ) * ct;
@@ -361,11 +411,11 @@ MDA_API int mda_pool_fc_bwd(int64_t dt, const void* dl, const void* dpooled, con
   if (dt == DT_F32)
     hipLaunchKernelGGL(pool_fc_bwd_kernel<float>, grid, dim3(256), lds, st, (const float*)dl,
                        (const float*)dpooled, (const float*)pooled, W, dW, db, (float*)dx, (int)N,
-                       (int)HW, (int)C, (int)J, 1.f / HW, (int)accum);
+                       (int)HW, (int)C, (int)J, 1.f / HW, (int)accum, bn);
   else
     hipLaunchKernelGGL(pool_fc_bwd_kernel<bf16_t>, grid, dim3(256), lds, st, (const bf16_t*)dl,
                        (const bf16_t*)dpooled, (const bf16_t*)pooled, W, dW, db, (bf16_t*)dx,
-                       (int)N, (int)HW, (int)C, (int)J, 1.f / HW, (int)accum);
+                       (int)N, (int)HW, (int)C, (int)J, 1.f / HW, (int)accum, bn);
   MDA_CHECK_LAUNCH();
 }
 

@@ -388,6 +388,74 @@ def _svd(feat, n=1):
     return u, s, v
 
 
+class _GramEig(torch.autograd.Function):
+    """Eigenvalues (descending) and eigenvectors (columns; largest-magnitude
+    component positive) of G = X^T X for a batch X [B, R, W], W <= 63: the
+    squared singular values and right singular vectors of X.
+
+    GPU: the Gram on rocBLAS, the eigensolver on the native Jacobi kernel
+    (csrc/eig.hip) -- nothing synchronises with the host, so KDSVD captures
+    into the step graph.  CPU: torch.linalg.eigh with the same order and sign
+    convention.  Backward (either way): with K = F o (V^T dV),
+    F_ij = 1 / (lam_j - lam_i) off the diagonal, dG = V (K + diag(dlam)) V^T
+    and dX = X (dG + dG^T) -- the SVD's V / sigma^2 gradient for distinct
+    singular values."""
+
+    @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
+    def forward(ctx, x):
+        B, R, W = x.shape
+        g = torch.bmm(x.transpose(1, 2), x).contiguous()
+        if x.is_cuda:
+            lam = torch.empty(B, W, dtype=torch.float32, device=x.device)
+            vec = torch.empty(B, W, W, dtype=torch.float32, device=x.device)
+            _ext.call("mda_sym_eig", g, B, W, 8, lam, vec)
+        else:
+            lam, vec = torch.linalg.eigh(g.double())
+            lam, vec = lam.flip(-1), vec.flip(-1)
+            idx = vec.abs().argmax(dim=1, keepdim=True)
+            vec = vec * torch.where(vec.gather(1, idx) < 0, -1.0, 1.0)
+            lam, vec = lam.to(x.dtype), vec.to(x.dtype)
+        ctx.save_for_backward(x, lam, vec)
+        return lam, vec
+
+    @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
+    def backward(ctx, dlam, dvec):
+        x, lam, v = ctx.saved_tensors
+        k = torch.zeros_like(v)
+        if dvec is not None:
+            diff = lam.unsqueeze(1) - lam.unsqueeze(2)  # [i, j] = lam_j - lam_i
+            f = torch.where(diff != 0, 1.0 / diff, torch.zeros_like(diff))
+            f.diagonal(dim1=1, dim2=2).zero_()
+            k = f * torch.bmm(v.transpose(1, 2), dvec)
+        if dlam is not None:
+            k = k + torch.diag_embed(dlam)
+        dg = torch.bmm(torch.bmm(v, k), v.transpose(1, 2))
+        return torch.bmm(x, dg + dg.transpose(1, 2))
+
+
+def _svd_native_ok(feat) -> bool:
+    N, C, H, W = feat.shape
+    if not (2 <= W <= 63 and C * H >= W and N <= 65535):
+        return False
+    return not feat.is_cuda or _ext.available()
+
+
+def _svd_gram(feat, n=1):
+    """``_svd`` through the Gram eigendecomposition (no U: KDSVD never uses
+    it); same normalisation of the leading n singular values / vectors."""
+    N, C, H, W = feat.shape
+    x = feat.float().contiguous().reshape(N, C * H, W)
+    lam, v = _GramEig.apply(x)
+    s = lam.clamp_min(0).sqrt()
+    s, v = _removenan(s), _removenan(v)
+    if n > 0:
+        s = F.normalize(s[:, :n], dim=1)
+        v = F.normalize(v[:, :, :n], dim=1)
+    return None, s, v
+
+
 def _align_rsv(a, b):
     cosine = torch.matmul(a.transpose(-2, -1), b)
     max_abs, _ = torch.max(torch.abs(cosine), 1, keepdim=True)
@@ -396,13 +464,27 @@ def _align_rsv(a, b):
     return torch.matmul(a, mask), b
 
 
-def kdsvd_loss(g_s, g_t, k):
-    """`distillers/KDSVD.py:8-35` (batched SVD via rocSOLVER through torch)."""
+def kdsvd_native_ok(g_s, g_t) -> bool:
+    """Every stage's SVD runs on the Gram eigensolver (graph-capturable)."""
+    return all(_svd_native_ok(f) for f in list(g_s) + list(g_t))
+
+
+def kdsvd_loss(g_s, g_t, k, native: bool | None = None):
+    """`distillers/KDSVD.py:8-35`.  ``native`` (default: whenever the shapes
+    allow): the SVDs through the Gram eigendecomposition (:class:`_GramEig`);
+    else torch.linalg.svd (rocSOLVER, host-synchronising).  Singular vectors
+    are defined up to sign; the native path's convention (largest component
+    positive) differs from LAPACK's arbitrary one, so the teacher-side signs
+    -- and with them the inter-stage RBF terms -- can differ from the
+    reference (parity is pinned on sign-invariant quantities)."""
+    if native is None:
+        native = kdsvd_native_ok(g_s, g_t)
+    svd = _svd_gram if native else _svd
     v_sb = v_tb = None
     losses = []
     for i, (f_s, f_t) in enumerate(zip(g_s, g_t)):
-        _, s_t, v_t = _svd(f_t.detach(), k)
-        _, _, v_s = _svd(f_s, k + 3)
+        _, s_t, v_t = svd(f_t.detach(), k)
+        _, _, v_s = svd(f_s, k + 3)
         v_s, v_t = _align_rsv(v_s, v_t)
         s_t = s_t.unsqueeze(1)
         v_t = v_t * s_t

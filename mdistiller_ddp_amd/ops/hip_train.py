@@ -301,7 +301,8 @@ def bn_dgrad_sums_count(reset: bool = False):
     return v
 
 
-def _bn_bwd(dout, dpre, y, res, stats, gamma, beta, M, C, act, need_res, direct_gb, link=None):
+def _bn_bwd(dout, dpre, y, res, stats, gamma, beta, M, C, act, need_res, direct_gb, link=None,
+            res_link=None):
     """BN (+ residual) (+ activation) backward -> (dy, dres or None, sums or
     None).  Fused: ONE grid-barrier launch (mda_bn_bwd_fused); else the
     partial-rows reduce + finalize + apply (3 launches).  dgamma / dbeta are
@@ -314,15 +315,24 @@ def _bn_bwd(dout, dpre, y, res, stats, gamma, beta, M, C, act, need_res, direct_
     dy = torch.empty_like(y)
     dres = torch.empty_like(y) if need_res else None
     reg = link.take(dout) if link is not None else None
+    # the residual's producer is a training BN without activation (a projection
+    # shortcut): dres IS its output gradient, so this pass adds its sums too
+    rl = res_link if (need_res and res_link is not None and 256 % (C // 8) == 0) else None
+    rreg = _region(C, dev) if rl is not None else None
+    ry, rst = (rl.y, rl.stats) if rl is not None else (None, None)
     if reg is not None and dpre is None:
         sums = None if direct_gb else torch.empty(2, C, dtype=torch.float32, device=dev)
         _ext.call("mda_bn_bwd_apply_reg", dout, None, y, res, stats, M, C, act, reg, dy, dres,
-                  dg, db, sums)
+                  dg, db, sums, ry, rst, rreg)
+        if rl is not None:
+            rl.arm(dres, rreg)
         return dy, dres, sums
     if _BN_FUSED[0]:
         sums = None if direct_gb else torch.empty(2, C, dtype=torch.float32, device=dev)
         _ext.call("mda_bn_bwd_fused", dout, None, dpre, y, res, stats, M, C, act, _region(C, dev),
-                  _err_word(dev), dy, dres, dg, db, sums)
+                  _err_word(dev), dy, dres, dg, db, sums, ry, rst, rreg)
+        if rl is not None:
+            rl.arm(dres, rreg)
         return dy, dres, sums
     sums = torch.empty(2, C, dtype=torch.float32, device=dev)
     _bn_bwd_reduce(dout, dpre, y, res, stats, M, C, act, ws, sums, dg, db)
@@ -747,6 +757,11 @@ class _ConvBNActTrain(torch.autograd.Function):
         ctx.has_res = residual is not None
         ctx.link_in = link_in if (link_in is not None and link_in.C == Cin
                                   and link_in.M == N * H * W) else None
+        # the residual's producer (a projection shortcut's BN: no activation, no
+        # residual of its own, not forked): its backward sums come from ours
+        rl = getattr(residual, "_mda_bnlink", None) if residual is not None else None
+        ctx.res_link = rl if (rl is not None and _BNB_ON[0] and rl.act == 0 and rl.res is None
+                              and rl.C == Cout and rl.M == M and forks[1] is None) else None
         # this layer's output, for its consumer's dgrad (no pre-activation
         # output: its gradient would join dz after the consumer's epilogue)
         ctx.bnlink = None
@@ -775,7 +790,7 @@ class _ConvBNActTrain(torch.autograd.Function):
         direct_gb = gamma.grad is not None and beta.grad is not None
         need_res = ctx.has_res and ctx.needs_input_grad[4]
         dy, dres, sums = _bn_bwd(dout, dpre, y, res, stats, gamma, beta, M, Cout, act, need_res,
-                                 direct_gb, ctx.bnlink)
+                                 direct_gb, ctx.bnlink, getattr(ctx, "res_link", None))
         x_fork, res_fork = ctx.forks
         if need_res:
             dres = _fork_sum(res_fork, dres)

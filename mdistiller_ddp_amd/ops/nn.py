@@ -204,6 +204,13 @@ class _PoolFC(torch.autograd.Function):
         _ext.call("mda_pool_fc_fwd", dt, xc, w, b, pooled, logits, N, H * W, C, J)
         ctx.save_for_backward(pooled, weight, bias)
         ctx.meta = (N, C, H, W, J, dt, bias is not None)
+        # x is a training BN's output (hip_train.BnLink): the backward's dx is
+        # that layer's whole output gradient, so the head kernel also adds its
+        # backward sums (small bf16 heads only; see csrc/head.hip)
+        from .hip_train import _BNB_ON
+        link = getattr(x, "_mda_bnlink", None) if _BNB_ON[0] else None
+        ctx.link = link if (link is not None and dt == 1 and J * C <= (1 << 16) and C <= 2048
+                            and link.C == C and link.M == N * H * W) else None
         return pooled, logits
 
     @staticmethod
@@ -225,8 +232,16 @@ class _PoolFC(torch.autograd.Function):
         dw = weight.grad if direct_w else (torch.zeros_like(weight) if need_w else None)
         db = bias.grad if direct_b else (torch.zeros_like(bias) if need_b else None)
         dx = torch.empty((N, C, H, W), dtype=dtype, device=dev, memory_format=torch.channels_last)
-        _ext.call("mda_pool_fc_bwd", dt, dlogits, dpooled, pooled, weight.detach(), dw, db, dx, N,
-                  H * W, C, J, 1)
+        link = ctx.link
+        if link is not None:
+            from .hip_train import _region
+            reg = _region(C, dev)
+            _ext.call("mda_pool_fc_bwd_bn", dt, dlogits, dpooled, pooled, weight.detach(), dw, db,
+                      dx, N, H * W, C, J, 1, link.y, link.res, link.stats, link.act, reg)
+            link.arm(dx, reg)
+        else:
+            _ext.call("mda_pool_fc_bwd", dt, dlogits, dpooled, pooled, weight.detach(), dw, db, dx,
+                      N, H * W, C, J, 1)
         if direct_w or direct_b:
             from ..parallel.grad_reducer import notify_grad
             notify_grad(*([weight] if direct_w else []), *([bias] if direct_b else []))

@@ -202,3 +202,79 @@ def test_depthwise_to_pointwise(C, H, stride):
         for p, q in zip(list(m[0].parameters()) + list(m[1].parameters()),
                         list(mo[0].parameters()) + list(mo[1].parameters())):
             assert _rel(p.grad, q.grad) < 1e-2
+
+
+@pytest.mark.parametrize("inplanes,planes", [(64, 128), (128, 256)])
+def test_projection_shortcut_bn_sums_from_bn2(inplanes, planes):
+    """A BasicBlock with a projection shortcut: bn2's backward also adds the
+    shortcut BN's sums (its output gradient is bn2's dres), so the shortcut
+    BN runs the streaming backward -- vs the same block with the links off."""
+    from mdistiller_ddp_amd.models.cifar.resnet import BasicBlock
+    from mdistiller_ddp_amd.ops.backend import use_backend
+    torch.manual_seed(6)
+    ds = nn.Sequential(nn.Conv2d(inplanes, planes, 1, 2, bias=False), nn.BatchNorm2d(planes))
+    blk = BasicBlock(inplanes, planes, 2, ds).cuda().to(memory_format=torch.channels_last)
+    off = copy.deepcopy(blk)
+    # M = 128*16*16: conv2's dgrad runs unsplit, so bn1 also takes its link
+    x = torch.randn(128, inplanes, 32, 32, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    g = torch.randn(128, planes, 16, 16, device="cuda").to(torch.bfloat16)
+
+    def run(m):
+        xx = x.clone().requires_grad_(True)
+        with use_backend("hip"), torch.autocast("cuda", dtype=torch.bfloat16):
+            out, _ = m(xx)
+        out.backward(g)
+        torch.cuda.synchronize()
+        return out, xx.grad
+
+    hip_train.bn_dgrad_sums_count(reset=True)
+    out, dx = run(blk)
+    hits, misses = hip_train.bn_dgrad_sums_count(reset=True)
+    assert hits >= 2 and misses == 0, (hits, misses)  # bn1 (from conv2's dgrad) + shortcut BN
+    hip_train.set_bn_dgrad_sums(False)
+    try:
+        out_off, dx_off = run(off)
+    finally:
+        hip_train.set_bn_dgrad_sums(True)
+    assert _rel(out, out_off) < 1e-6
+    assert _rel(dx, dx_off) < 2e-2
+    for (n, p), (_, q) in zip(blk.named_parameters(), off.named_parameters()):
+        assert _rel(p.grad, q.grad) < 2e-2, n
+
+
+@pytest.mark.parametrize("act", ["relu", "none"])
+def test_head_bn_sums_from_pool_fc(act):
+    """The last BN's output feeds the fused pool + FC head: the head's backward
+    adds that BN's sums, so it runs the streaming backward -- vs links off."""
+    from mdistiller_ddp_amd.ops.backend import use_backend
+    from mdistiller_ddp_amd.ops.nn import conv_bn_act, pool_linear
+    torch.manual_seed(7)
+    conv = nn.Conv2d(64, 256, 3, 1, 1, bias=False).cuda()
+    bn = nn.BatchNorm2d(256).cuda()
+    fc = nn.Linear(256, 100).cuda()
+    mods = nn.ModuleList([conv, bn, fc])
+    off = copy.deepcopy(mods)
+    x = torch.randn(128, 64, 8, 8, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    g = torch.randn(128, 100, device="cuda")
+
+    def run(m):
+        xx = x.clone().requires_grad_(True)
+        with use_backend("hip"), torch.autocast("cuda", dtype=torch.bfloat16):
+            h, _ = conv_bn_act(xx, m[0], m[1], act)
+            _, logits = pool_linear(h, m[2])
+        logits.float().backward(g)
+        torch.cuda.synchronize()
+        return logits, xx.grad
+
+    hip_train.bn_dgrad_sums_count(reset=True)
+    out, dx = run(mods)
+    assert hip_train.bn_dgrad_sums_count(reset=True) == (1, 0)
+    hip_train.set_bn_dgrad_sums(False)
+    try:
+        out_off, dx_off = run(off)
+    finally:
+        hip_train.set_bn_dgrad_sums(True)
+    assert _rel(out, out_off) < 1e-6
+    assert _rel(dx, dx_off) < 2e-2
+    for (n, p), (_, q) in zip(mods.named_parameters(), off.named_parameters()):
+        assert _rel(p.grad, q.grad) < 2e-2, n

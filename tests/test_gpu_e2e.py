@@ -35,7 +35,7 @@ def test_distiller_graph_steps(typ):
     d = build_distiller(cfg, 100, "cuda", num_data=2000)
     d.train()
     keys = ("image", "target", "index", "contrastive_index") if typ == "CRD" else ("image", "target")
-    st = TrainStep(d, cfg, "cuda", trainer=cfg.SOLVER.TRAINER, use_graph=typ != "KDSVD",
+    st = TrainStep(d, cfg, "cuda", trainer=cfg.SOLVER.TRAINER, use_graph=True,
                    dtype=torch.bfloat16, batch_keys=keys)
     st.set_epoch(1.0)
     ld = SyntheticLoader("cifar100", 32, "cuda", steps_per_epoch=8, crd_k=cfg.CRD.NCE.K,

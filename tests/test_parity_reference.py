@@ -130,7 +130,29 @@ def test_kdsvd_loss():
     fs = [torch.randn(4, 8, 8, 8), torch.randn(4, 16, 4, 4)]
     ft = [torch.randn(4, 8, 8, 8), torch.randn(4, 16, 4, 4)]
     lr = ref.kdsvd_loss(fs, ft, 1)
-    ln = FL.kdsvd_loss(fs, ft, 1)
+    # the rocSOLVER/LAPACK path: same SVD, same signs as the reference
+    ln = FL.kdsvd_loss(fs, ft, 1, native=False)
+    torch.testing.assert_close(ln, lr, atol=1e-4, rtol=1e-3)
+
+
+def test_kdsvd_loss_gram_path_with_reference_signs(monkeypatch):
+    """The Gram-eigensolver path vs the reference once the reference's SVD
+    signs follow the same convention (singular vectors are sign-ambiguous;
+    LAPACK's choice is arbitrary)."""
+    ref = R.load("distillers", "KDSVD")
+    torch.manual_seed(8)
+    fs = [torch.randn(4, 8, 8, 8), torch.randn(4, 16, 4, 4)]
+    ft = [torch.randn(4, 8, 8, 8), torch.randn(4, 16, 4, 4)]
+    ref_svd = ref.svd
+
+    def svd_fixed(feat, n=1):
+        u, s_, v = ref_svd(feat, n)
+        idx = v.abs().argmax(dim=1, keepdim=True)
+        return u, s_, v * torch.where(v.gather(1, idx) < 0, -1.0, 1.0)
+
+    monkeypatch.setattr(ref, "svd", svd_fixed)
+    lr = ref.kdsvd_loss(fs, ft, 1)
+    ln = FL.kdsvd_loss(fs, ft, 1, native=True)
     torch.testing.assert_close(ln, lr, atol=1e-4, rtol=1e-3)
 
 

@@ -12,8 +12,8 @@
 //     rotations are exactly the identity, so it never mixes and is dropped);
 //   * parallel cyclic Jacobi: each step applies n/2 disjoint rotations
 //     (round-robin tournament pairing, n-1 steps per sweep), a fixed number of
-//     sweeps (quadratic convergence: 8 sweeps reach fp64 round-off for n <= 64;
-//     rotations of already-zero pairs are the identity);
+//     sweeps at most (quadratic convergence: 8 sweeps reach fp64 round-off for
+//     n <= 64), stopping early once the off-diagonal mass is negligible;
 //   * eigenvalues sorted descending (rank by comparison, ties by index),
 //     each eigenvector's sign fixed so its largest-magnitude component is
 //     positive (LAPACK's sign is arbitrary; this one is deterministic).
@@ -35,6 +35,7 @@ __global__ void __launch_bounds__(256) sym_eig_kernel(const float* __restrict__ 
   __shared__ int pp[EIG_NMAX / 2], qq[EIG_NMAX / 2];  // this step's pairs
   __shared__ double lam[EIG_NMAX];
   __shared__ int order[EIG_NMAX];
+  __shared__ double red[2][8];
   const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
   const float* gb = g + (int64_t)b * n0 * n0;
   const int n = n0 + (n0 & 1);
@@ -47,6 +48,27 @@ __global__ void __launch_bounds__(256) sym_eig_kernel(const float* __restrict__ 
   const int m = n - 1, half = n / 2;
   __syncthreads();
   for (int sw = 0; sw < sweeps; ++sw) {
+    // converged (off-diagonal mass below 1e-22 of the total): every further
+    // rotation would be the identity to fp32 output precision
+    {
+      double off = 0.0, tot = 0.0;
+      for (int e = tid; e < n * n; e += nt) {
+        const int i = e / n, j = e % n;
+        const double a2 = A[i][j] * A[i][j];
+        tot += a2;
+        off += i == j ? 0.0 : a2;
+      }
+      for (int o = 32; o > 0; o >>= 1) {
+        off += __shfl_xor(off, o);
+        tot += __shfl_xor(tot, o);
+      }
+      if ((tid & 63) == 0) { red[0][tid >> 6] = off; red[1][tid >> 6] = tot; }
+      __syncthreads();
+      off = tot = 0.0;
+      for (int w = 0; w < (nt >> 6); ++w) { off += red[0][w]; tot += red[1][w]; }
+      __syncthreads();
+      if (off <= 1e-22 * tot) break;  // uniform across the block
+    }
     for (int r = 0; r < m; ++r) {
       // round-robin pairing: (m, r) and ((r+k) % m, (r-k+m) % m), k = 1..half-1
       if (tid < half) {

@@ -388,10 +388,28 @@ def _svd(feat, n=1):
     return u, s, v
 
 
+def _sym_eig(g):
+    """(descending eigenvalues, eigenvector columns with their largest-magnitude
+    component positive) of a batch of symmetric matrices; no autograd."""
+    B, W, _ = g.shape
+    if g.is_cuda:
+        lam = torch.empty(B, W, dtype=torch.float32, device=g.device)
+        vec = torch.empty(B, W, W, dtype=torch.float32, device=g.device)
+        _ext.call("mda_sym_eig", g.float().contiguous(), B, W, 8, lam, vec)
+        return lam, vec
+    lam, vec = torch.linalg.eigh(g.double())
+    lam, vec = lam.flip(-1), vec.flip(-1)
+    idx = vec.abs().argmax(dim=1, keepdim=True)
+    vec = vec * torch.where(vec.gather(1, idx) < 0, -1.0, 1.0)
+    return lam.to(g.dtype), vec.to(g.dtype)
+
+
 class _GramEig(torch.autograd.Function):
     """Eigenvalues (descending) and eigenvectors (columns; largest-magnitude
     component positive) of G = X^T X for a batch X [B, R, W], W <= 63: the
-    squared singular values and right singular vectors of X.
+    squared singular values and right singular vectors of X.  ``x_other``
+    (optional, [B', R', W], no gradient): another batch whose Grams are
+    diagonalised in the same launch (KDSVD's teacher stage), returned second.
 
     GPU: the Gram on rocBLAS, the eigensolver on the native Jacobi kernel
     (csrc/eig.hip) -- nothing synchronises with the host, so KDSVD captures
@@ -403,25 +421,23 @@ class _GramEig(torch.autograd.Function):
 
     @staticmethod
     @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
-    def forward(ctx, x):
-        B, R, W = x.shape
-        g = torch.bmm(x.transpose(1, 2), x).contiguous()
-        if x.is_cuda:
-            lam = torch.empty(B, W, dtype=torch.float32, device=x.device)
-            vec = torch.empty(B, W, W, dtype=torch.float32, device=x.device)
-            _ext.call("mda_sym_eig", g, B, W, 8, lam, vec)
-        else:
-            lam, vec = torch.linalg.eigh(g.double())
-            lam, vec = lam.flip(-1), vec.flip(-1)
-            idx = vec.abs().argmax(dim=1, keepdim=True)
-            vec = vec * torch.where(vec.gather(1, idx) < 0, -1.0, 1.0)
-            lam, vec = lam.to(x.dtype), vec.to(x.dtype)
-        ctx.save_for_backward(x, lam, vec)
-        return lam, vec
+    def forward(ctx, x, x_other=None):
+        B = x.shape[0]
+        g = torch.bmm(x.transpose(1, 2), x)
+        if x_other is not None:
+            g = torch.cat([g, torch.bmm(x_other.transpose(1, 2), x_other)])
+        lam, vec = _sym_eig(g.contiguous())
+        lam_s, vec_s = lam[:B], vec[:B]
+        ctx.save_for_backward(x, lam_s, vec_s)
+        if x_other is None:
+            return lam_s, vec_s
+        lam_o, vec_o = lam[B:], vec[B:]
+        ctx.mark_non_differentiable(lam_o, vec_o)
+        return lam_s, vec_s, lam_o, vec_o
 
     @staticmethod
     @torch.amp.custom_bwd(device_type="cuda")
-    def backward(ctx, dlam, dvec):
+    def backward(ctx, dlam, dvec, *unused):
         x, lam, v = ctx.saved_tensors
         k = torch.zeros_like(v)
         if dvec is not None:
@@ -432,7 +448,7 @@ class _GramEig(torch.autograd.Function):
         if dlam is not None:
             k = k + torch.diag_embed(dlam)
         dg = torch.bmm(torch.bmm(v, k), v.transpose(1, 2))
-        return torch.bmm(x, dg + dg.transpose(1, 2))
+        return torch.bmm(x, dg + dg.transpose(1, 2)), None
 
 
 def _svd_native_ok(feat) -> bool:
@@ -448,6 +464,10 @@ def _svd_gram(feat, n=1):
     N, C, H, W = feat.shape
     x = feat.float().contiguous().reshape(N, C * H, W)
     lam, v = _GramEig.apply(x)
+    return _svd_post(lam, v, n)
+
+
+def _svd_post(lam, v, n):
     s = lam.clamp_min(0).sqrt()
     s, v = _removenan(s), _removenan(v)
     if n > 0:
@@ -479,12 +499,22 @@ def kdsvd_loss(g_s, g_t, k, native: bool | None = None):
     reference (parity is pinned on sign-invariant quantities)."""
     if native is None:
         native = kdsvd_native_ok(g_s, g_t)
-    svd = _svd_gram if native else _svd
     v_sb = v_tb = None
     losses = []
     for i, (f_s, f_t) in enumerate(zip(g_s, g_t)):
-        _, s_t, v_t = svd(f_t.detach(), k)
-        _, _, v_s = svd(f_s, k + 3)
+        if native and f_s.shape[-1] == f_t.shape[-1]:
+            # student and teacher Grams diagonalised in one launch
+            N, C, H, W = f_t.shape
+            xt = f_t.detach().float().contiguous().reshape(N, C * H, W)
+            N, C, H, W = f_s.shape
+            xs = f_s.float().contiguous().reshape(N, C * H, W)
+            lam_s, vec_s, lam_t, vec_t = _GramEig.apply(xs, xt)
+            _, s_t, v_t = _svd_post(lam_t, vec_t, k)
+            _, _, v_s = _svd_post(lam_s, vec_s, k + 3)
+        else:
+            svd = _svd_gram if native else _svd
+            _, s_t, v_t = svd(f_t.detach(), k)
+            _, _, v_s = svd(f_s, k + 3)
         v_s, v_t = _align_rsv(v_s, v_t)
         s_t = s_t.unsqueeze(1)
         v_t = v_t * s_t

@@ -112,8 +112,13 @@ def main():
         n = r["n_gpus"]
         if n != args.gpus:
             raise SystemExit(f"bench.py: measured on {n} ranks, asked for {args.gpus}")
+        # the BASELINE metric / model names only for the flagship config; any
+        # other --cfg is labelled by its file and has no baseline ratio
+        flagship = os.path.realpath(args.cfg) == os.path.realpath(CFG_FILE)
+        cfg_name = os.path.relpath(args.cfg, HERE)
         out = {
-            "metric": "images/sec (whole node) DKD ResNet32x4->ResNet8x4 CIFAR-100",
+            "metric": ("images/sec (whole node) DKD ResNet32x4->ResNet8x4 CIFAR-100" if flagship
+                       else f"images/sec (whole node) {cfg_name}"),
             "value": round(r["images_per_s"], 1),
             "unit": "images/s",
             "n_gpus": n,
@@ -122,11 +127,11 @@ def main():
             "ms_per_step": round(r["ms_per_step"], 4),
             "higher_is_better": True,
             "scaling": args.scaling,
-            "vs_baseline": round(r["images_per_s"] / BASELINE_IMG_S, 3),
+            "vs_baseline": round(r["images_per_s"] / BASELINE_IMG_S, 3) if flagship else None,
             "dtype": r["dtype"],
             "data": "synthetic (CIFAR-100 shape 3x32x32, 100 classes, device-resident), random-init weights (random teacher classifier rescaled to logit std 4)",
             "config": {
-                "model": "DKD resnet32x4->resnet8x4",
+                "model": "DKD resnet32x4->resnet8x4" if flagship else cfg_name,
                 "global_batch": r["global_batch"],
                 "per_gpu_batch": per_gpu,
                 "seq_len": None,

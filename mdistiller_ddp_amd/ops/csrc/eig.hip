@@ -20,6 +20,8 @@
 //
 // Output: vals [B][n] (descending), vecs [B][n][n] row-major with the
 // eigenvectors as COLUMNS (V[:, j] pairs with vals[j]), fp32.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -142,7 +144,14 @@ MDA_API int mda_sym_eig(const float* g, int64_t B, int64_t n, int64_t sweeps, fl
                         float* vecs, hipStream_t st) {
   if (B <= 0 || B > 65535 || n < 2 || n >= EIG_NMAX || sweeps < 1 || sweeps > 64)
     return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(sym_eig_kernel, dim3((unsigned)B), dim3(256), 0, st, g, (int)n, (int)sweeps,
+  // block size (64 / 128 / 256; MDA_EIG_THREADS): the Jacobi steps are
+  // latency bound, fewer waves make each step's barriers cheaper
+  static const int threads = [] {
+    const char* e = getenv("MDA_EIG_THREADS");
+    const int t = e ? atoi(e) : 256;
+    return (t == 64 || t == 128) ? t : 256;
+  }();
+  hipLaunchKernelGGL(sym_eig_kernel, dim3((unsigned)B), dim3(threads), 0, st, g, (int)n, (int)sweeps,
                      vals, vecs);
   return (int)hipGetLastError();
 }

@@ -467,12 +467,17 @@ def _svd_gram(feat, n=1):
     return _svd_post(lam, v, n)
 
 
-def _svd_post(lam, v, n):
+def _svd_post(lam, v, n, exact=False):
+    """``exact``: v came from the eigensolver, finite with unit columns -- the
+    reference's NaN scrub and column normalisation of V are then identities
+    (and so is normalize's backward: it only removes dV's component along
+    each v_j, which the eigenvector gradient ignores), so they are skipped."""
     s = lam.clamp_min(0).sqrt()
-    s, v = _removenan(s), _removenan(v)
+    if not exact:
+        s, v = _removenan(s), _removenan(v)
     if n > 0:
         s = F.normalize(s[:, :n], dim=1)
-        v = F.normalize(v[:, :, :n], dim=1)
+        v = v[:, :, :n] if exact else F.normalize(v[:, :, :n], dim=1)
     return None, s, v
 
 
@@ -509,8 +514,8 @@ def kdsvd_loss(g_s, g_t, k, native: bool | None = None):
             N, C, H, W = f_s.shape
             xs = f_s.float().contiguous().reshape(N, C * H, W)
             lam_s, vec_s, lam_t, vec_t = _GramEig.apply(xs, xt)
-            _, s_t, v_t = _svd_post(lam_t, vec_t, k)
-            _, _, v_s = _svd_post(lam_s, vec_s, k + 3)
+            _, s_t, v_t = _svd_post(lam_t, vec_t, k, exact=True)
+            _, _, v_s = _svd_post(lam_s, vec_s, k + 3, exact=True)
         else:
             svd = _svd_gram if native else _svd
             _, s_t, v_t = svd(f_t.detach(), k)

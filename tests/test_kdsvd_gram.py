@@ -66,7 +66,15 @@ def test_kdsvd_loss_native_matches_svd_path_with_same_signs(monkeypatch):
         u, s, v = ref_svd(feat, n)
         return u, s, _fix_signs(v)
 
+    g_s2 = [t.clone().requires_grad_(True) for t in g_s]
+    g_s = [t.requires_grad_(True) for t in g_s]
     ln = FL.kdsvd_loss(g_s, g_t, 1, native=True)
     monkeypatch.setattr(FL, "_svd", svd_fixed)
-    lr = FL.kdsvd_loss(g_s, g_t, 1, native=False)
+    lr = FL.kdsvd_loss(g_s2, g_t, 1, native=False)
     torch.testing.assert_close(ln, lr, atol=1e-4, rtol=1e-4)
+    # gradients too (the native path skips V's normalisation: an identity
+    # whose backward only touches what the eigenvector gradient ignores)
+    ln.backward()
+    lr.backward()
+    for a, b in zip(g_s, g_s2):
+        assert (a.grad - b.grad).norm() <= 1e-3 * b.grad.norm()

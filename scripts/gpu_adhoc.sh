@@ -1,8 +1,8 @@
 set -o pipefail
 mkdir -p gpurun_out; export PYTHONPATH=$PWD TMPDIR=/tmp
-run() { tag=$1; shift; timeout -k 10 200 "$@" > gpurun_out/q_$tag.log 2>&1; rc=$?; if [ $rc -ne 0 ]; then tail -3 gpurun_out/q_$tag.log; case $rc in 124|134|137|139) exit $rc;; esac; return 0; fi; echo "$tag $(tail -1 gpurun_out/q_$tag.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["final_loss"])')"; }
-for t in 64 128 256; do
-  MDA_EIG_THREADS=$t timeout -k 10 200 python -u -m pytest tests/test_gpu_kdsvd.py -x -q --timeout 150 --timeout-method thread -k "eigh or cpu" > gpurun_out/t_e$t.log 2>&1 || { tail -20 gpurun_out/t_e$t.log; exit 1; }
-  tail -1 gpurun_out/t_e$t.log
-  run kdsvd_t$t env MDA_EIG_THREADS=$t python bench.py --steps 100 --warmup 20 --cfg configs/cifar100/kdsvd.yaml
-done
+timeout -k 10 600 python -u -m pytest tests/test_gpu_kdsvd.py tests/test_gpu_e2e.py tests/test_gpu_head.py -x -q --timeout 150 --timeout-method thread > gpurun_out/t_fin.log 2>&1 || { tail -30 gpurun_out/t_fin.log; exit 1; }
+tail -1 gpurun_out/t_fin.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
+tail -1 gpurun_out/smoke.log
+timeout -k 10 300 python bench.py > gpurun_out/bench_default.log 2>&1 || { tail -5 gpurun_out/bench_default.log; exit 1; }
+tail -1 gpurun_out/bench_default.log | cut -c1-300

@@ -31,6 +31,12 @@ from ..ops import crd as CO
 from ..ops import losses as L
 
 
+def _capturing(device=None) -> bool:
+    if device is not None and torch.device(device).type != "cuda":
+        return False
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+
+
 class Normalize(nn.Module):
     def __init__(self, power=2):
         super().__init__()
@@ -132,28 +138,50 @@ class ContrastMemory(nn.Module):
             return
         ws = dist.get_world_size()
         B, D = v1.shape
-        xl = getattr(self, "_xlocal", None)
-        if xl is None or xl.shape != (B, 1 + 2 * D) or xl.device != v1.device:
-            # (eager steps only: a capture reuses the warm-up's buffers)
-            self._xlocal = torch.empty(B, 1 + 2 * D, dtype=torch.float64, device=v1.device)
-            self._xall = torch.empty(ws * B, 1 + 2 * D, dtype=torch.float64, device=v1.device)
-        self._xlocal[:, 0].copy_(y)
-        self._xlocal[:, 1:1 + D].copy_(v1)
-        self._xlocal[:, 1 + D:].copy_(v2)
-        self._xdim = D
+        # one (local, gathered) buffer pair PER batch shape, never rebound: the
+        # captured fwd+bwd / update graphs keep the full-batch pair, and an eager
+        # partial batch (the epoch's last, drop_last=False) gets its own pair
+        # instead of freeing the memory those graphs were recorded against
+        key = (B, D, v1.device)
+        bufs = self.__dict__.setdefault("_xbufs", {})
+        if key not in bufs:
+            if _capturing(v1.device):
+                raise RuntimeError("CRD exchange buffers must exist before capture "
+                                   "(the eager warm-up step of the same shape creates them)")
+            bufs[key] = (torch.empty(B, 1 + 2 * D, dtype=torch.float64, device=v1.device),
+                         torch.empty(ws * B, 1 + 2 * D, dtype=torch.float64, device=v1.device))
+        xl, _ = bufs[key]
+        xl[:, 0].copy_(y)
+        xl[:, 1:1 + D].copy_(v1)
+        xl[:, 1 + D:].copy_(v2)
+        if _capturing(v1.device):
+            self._graph_key = key   # what every replay of the captured step staged into
+        else:
+            self._eager_key = key   # this eager step's rows (consumed by apply_exchange)
+
+    def _xkey(self):
+        """Buffers of the current step: an eager step's own pair, else the pair
+        the captured graphs stage into (a replay runs no Python in between)."""
+        k = None if _capturing() else self.__dict__.get("_eager_key")
+        return k if k is not None else self.__dict__.get("_graph_key")
 
     def exchange(self):
         """The memory-update all-gather (a collective: never inside a capture
         in split mode; TrainStep calls it between the graphs)."""
-        if getattr(self, "_xlocal", None) is not None:
-            dist.all_gather_into_tensor(self._xall, self._xlocal)
+        k = self._xkey()
+        if k is not None:
+            xl, xa = self._xbufs[k]
+            dist.all_gather_into_tensor(xa, xl)
 
     @torch.no_grad()
     def apply_exchange(self):
-        xa = getattr(self, "_xall", None)
-        if xa is None:
+        k = self._xkey()
+        if k is None:
             return
-        D = self._xdim
+        if not _capturing():
+            self._eager_key = None
+        _, xa = self._xbufs[k]
+        D = k[1]
         y = xa[:, 0].long()
         CO.update(self.memory_v1, y, xa[:, 1:1 + D].float(), self.momentum)
         CO.update(self.memory_v2, y, xa[:, 1 + D:].float(), self.momentum)

@@ -98,6 +98,7 @@ class GradReducer:
         self._wires = {}
         self._hooks = []
         self._armed = False
+        self._error = None
         if self.overlap:
             for i, p in enumerate(flat.params):
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
@@ -120,10 +121,12 @@ class GradReducer:
             return
         b = self._param_bucket[i]
         self._pending[b] -= 1
-        if self._pending[b] < 0 and b in self._works:
+        if self._pending[b] < 0 and b in self._works and self._error is None:
             # more contributions than the calibration step counted, after the
-            # bucket was already all-reduced: the reduced values are stale
-            raise RuntimeError(
+            # bucket was already all-reduced: the reduced values are stale.
+            # Recorded, not raised here: the peers are about to enter the
+            # remaining buckets' collectives, so finish() drains them first
+            self._error = (
                 f"GradReducer: parameter {i} received a gradient contribution after its "
                 f"bucket {b} was launched (calibrated {self._expected[i] if self._expected else '?'} "
                 "contributions); disable DIST.OVERLAP or keep the backward graph static")
@@ -184,10 +187,10 @@ class GradReducer:
             return
         if self._calib is not None:
             self._expected, self._calib = self._calib, None
-        elif self._armed and any(p < 0 for p in self._pending):
-            raise RuntimeError(f"GradReducer: bucket contribution counts went negative "
-                               f"{self._pending} (a parameter got more gradient writes than "
-                               f"the calibration step counted)")
+        elif self._armed and any(p < 0 for p in self._pending) and self._error is None:
+            self._error = (f"GradReducer: bucket contribution counts went negative "
+                           f"{self._pending} (a parameter got more gradient writes than "
+                           f"the calibration step counted)")
         for b in range(len(self.buckets)):
             if b not in self._works:
                 self._launch(b, async_op=True)
@@ -200,6 +203,12 @@ class GradReducer:
         self._armed = False
         if self in _ARMED:
             _ARMED.remove(self)
+        # every bucket was launched and drained before raising, so no peer is
+        # left waiting in a collective this rank skipped (a peer that goes on
+        # to the next step fails on the process group's timeout, not a hang)
+        err, self._error = self._error, None
+        if err is not None:
+            raise RuntimeError(err)
 
     def reduce_all(self) -> None:
         """Non-overlapped reduction of the currently bound gradient set."""

@@ -32,12 +32,29 @@ def enabled() -> bool:
     return _state["enabled"]
 
 
+def _fresh_stream(idx, avoid=()) -> "torch.cuda.Stream":
+    """A pool stream that is not the current stream nor any in ``avoid``.
+
+    ``torch.cuda.Stream()`` hands out the device's pool streams round-robin
+    (32 per priority): after enough TrainSteps (capture, DOT-dual, branch and
+    teacher streams) a new draw can alias a stream already in use, so draw
+    again until it differs (the pool has more streams than a step uses)."""
+    bad = {torch.cuda.current_stream(idx).cuda_stream}
+    bad.update(a.cuda_stream for a in avoid if a is not None)
+    s = torch.cuda.Stream(device=idx)
+    for _ in range(64):
+        if s.cuda_stream not in bad:
+            break
+        s = torch.cuda.Stream(device=idx)
+    return s
+
+
 def side_stream(device) -> "torch.cuda.Stream":
     idx = torch.device(device).index or 0
     with _lock:
         s = _streams.get(idx)
         if s is None:
-            s = torch.cuda.Stream(device=idx)
+            s = _fresh_stream(idx, (_branch_streams.get(idx),))
             _streams[idx] = s
         return s
 
@@ -50,7 +67,10 @@ def renew(device) -> None:
     the 4 queues of a process, which of a step's concurrently replayed streams
     share a queue decides whether they overlap -- DOT's dual-stream step ran
     1.33 ms/step alone and 1.59-1.60 after another DOT or two other configs
-    in the same process, `profiles/r3_dot_history.md`.)"""
+    in the same process, `profiles/r3_dot_history.md`.)  The pool is
+    round-robin, so a "fresh" draw can wrap around onto a live stream:
+    :func:`_fresh_stream` skips the current one, and the launch helpers run
+    inline when the side stream still equals the current stream."""
     idx = torch.device(device).index or 0
     with _lock:
         _streams.pop(idx, None)
@@ -93,6 +113,10 @@ def run_teacher_async(teacher, image, train_bn: bool = False) -> TeacherOutput:
             return TeacherOutput(teacher(image))
     s = side_stream(image.device)
     cur = torch.cuda.current_stream()
+    if s.cuda_stream == cur.cuda_stream:
+        # an aliased pool stream: a fork onto the same stream is no fork
+        with torch.no_grad():
+            return TeacherOutput(teacher(image))
     s.wait_stream(cur)
     with torch.cuda.stream(s), torch.no_grad():
         image.record_stream(s)
@@ -232,7 +256,7 @@ def branch_stream(device) -> "torch.cuda.Stream":
     with _lock:
         s = _branch_streams.get(idx)
         if s is None:
-            s = torch.cuda.Stream(device=idx)
+            s = _fresh_stream(idx, (_streams.get(idx),))
             _branch_streams[idx] = s
         return s
 

@@ -200,3 +200,58 @@ def test_bench_refuses_mismatched_world():
     out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"],
                          capture_output=True, text=True, timeout=300, env=env, cwd=root)
     assert out.returncode != 0 and "WORLD_SIZE" in (out.stderr + out.stdout)
+
+
+def _crd_exchange_worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank), LOCAL_RANK=str(rank), MDA_BACKEND="torch")
+    torch.set_num_threads(1)
+    import torch.distributed as dist
+    from mdistiller_ddp_amd.parallel import dist as D
+    from mdistiller_ddp_amd.distillers.CRD import ContrastMemory
+    D.init_distributed("gloo", 60.0, device="cpu")
+    torch.manual_seed(0)  # identical banks on every rank
+    mem = ContrastMemory(16, 64, K=8)
+    start = (mem.memory_v1.clone(), mem.memory_v2.clone())
+    g = torch.Generator().manual_seed(7)
+    rows = []
+    # a full batch (B=4), then the epoch's partial last batch (B=3), then a full one:
+    # each step stages its own rows, all-gathers them and applies every rank's in order
+    for step, B in enumerate((4, 3, 4)):
+        allv = [(torch.randn(B, 16, generator=g), torch.randn(B, 16, generator=g)) for _ in range(world)]
+        ally = [torch.arange(B) + 8 * (step * world + r) for r in range(world)]
+        rows.append((allv, ally))
+        v1, v2 = allv[rank]
+        mem._pending = (v1, v2, ally[rank])
+        mem.apply_pending()
+        mem.exchange()
+        mem.apply_exchange()
+    out = {"v1": mem.memory_v1.clone(), "v2": mem.memory_v2.clone(), "keys": len(mem._xbufs)}
+    # single-process reference: the concatenated rows of every rank, in rank order
+    from mdistiller_ddp_amd.ops import crd as CO
+    r1, r2 = start[0].clone(), start[1].clone()
+    for allv, ally in rows:
+        y = torch.cat(ally)
+        CO.update_ref(r1, y, torch.cat([a for a, _ in allv]), mem.momentum)
+        CO.update_ref(r2, y, torch.cat([b for _, b in allv]), mem.momentum)
+    out["ref_v1"], out["ref_v2"] = r1, r2
+    out["start_v1"] = start[0]
+    torch.save(out, os.path.join(outdir, f"r{rank}.pt"))
+    D.destroy()
+
+
+def test_crd_exchange_matches_single_process_update_with_partial_batch():
+    """the gathered update equals a single-process update over the
+    concatenated per-rank rows, and a partial batch gets its own buffers (the
+    full-batch pair a captured graph was recorded against is never rebound)."""
+    world = 2
+    with tempfile.TemporaryDirectory() as td:
+        mp.spawn(_crd_exchange_worker, args=(world, _free_port(), td), nprocs=world, join=True)
+        res = [torch.load(os.path.join(td, f"r{r}.pt"), weights_only=True) for r in range(world)]
+    for r in res:
+        assert r["keys"] == 2  # B=4 and B=3 pairs, both kept
+        assert not torch.equal(r["v1"], r["start_v1"])  # the bank really changed
+        # fp64 staging + the same per-row arithmetic: equal to fp32 rounding
+        assert torch.allclose(r["v1"], r["ref_v1"], atol=1e-6, rtol=0)
+        assert torch.allclose(r["v2"], r["ref_v2"], atol=1e-6, rtol=0)
+    assert torch.equal(res[0]["v1"], res[1]["v1"]) and torch.equal(res[0]["v2"], res[1]["v2"])

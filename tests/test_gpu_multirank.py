@@ -75,8 +75,16 @@ def _worker(rank, world, port, scenario, outdir):
         for i, b in enumerate(ld.batches):
             b["index"] = (torch.arange(32, device=dev) + 32 * (2 * i + rank)) % 1000
             b["contrastive_index"][:, 0] = b["index"]
-    for b in ld:
+    mem0 = None
+    if typ == "CRD":
+        mem0 = torch.cat([d.contrast.memory_v1.reshape(-1), d.contrast.memory_v2.reshape(-1)]).clone()
+    for i, b in enumerate(ld):
         st.step(b)
+        if typ == "CRD" and i == 10:
+            # an epoch's partial last batch between graph replays:
+            # it runs eagerly on its own exchange buffers; the captured graphs'
+            # full-batch buffers must stay valid for the replays that follow
+            st.step({k: v[:24] for k, v in b.items()})
     torch.cuda.synchronize()
     out["graph"] = st._graphs is not None
     # split = the optimizer replays as its own graph after the eager all-reduce
@@ -96,6 +104,8 @@ def _worker(rank, world, port, scenario, outdir):
         allm = [torch.empty_like(mem) for _ in range(world)]
         dist.all_gather(allm, mem)
         out["memory_equal"] = all(torch.equal(allm[0], a) for a in allm)
+        out["memory_moved"] = float((mem - mem0).norm())
+        out["memory_finite"] = bool(torch.isfinite(mem).all())
     if scenario == "dkd":
         # reduced grad == mean of the local grads (one eager fwd+bwd)
         st.flat.zero_grad()
@@ -135,3 +145,4 @@ def test_two_ranks_one_gpu_graph_replicas(scenario):
         assert res[0]["grad_rel"] < 1e-5, res[0]
     if scenario == "crd":
         assert all(r["memory_equal"] for r in res), res
+        assert all(r["memory_moved"] > 0 and r["memory_finite"] for r in res), res

@@ -85,6 +85,9 @@ CFG.RUNTIME.TEACHER_STREAM = True    # teacher forward on its own HIP stream
 CFG.RUNTIME.DOT_DUAL_STREAM = True   # DOT: replay the task / KD backwards as concurrent graphs
 CFG.RUNTIME.TEACHER_LOOKAHEAD = "auto"  # auto | on | off: captured steps run the teacher of batch t+1
                                         # beside the student step t (auto: off for >= 128 px feature KD)
+CFG.RUNTIME.TEACHER_GRAPH = "split"  # split | fork: the look-ahead teacher as its OWN single-chain graph
+                                     # replayed on the teacher stream (split), or forked inside the step graph
+CFG.RUNTIME.TEACHER_FIRST = True     # split: enqueue the teacher graph before the student's
 CFG.RUNTIME.WGRAD_DEFER = True       # captured backward: all layers' wgrad split reductions in one launch
 CFG.RUNTIME.WGRAD_STREAM = "auto"    # auto | on | off: captured-backward wgrads on a forked stream (auto: >= 128 px inputs)
 CFG.RUNTIME.FOLD_TEACHER_BN = True   # fold frozen teacher BN into conv weights
@@ -101,8 +104,10 @@ CFG.DIST.BACKEND = "auto"            # auto -> nccl(RCCL) on GPU, gloo on CPU
 CFG.DIST.BUCKET_MB = 8.0             # gradient bucket size (MB of fp32)
 CFG.DIST.TIMEOUT_S = 600
 CFG.DIST.GRAD_DTYPE = "fp32"         # fp32 | bf16 wire format for gradient all-reduce
-CFG.DIST.GRAPH_COMM = "auto"         # capture | split | auto(=split): all-reduce inside the step's
-                                     # hipGraph (RCCL, overlapped with backward) or between two graphs
+CFG.DIST.GRAPH_COMM = "auto"         # events | split | capture | auto (= events with RCCL, split with gloo):
+                                     # per-bucket all-reduce behind events of the captured backward
+                                     # (events), eager between the fwd+bwd and update graphs (split),
+                                     # or inside one multi-branch graph (capture)
 CFG.DIST.BROADCAST_INIT = True       # rank-0 broadcast of all params/buffers at step construction (C2)
 
 # Distillation methods -----------------------------------------------------

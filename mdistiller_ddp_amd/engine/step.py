@@ -217,21 +217,30 @@ class TrainStep:
         self._static_next = None
         self._x_for = None      # the image tensor whose teacher outputs the feed holds
         self._la_misses = 0     # consecutive look-ahead steps without a next batch
+        # the look-ahead teacher as its own graph on the teacher stream (see
+        # runtime/streams.py::TeacherFeed.capture_pipe) instead of a branch of
+        # the step graph
+        self.teacher_split = str(cfg.RUNTIME.get("TEACHER_GRAPH", "split")).lower() == "split"
+        self.teacher_first = bool(cfg.RUNTIME.get("TEACHER_FIRST", True))
+        self._tsplit = None     # (graph, T list, X list, stream, teacher-done event, copy-done event)
+        self._tp_inflight = False
         self.wgrad_side = (False if self.device.type != "cuda" else
                            "auto" if ws == "auto" else ws in (True, "true", "1", "on"))
         self._wg_auto = False
         self._wg_stream = None
         self.wgrad_defer = self.device.type == "cuda" and bool(cfg.RUNTIME.get("WGRAD_DEFER", True))
 
-    def _graph_comm_mode(self, cfg) -> bool:
-        """True: the gradient all-reduce is captured inside the step's hipGraph.
+    def _graph_comm_mode(self, cfg):
+        """How the gradient all-reduce meets the captured step at world > 1.
 
-        Only RCCL collectives are capturable (gloo reduces on the host).
-        ``auto`` = ``split``: RCCL rejects two ranks on one device, so the
-        single-GPU test box cannot exercise captured multi-rank collectives;
-        the split path (fwd+bwd graph -> eager async RCCL all-reduce -> optimizer
-        graph, no host synchronisation) is the one covered by the 2-rank GPU
-        test.  ``capture`` opts into the single graph.
+        ``False`` (split): fwd+bwd graph -> eager bucketed all-reduce -> optimizer
+        graph.  ``"events"``: the same two graphs, but the captured backward
+        records one external event per gradient bucket and the all-reduces are
+        enqueued right after the replay launch on a comm stream, each behind
+        its bucket's event, so they overlap the rest of the backward
+        (GradReducer.arm_capture).  ``True`` (capture): the all-reduce inside
+        the single step graph (a multi-branch graph, slow on ROCm's executor).
+        ``auto`` = events with RCCL, split otherwise (gloo reduces on the host).
         """
         if self.world <= 1 or not self.use_graph:
             return False
@@ -242,7 +251,9 @@ class TrainStep:
             if not rccl:
                 raise ValueError("DIST.GRAPH_COMM=capture needs the RCCL (nccl) backend")
             return True
-        return False  # split / auto
+        if mode == "events" or (mode == "auto" and rccl):
+            return "events"
+        return False  # split
 
     # ------------------------------------------------------------------
     def set_epoch(self, epoch: float) -> None:
@@ -300,10 +311,11 @@ class TrainStep:
         self.opt.set_active([id(p) in r for p in self.flat.params])
         self._reach_ready = True
 
-    def _fwd_bwd(self, b: dict, overlap_comm: bool):
+    def _fwd_bwd(self, b: dict, overlap_comm):
         preds, losses = self._fwd(b)
         armed = self._arm_wgrad_stream()
         deferred = (not armed) and self._arm_wgrad_defer()
+        events = overlap_comm == "events" and not self.is_dot
         try:
             if self.is_dot:
                 self.flat.bind_grads(1)
@@ -311,7 +323,12 @@ class TrainStep:
                 self.flat.bind_grads(0)
                 losses["loss_ce"].backward()
             else:
-                if overlap_comm:
+                if events:
+                    from ..ops import hip_train
+                    # a bucket's deferred weight-gradient reductions are flushed
+                    # before its event, so the event marks final gradients
+                    self.reducer.arm_capture(hip_train.flush_wgrad_reduces if deferred else None)
+                elif overlap_comm:
                     self.reducer.arm()
                 # backward of the loss terms with unit seeds straight into each term
                 # (no sum node, no per-step fill kernels)
@@ -322,6 +339,8 @@ class TrainStep:
             self._flush_wgrad_defer(deferred)
             self._join_wgrad_stream(armed)
             join_branches()
+        if events:
+            self.reducer.finish_capture()
         self._post_backward()
         feed = self.distiller.__dict__.get("_teacher_feed")
         if feed is not None:
@@ -332,7 +351,8 @@ class TrainStep:
         """While a backward is being captured (and the wgrads stay on the main
         stream), defer every layer's split reduction to one multi-layer launch
         at the end of the backward (``hip_train.set_wgrad_defer``)."""
-        if not (self.wgrad_defer and torch.cuda.is_current_stream_capturing()) or self.graph_comm:
+        if not (self.wgrad_defer and torch.cuda.is_current_stream_capturing()) or \
+                self.graph_comm is True:
             return False
         from ..ops import hip_train
         hip_train.set_wgrad_defer(True)
@@ -353,7 +373,7 @@ class TrainStep:
         all-reduce captured in the same graph (its bucket hooks assume the
         gradients are complete on the main stream)."""
         if not (self.wgrad_side and torch.cuda.is_current_stream_capturing()) or self.graph_comm:
-            return False
+            return False  # (events mode too: its bucket events assume one stream)
         if self.is_dot and self.dot_dual:
             return False  # measured: the forks serialise the two concurrently replayed passes
         if self.wgrad_side == "auto" and not self._wg_auto:
@@ -410,15 +430,19 @@ class TrainStep:
             self._dot_reachability(losses)
         return preds, losses
 
-    def _reduce(self):
+    def _reduce(self, replay: bool = False):
         """The step's collectives: the gradient all-reduce, then any exchange the
         distiller staged after its backward (CRD's memory-update all-gather).
         Eager between the fwd+bwd and update graphs (split mode), captured in
-        the one graph in ``DIST.GRAPH_COMM=capture`` mode."""
+        the one graph in ``DIST.GRAPH_COMM=capture`` mode; after a replay in
+        ``events`` mode each bucket's all-reduce waits only for its event."""
         if self.world <= 1:
             return
         if self.is_dot:
             self.reducer.reduce_sets((0, 1))
+        elif replay and self.graph_comm == "events" and self.reducer.graph_events is not None:
+            self.reducer.launch_from_events()
+            self.reducer.wait_launched()
         else:
             self.reducer.finish()
         exchange = getattr(self.distiller, "exchange", None)
@@ -473,17 +497,36 @@ class TrainStep:
             # back to MIOpen on some layer): stay eager for good
             self.use_graph = False
             return out
-        if self.is_dot and self.dot_dual and not self.graph_comm:
+        if self.is_dot and self.dot_dual and self.graph_comm is not True:
             return self._capture_dot_dual(static, pool, s, out)
         feed = None
         if self._lookahead_on(static) and getattr(self.distiller, "teacher", None) is not None:
             feed = self._capture_teacher_feed(static, pool, s)
+            if self.teacher_split:
+                feed.mode = "use"  # the step graph reads X; the teacher is a graph of its own
         try:
             self._capture_step(static, pool, s)
         finally:
             if feed is not None:
                 feed.mode = None  # eager steps (e.g. a partial batch) run the teacher inline
+        if feed is not None and self.teacher_split:
+            self._capture_teacher_split(feed)
         return out
+
+    def _capture_teacher_split(self, feed):
+        """``RUNTIME.TEACHER_GRAPH=split``: the next batch's teacher forward as a
+        single-chain graph of its own, replayed on the teacher stream beside the
+        student's step graph (own memory pool: the two graphs run concurrently,
+        so no block of one may be handed to the other)."""
+        from ..runtime.streams import side_stream
+        ts = side_stream(self.device)
+        g = torch.cuda.CUDAGraph()
+        ts.wait_stream(torch.cuda.current_stream())
+        t_list, x_list = feed.capture_pipe(self.distiller.teacher, g, torch.cuda.graph_pool_handle(), ts,
+                                           lambda: _autocast(self.device, self.dtype))
+        self._tsplit = (g, t_list, x_list, ts, torch.cuda.Event(), torch.cuda.Event())
+        self._tp_inflight = False
+        self._x_for = None
 
     def _lookahead_on(self, static) -> bool:
         """Measured (profiles/r2_teacher_lookahead_ab.md): the look-ahead takes the
@@ -533,7 +576,7 @@ class TrainStep:
                 preds, losses = self._fwd_bwd(static, overlap_comm=False)
                 self._update(preds, static["target"], losses)
             g2 = None
-        elif self.graph_comm:
+        elif self.graph_comm is True:
             # one graph: bucket all-reduces are issued from the backward hooks
             # while the rest of backward is being captured, so the replayed
             # DAG overlaps them with the remaining gradient kernels
@@ -544,7 +587,8 @@ class TrainStep:
             g2 = None
         else:
             with torch.cuda.graph(g1, pool=pool, stream=s):
-                preds, losses = self._fwd_bwd(static, overlap_comm=False)
+                preds, losses = self._fwd_bwd(static, overlap_comm=self.graph_comm == "events"
+                                              and "events")
             g2 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g2, pool=pool, stream=s):
                 self._update(preds, static["target"], losses)
@@ -689,6 +733,8 @@ class TrainStep:
             out = self._eager(b)
             self.steps_done += 1
             return out
+        if self._tsplit is not None and self._pipe is not None and self._dual is None:
+            return self._step_split(batch, b, next_batch, static, preds, losses)
         # the step's input copies in one multi-tensor launch (each separate copy is a
         # ~5 us kernel ahead of the graph)
         dst = [static[k] for k in b]
@@ -728,8 +774,71 @@ class TrainStep:
         g1, g2 = self._graphs
         g1.replay()
         if g2 is not None:  # split mode: eager all-reduce between the graphs
-            self._reduce()
+            self._reduce(replay=True)
             g2.replay()
+        self.steps_done += 1
+        return preds, losses
+
+    def _step_split(self, batch, b, next_batch, static, preds, losses):
+        """A replayed step with the look-ahead teacher as its own graph: main
+        stream -- wait for the teacher of this batch, ONE multi-tensor copy of
+        the inputs and of its outputs T into X, the student's step graph(s);
+        teacher stream -- once that copy is done, the next image into the
+        teacher's input buffer and the teacher graph of the next batch."""
+        g_teach, _ = self._pipe
+        g_tp, t_list, x_list, ts, ev_t, ev_c = self._tsplit
+        cur = torch.cuda.current_stream()
+        nxt = self._static_next["image"]
+        prefetched = False
+        if self._tp_inflight:
+            cur.wait_event(ev_t)  # T (or a discarded prefetch) is complete; nxt is free
+            self._tp_inflight = False
+            prefetched = self._x_for is not None and self._x_for is batch.get("image")
+        dst = [static[k] for k in b]
+        src = [b[k] for k in b]
+        if prefetched:
+            torch._foreach_copy_(dst + x_list, src + t_list)
+        else:
+            torch._foreach_copy_(dst, src)
+            nxt.copy_(static["image"], non_blocking=True)  # this batch was not prefetched
+            g_teach.replay()                                # its teacher straight into X
+        nimg = None
+        if next_batch is not None and next_batch.get("image") is not None \
+                and tuple(next_batch["image"].shape) == tuple(nxt.shape):
+            nimg = self._prep_image(next_batch["image"])
+            self._x_for = next_batch["image"]
+            self._la_misses = 0
+        else:
+            self._x_for = None
+            self._la_misses += 1
+            if self._la_misses >= 3:
+                self.lookahead = False
+                self.invalidate_graph()
+                out = self._eager(b)
+                self.steps_done += 1
+                return out
+
+        if nimg is not None:
+            ev_c.record(cur)  # X copied (and g_teach done): T and nxt may be overwritten
+
+        def launch_teacher():
+            ts.wait_event(ev_c)
+            with torch.cuda.stream(ts):
+                nxt.copy_(nimg, non_blocking=True)
+                g_tp.replay()
+            ev_t.record(ts)
+            nimg.record_stream(ts)
+            self._tp_inflight = True
+
+        if nimg is not None and self.teacher_first:
+            launch_teacher()
+        g1, g2 = self._graphs
+        g1.replay()
+        if g2 is not None:
+            self._reduce(replay=True)
+            g2.replay()
+        if nimg is not None and not self.teacher_first:
+            launch_teacher()
         self.steps_done += 1
         return preds, losses
 
@@ -741,6 +850,12 @@ class TrainStep:
         self._drop_feed()
 
     def _drop_feed(self) -> None:
+        if self._tsplit is not None:
+            if self._tp_inflight:
+                torch.cuda.current_stream().wait_event(self._tsplit[4])
+                self._tp_inflight = False
+            torch.cuda.current_stream().synchronize()
+            self._tsplit = None
         if self._pipe is not None:
             self._pipe = None
             self.distiller.__dict__.pop("_teacher_feed", None)

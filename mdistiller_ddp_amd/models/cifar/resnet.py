@@ -13,6 +13,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ...ops.nn import conv_bn_act, grad_fork, pool_linear
+from ...ops.hip_train import can_defer_residual
 from ...runtime.streams import run_branch
 from .._base import ModelBase, PreactStage
 
@@ -36,8 +37,9 @@ class BasicBlock(nn.Module):
         self.downsample = downsample
         self.stride = stride
 
-    def _shortcut(self, x, fork=None):
-        return conv_bn_act(x, self.downsample[0], self.downsample[1], "none", fork=fork)[0]
+    def _shortcut(self, x, fork=None, defer=False):
+        return conv_bn_act(x, self.downsample[0], self.downsample[1], "none", fork=fork,
+                           defer_apply=defer)[0]
 
     def forward(self, x):
         # x feeds conv1 and the shortcut: their input gradients are summed in
@@ -50,8 +52,10 @@ class BasicBlock(nn.Module):
             # projection shortcut on the branch stream, beside conv2.  Created
             # after conv1, so autograd issues its backward first: the shorter
             # branch chain (BN backward + 1x1 dgrad) parks its input gradient
-            # and conv1's dgrad, last on the main chain, adds it in its epilogue
-            res = run_branch(x, lambda t: self._shortcut(t, fork))
+            # and conv1's dgrad, last on the main chain, adds it in its epilogue.
+            # Its BN is applied inside bn2's apply (ops/hip_train.py VirtualBN)
+            defer = can_defer_residual(h, self.conv2, self.bn2)
+            res = run_branch(x, lambda t: self._shortcut(t, fork, defer))
             fork = None
         return conv_bn_act(h, self.conv2, self.bn2, "relu", residual=res,
                            want_preact=self.is_last and self._need_preact, res_fork=fork)
@@ -74,14 +78,16 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
         self.stride = stride
 
-    def _shortcut(self, x, fork=None):
-        return conv_bn_act(x, self.downsample[0], self.downsample[1], "none", fork=fork)[0]
+    def _shortcut(self, x, fork=None, defer=False):
+        return conv_bn_act(x, self.downsample[0], self.downsample[1], "none", fork=fork,
+                           defer_apply=defer)[0]
 
     def forward(self, x):
         fork = grad_fork(x)
         h, _ = conv_bn_act(x, self.conv1, self.bn1, "relu", fork=fork)
-        res = x if self.downsample is None else run_branch(x, lambda t: self._shortcut(t, fork))
         h, _ = conv_bn_act(h, self.conv2, self.bn2, "relu")
+        res = x if self.downsample is None else run_branch(
+            x, lambda t: self._shortcut(t, fork, can_defer_residual(h, self.conv3, self.bn3)))
         return conv_bn_act(h, self.conv3, self.bn3, "relu", residual=res,
                            want_preact=self.is_last and self._need_preact,
                            res_fork=fork if self.downsample is None else None)

@@ -47,7 +47,7 @@ SIGNATURES = {
     "mda_conv_dgrad": "pppp" + "i" * 14 + "s",
     "mda_conv_dgrad_res": "ppppp" + "i" * 14 + "s",
     "mda_conv_dgrad_bnsum": "ppppp" + "i" * 14 + "ppp" + "i" + "p" + "s",
-    "mda_conv_dgrad_bnsum_g": "ppppp" + "i" * 14 + "ppp" + "i" + "p" + "i" + "s",
+    "mda_conv_dgrad_bnsum_g": "ppppp" + "i" * 14 + "ppp" + "i" + "p" + "i" + "p" + "s",
     "mda_conv_fwd_bnacc_g": "ppppp" + "i" * 14 + "i" + "s",
     "mda_pack_conv_weights_gc": "ppp" + "i" * 7 + "s",
     "mda_channel_gather": "ppp" + "iii" + "s",
@@ -88,8 +88,9 @@ SIGNATURES = {
     "mda_bn_region_bytes": "ip",
     "mda_bn_stats_acc": "piips",
     "mda_bn_apply_fin": "ppii" + "ppppp" + "ff" + "p" + "ppp" + "i" + "s",
-    "mda_bn_bwd_fused": "ppppp" + "p" + "iii" + "pp" + "pp" + "ppp" + "ppp" + "s",
-    "mda_bn_bwd_apply_reg": "pppp" + "p" + "iii" + "p" + "pp" + "ppp" + "ppp" + "s",
+    "mda_bn_apply_fin_vr": "ppii" + "ppppp" + "ff" + "p" + "ppp" + "i" + "pppppp" + "ff" + "p" + "s",
+    "mda_bn_bwd_fused": "ppppp" + "p" + "iii" + "pp" + "pp" + "ppp" + "ppp" + "p" + "s",
+    "mda_bn_bwd_apply_reg": "pppp" + "p" + "iii" + "p" + "pp" + "ppp" + "ppp" + "p" + "s",
     "mda_conv_fwd_bnacc": "ppppp" + "i" * 14 + "s",
     # CRD memory (csrc/crd.hip)
     "mda_crd_scores": "ppppiiifs",
@@ -99,7 +100,7 @@ SIGNATURES = {
     "mda_pool_fc_fwd": "ipppppiiiis",
     "mda_pool_fc_bwd": "ippppppp" + "iiiii" + "s",
     "mda_sym_eig": "piiipp" + "s",
-    "mda_pool_fc_bwd_bn": "ippppppp" + "iiiii" + "pppip" + "s",
+    "mda_pool_fc_bwd_bn": "ippppppp" + "iiiii" + "pppip" + "p" + "s",
     "mda_meters_update": "ippii" + "pppp" + "ips",
     # ReviewKD HCL + ABF (csrc/reviewkd.hip)
     "mda_hcl_loss": "piiipfpfps",

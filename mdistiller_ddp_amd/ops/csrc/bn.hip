@@ -661,7 +661,8 @@ _Pragma("unroll")
 constexpr int APPLY_V = 4;  // 16-byte vectors per thread, all loads issued before any math
 
 __device__ __forceinline__ void apply8(const uint4& yv, const uint4& rv, bool has_res, const float* sc,
-                                       const float* sh, int act, uint4& out, uint4& z) {
+                                       const float* sh, int act, uint4& out, uint4& z,
+                                       const float* rsc = nullptr, const float* rsh = nullptr) {
   const uint32_t yw[4] = {yv.x, yv.y, yv.z, yv.w};
   const uint32_t rw[4] = {rv.x, rv.y, rv.z, rv.w};
   uint32_t zo[4], oo[4];
@@ -670,8 +671,14 @@ __device__ __forceinline__ void apply8(const uint4& yv, const uint4& rv, bool ha
     float v0 = __uint_as_float(yw[k] << 16) * sc[2 * k] + sh[2 * k];
     float v1 = __uint_as_float(yw[k] & 0xffff0000u) * sc[2 * k + 1] + sh[2 * k + 1];
     if (has_res) {
-      v0 += __uint_as_float(rw[k] << 16);
-      v1 += __uint_as_float(rw[k] & 0xffff0000u);
+      const float r0 = __uint_as_float(rw[k] << 16), r1 = __uint_as_float(rw[k] & 0xffff0000u);
+      if (rsc) {  // virtual residual: the raw input of another BN, applied here
+        v0 += r0 * rsc[2 * k] + rsh[2 * k];
+        v1 += r1 * rsc[2 * k + 1] + rsh[2 * k + 1];
+      } else {
+        v0 += r0;
+        v1 += r1;
+      }
     }
     zo[k] = pack_bf16x2(v0, v1);
     oo[k] = pack_bf16x2(act_f(v0, act), act_f(v1, act));
@@ -680,15 +687,48 @@ __device__ __forceinline__ void apply8(const uint4& yv, const uint4& rv, bool ha
   z = make_uint4(zo[0], zo[1], zo[2], zo[3]);
 }
 
+// Batch statistics of channel c from a region -> scale / shift (and, by block
+// 0, the [4][C] stats of the backward and the running-stat update).
+__device__ __forceinline__ void fin_channel(BnRegion* reg, int64_t M, int C, int c, const FinArgs& f,
+                                            float& sc, float& sh) {
+  double t0, t1;
+  region_channel<false>(reg, C, c, t0, t1);
+  const double mean = t0 / (double)M;
+  double var = t1 / (double)M - mean * mean;
+  if (var < 0) var = 0;
+  const float rstd = (float)(1.0 / sqrt(var + (double)f.eps));
+  const float g = f.gamma ? f.gamma[c] : 1.f;
+  const float bb = f.beta ? f.beta[c] : 0.f;
+  sc = g * rstd;
+  sh = bb - (float)mean * sc;
+  if (blockIdx.x == 0) {
+    f.stats[c] = (float)mean;
+    f.stats[C + c] = rstd;
+    f.stats[2 * C + c] = sc;
+    f.stats[3 * C + c] = sh;
+    if (f.running_mean) {
+      const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
+      f.running_mean[c] = (1.f - f.momentum) * f.running_mean[c] + f.momentum * (float)mean;
+      f.running_var[c] = (1.f - f.momentum) * f.running_var[c] + f.momentum * (float)unbiased;
+    }
+  }
+}
+
 // z = y*scale + shift (+ res); out = act(z); preact = z -- with the finalize
 // of the region's sums in the prologue.  The thread's APPLY_V vectors of y
 // (and res) are loaded BEFORE the prologue, so their latency overlaps the
 // region loads; grids past APPLY_V vectors per thread loop.
+// rreg != null: `res` is the RAW output of another training conv whose BN
+// (no activation: a projection shortcut) is applied here too -- its batch
+// statistics are finalized from rreg in the same prologue (rf: its affine,
+// running stats and [4][C] stats) and res contributes res*rscale + rshift, so
+// that BN never runs an apply pass of its own.
 __global__ void __launch_bounds__(256)
 bn_apply_fin_kernel(const bf16_t* __restrict__ y, BnRegion* __restrict__ reg, int64_t M, int C,
                     FinArgs f, const bf16_t* __restrict__ res, bf16_t* __restrict__ out,
-                    bf16_t* __restrict__ preact, int act) {
+                    bf16_t* __restrict__ preact, int act, BnRegion* __restrict__ rreg, FinArgs rf) {
   __shared__ float s_scale[SLOT_CMAX], s_shift[SLOT_CMAX];
+  __shared__ float s_rscale[SLOT_CMAX], s_rshift[SLOT_CMAX];
   const int64_t total = M * C / 8;
   const int c8 = C / 8;
   const int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -702,42 +742,28 @@ bn_apply_fin_kernel(const bf16_t* __restrict__ y, BnRegion* __restrict__ reg, in
     rv[k] = res ? ((const uint4*)res)[ii] : make_uint4(0, 0, 0, 0);
   }
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    double t0, t1;
-    region_channel<false>(reg, C, c, t0, t1);
-    const double mean = t0 / (double)M;
-    double var = t1 / (double)M - mean * mean;
-    if (var < 0) var = 0;
-    const float rstd = (float)(1.0 / sqrt(var + (double)f.eps));
-    const float g = f.gamma ? f.gamma[c] : 1.f;
-    const float bb = f.beta ? f.beta[c] : 0.f;
-    const float sc = g * rstd;
-    const float sh = bb - (float)mean * sc;
-    s_scale[c] = sc;
-    s_shift[c] = sh;
-    if (blockIdx.x == 0) {
-      f.stats[c] = (float)mean;
-      f.stats[C + c] = rstd;
-      f.stats[2 * C + c] = sc;
-      f.stats[3 * C + c] = sh;
-      if (f.running_mean) {
-        const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
-        f.running_mean[c] = (1.f - f.momentum) * f.running_mean[c] + f.momentum * (float)mean;
-        f.running_var[c] = (1.f - f.momentum) * f.running_var[c] + f.momentum * (float)unbiased;
-      }
-    }
+    fin_channel(reg, M, C, c, f, s_scale[c], s_shift[c]);
+    if (rreg) fin_channel(rreg, M, C, c, rf, s_rscale[c], s_rshift[c]);
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0 && f.nbt) f.nbt[0] += 1;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (f.nbt) f.nbt[0] += 1;
+    if (rreg && rf.nbt) rf.nbt[0] += 1;
+  }
   __syncthreads();
-  float sc[8], sh[8];
+  float sc[8], sh[8], rsc[8], rsh[8];
+  const bool vr = rreg != nullptr;
 #pragma unroll
   for (int k = 0; k < APPLY_V; ++k) {
     const int64_t i = i0 + k * stride;
     if (i < total) {
       const int cc = (int)(i % c8) * 8;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { sc[e] = s_scale[cc + e]; sh[e] = s_shift[cc + e]; }
+      for (int e = 0; e < 8; ++e) {
+        sc[e] = s_scale[cc + e]; sh[e] = s_shift[cc + e];
+        rsc[e] = vr ? s_rscale[cc + e] : 1.f; rsh[e] = vr ? s_rshift[cc + e] : 0.f;
+      }
       uint4 o, z;
-      apply8(yv[k], rv[k], res != nullptr, sc, sh, act, o, z);
+      apply8(yv[k], rv[k], res != nullptr, sc, sh, act, o, z, vr ? rsc : nullptr, vr ? rsh : nullptr);
       ((uint4*)out)[i] = o;
       if (preact) ((uint4*)preact)[i] = z;
     }
@@ -745,11 +771,14 @@ bn_apply_fin_kernel(const bf16_t* __restrict__ y, BnRegion* __restrict__ reg, in
   for (int64_t i = i0 + APPLY_V * stride; i < total; i += stride) {
     const int cc = (int)(i % c8) * 8;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) { sc[e] = s_scale[cc + e]; sh[e] = s_shift[cc + e]; }
+    for (int e = 0; e < 8; ++e) {
+      sc[e] = s_scale[cc + e]; sh[e] = s_shift[cc + e];
+      rsc[e] = vr ? s_rscale[cc + e] : 1.f; rsh[e] = vr ? s_rshift[cc + e] : 0.f;
+    }
     const uint4 y1 = ((const uint4*)y)[i];
     const uint4 r1 = res ? ((const uint4*)res)[i] : make_uint4(0, 0, 0, 0);
     uint4 o, z;
-    apply8(y1, r1, res != nullptr, sc, sh, act, o, z);
+    apply8(y1, r1, res != nullptr, sc, sh, act, o, z, vr ? rsc : nullptr, vr ? rsh : nullptr);
     ((uint4*)out)[i] = o;
     if (preact) ((uint4*)preact)[i] = z;
   }
@@ -769,6 +798,11 @@ struct BwdArgs {
   // layer's sum dres and sum dres*xhat_r (ry = its BN input, rstats = its
   // [4][C] stats) into rreg -- its backward is then one streaming pass too
   const bf16_t* ry; const float* rstats; BnRegion* rreg;
+  // optional: `res` is the RAW input of another training BN (a projection
+  // shortcut whose apply was folded into this layer's, mda_bn_apply_fin_vr):
+  // the residual value is res * vres[2C + c] + vres[3C + c] (vres = that
+  // layer's [4][C] stats)
+  const float* vres;
 };
 
 // res-producer sums of one 8-channel vector (dz = the stored dres values)
@@ -798,7 +832,8 @@ __device__ __forceinline__ void bwd_load8(const BwdArgs& a, int64_t o, Raw8& v) 
 
 // dz of 8 channels (z recomputed from y: no stored mask)
 __device__ __forceinline__ void bwd_dz8(const BwdArgs& a, const Raw8& v, const float* sc,
-                                        const float* sh, float (&dz)[8]) {
+                                        const float* sh, float (&dz)[8], const float* vsc,
+                                        const float* vsh) {
   const uint32_t yw[4] = {v.y.x, v.y.y, v.y.z, v.y.w}, dw[4] = {v.d.x, v.d.y, v.d.z, v.d.w};
   const uint32_t d2w[4] = {v.d2.x, v.d2.y, v.d2.z, v.d2.w}, pw[4] = {v.p.x, v.p.y, v.p.z, v.p.w};
   const uint32_t rw[4] = {v.r.x, v.r.y, v.r.z, v.r.w};
@@ -811,7 +846,7 @@ __device__ __forceinline__ void bwd_dz8(const BwdArgs& a, const Raw8& v, const f
     if (a.dout2) d += f(d2w[w]);
     if (a.act != ACT_NONE) {
       float z = f(yw[w]) * sc[k] + sh[k];
-      if (a.res) z += f(rw[w]);
+      if (a.res) z += a.vres ? f(rw[w]) * vsc[k] + vsh[k] : f(rw[w]);
       d *= act_grad(z, a.act);
     }
     if (a.dpre) d += f(pw[w]);
@@ -829,11 +864,13 @@ bn_bwd_fused_kernel(BwdArgs a) {
   const int cg = threadIdx.x % C8, r0 = threadIdx.x / C8;
   const bool active = r0 < rpi;
   const int c0 = cg * 8;
-  float sc[8], sh[8], mu[8], rs[8];
+  float sc[8], sh[8], mu[8], rs[8], vsc[8], vsh[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     mu[k] = a.stats[c0 + k]; rs[k] = a.stats[C + c0 + k];
     sc[k] = a.stats[2 * C + c0 + k]; sh[k] = a.stats[3 * C + c0 + k];
+    vsc[k] = a.vres ? a.vres[2 * C + c0 + k] : 1.f;
+    vsh[k] = a.vres ? a.vres[3 * C + c0 + k] : 0.f;
   }
   const int rstride = gridDim.x * rpi;
   float sdz[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sdzx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -862,7 +899,7 @@ bn_bwd_fused_kernel(BwdArgs a) {
       const int m = blockIdx.x * rpi + r0 + k * rstride;
       hy[k] = raw[k].y;
       if (active && m < M) {
-        bwd_dz8(a, raw[k], sc, sh, hz[k]);
+        bwd_dz8(a, raw[k], sc, sh, hz[k], vsc, vsh);
         accum(hz[k], hy[k]);
       }
     }
@@ -873,16 +910,16 @@ bn_bwd_fused_kernel(BwdArgs a) {
       bwd_load8(a, (int64_t)m * C + c0, v0);
       bwd_load8(a, (int64_t)(m + rstride) * C + c0, v1);
       float dz[8];
-      bwd_dz8(a, v0, sc, sh, dz);
+      bwd_dz8(a, v0, sc, sh, dz, vsc, vsh);
       accum(dz, v0.y);
-      bwd_dz8(a, v1, sc, sh, dz);
+      bwd_dz8(a, v1, sc, sh, dz, vsc, vsh);
       accum(dz, v1.y);
     }
     if (m < M) {
       Raw8 v0;
       bwd_load8(a, (int64_t)m * C + c0, v0);
       float dz[8];
-      bwd_dz8(a, v0, sc, sh, dz);
+      bwd_dz8(a, v0, sc, sh, dz, vsc, vsh);
       accum(dz, v0.y);
     }
   }
@@ -941,7 +978,7 @@ bn_bwd_fused_kernel(BwdArgs a) {
       Raw8 v0;
       bwd_load8(a, (int64_t)m * C + c0, v0);
       float dz[8];
-      bwd_dz8(a, v0, sc, sh, dz);
+      bwd_dz8(a, v0, sc, sh, dz, vsc, vsh);
       emit(m, dz, v0.y);
     }
   }
@@ -963,11 +1000,13 @@ bn_bwd_sums_kernel(BwdArgs a) {
   const int rpi = 256 / C8;
   const int cg = threadIdx.x % C8, r0 = threadIdx.x / C8;
   const int c0 = cg * 8;
-  float sc[8], sh[8], mu[8], rs[8];
+  float sc[8], sh[8], mu[8], rs[8], vsc[8], vsh[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     mu[k] = a.stats[c0 + k]; rs[k] = a.stats[C + c0 + k];
     sc[k] = a.stats[2 * C + c0 + k]; sh[k] = a.stats[3 * C + c0 + k];
+    vsc[k] = a.vres ? a.vres[2 * C + c0 + k] : 1.f;
+    vsh[k] = a.vres ? a.vres[3 * C + c0 + k] : 0.f;
   }
   float sdz[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sdzx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (r0 < rpi) {
@@ -975,7 +1014,7 @@ bn_bwd_sums_kernel(BwdArgs a) {
       Raw8 v;
       bwd_load8(a, o, v);
       float dz[8];
-      bwd_dz8(a, v, sc, sh, dz);
+      bwd_dz8(a, v, sc, sh, dz, vsc, vsh);
       const uint32_t yw[4] = {v.y.x, v.y.y, v.y.z, v.y.w};
 _Pragma("unroll")
       for (int e = 0; e < 8; ++e) {
@@ -999,7 +1038,7 @@ __global__ void __launch_bounds__(256)
 bn_bwd_apply_reg_kernel(BwdArgs a) {
   // per-channel operands in LDS: a thread's channel group changes along the
   // grid stride when C / 8 is not a power of two (MobileNetV2 widths)
-  __shared__ float s_m0[SLOT_CMAX], s_m1[SLOT_CMAX], s_st[4][SLOT_CMAX];
+  __shared__ float s_m0[SLOT_CMAX], s_m1[SLOT_CMAX], s_st[4][SLOT_CMAX], s_vr[2][SLOT_CMAX];
   const int C = a.C;
   const int c8 = C / 8;
   const int64_t total = (int64_t)a.M * c8;
@@ -1021,6 +1060,8 @@ bn_bwd_apply_reg_kernel(BwdArgs a) {
       s_m1[c] = t1 * invM;
 #pragma unroll
       for (int q = 0; q < 4; ++q) s_st[q][c] = a.stats[q * C + c];
+      s_vr[0][c] = a.vres ? a.vres[2 * C + c] : 1.f;
+      s_vr[1][c] = a.vres ? a.vres[3 * C + c] : 0.f;
       if (blockIdx.x == 0) {
         if (a.sums) { a.sums[c] = t0; a.sums[C + c] = t1; }
         if (a.dbeta) a.dbeta[c] += t0;
@@ -1032,13 +1073,14 @@ bn_bwd_apply_reg_kernel(BwdArgs a) {
   float r1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, r2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   auto emit = [&](int64_t i, const Raw8& v) {
     const int c0 = (int)(i % c8) * 8;
-    float sc[8], sh[8], mu[8], rs[8], dz[8];
+    float sc[8], sh[8], mu[8], rs[8], dz[8], vsc[8], vsh[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       mu[e] = s_st[0][c0 + e]; rs[e] = s_st[1][c0 + e];
       sc[e] = s_st[2][c0 + e]; sh[e] = s_st[3][c0 + e];
+      vsc[e] = s_vr[0][c0 + e]; vsh[e] = s_vr[1][c0 + e];
     }
-    bwd_dz8(a, v, sc, sh, dz);
+    bwd_dz8(a, v, sc, sh, dz, vsc, vsh);
     const uint32_t yw[4] = {v.y.x, v.y.y, v.y.z, v.y.w};
     uint32_t go[4], ro[4];
 #pragma unroll
@@ -1110,18 +1152,32 @@ MDA_API int mda_bn_stats_acc(const void* y, int64_t M, int64_t C, void* region, 
   MDA_CHECK_LAUNCH();
 }
 
+MDA_API int mda_bn_apply_fin_vr(const void* y, void* region, int64_t M, int64_t C, const float* gamma,
+                                const float* beta, float* running_mean, float* running_var,
+                                float* stats, float momentum, float eps, int64_t* nbt,
+                                const void* res, void* out, void* preact, int64_t act,
+                                void* rregion, const float* rgamma, const float* rbeta,
+                                float* rrunning_mean, float* rrunning_var, float* rstats,
+                                float rmomentum, float reps, int64_t* rnbt, hipStream_t st) {
+  if (C % 8 || C > SLOT_CMAX || M <= 0 || M >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
+  if (rregion != nullptr && (res == nullptr || rstats == nullptr)) return (int)hipErrorInvalidValue;
+  FinArgs f{gamma, beta, running_mean, running_var, stats, momentum, eps, nbt};
+  FinArgs rf{rgamma, rbeta, rrunning_mean, rrunning_var, rstats, rmomentum, reps, rnbt};
+  const int nb = apply_blocks(M * C / 8, APPLY_V);
+  hipLaunchKernelGGL(bn_apply_fin_kernel, dim3(nb), dim3(256), 0, st, (const bf16_t*)y,
+                     (BnRegion*)region, M, (int)C, f, (const bf16_t*)res, (bf16_t*)out,
+                     (bf16_t*)preact, (int)act, (BnRegion*)rregion, rf);
+  MDA_CHECK_LAUNCH();
+}
+
 MDA_API int mda_bn_apply_fin(const void* y, void* region, int64_t M, int64_t C, const float* gamma,
                              const float* beta, float* running_mean, float* running_var,
                              float* stats, float momentum, float eps, int64_t* nbt,
                              const void* res, void* out, void* preact, int64_t act,
                              hipStream_t st) {
-  if (C % 8 || C > SLOT_CMAX || M <= 0 || M >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
-  FinArgs f{gamma, beta, running_mean, running_var, stats, momentum, eps, nbt};
-  const int nb = apply_blocks(M * C / 8, APPLY_V);
-  hipLaunchKernelGGL(bn_apply_fin_kernel, dim3(nb), dim3(256), 0, st, (const bf16_t*)y,
-                     (BnRegion*)region, M, (int)C, f, (const bf16_t*)res, (bf16_t*)out,
-                     (bf16_t*)preact, (int)act);
-  MDA_CHECK_LAUNCH();
+  return mda_bn_apply_fin_vr(y, region, M, C, gamma, beta, running_mean, running_var, stats, momentum,
+                             eps, nbt, res, out, preact, act, nullptr, nullptr, nullptr, nullptr,
+                             nullptr, nullptr, 0.f, 0.f, nullptr, st);
 }
 
 // Fused BN backward (one launch) on a fresh (zeroed) region.  dout2
@@ -1132,7 +1188,8 @@ MDA_API int mda_bn_bwd_fused(const void* dout, const void* dout2, const void* dp
                              const void* res, const float* stats, int64_t M, int64_t C,
                              int64_t act, void* region, void* err, void* dy, void* dres,
                              float* dgamma, float* dbeta, float* sums, const void* ry,
-                             const float* rstats, void* rregion, hipStream_t st) {
+                             const float* rstats, void* rregion, const float* vres,
+                             hipStream_t st) {
   if (C % 8 || C > SLOT_CMAX || M <= 0 || M >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
   if (rregion != nullptr && (dres == nullptr || ry == nullptr || rstats == nullptr ||
                              256 % (C / 8) != 0))
@@ -1140,7 +1197,7 @@ MDA_API int mda_bn_bwd_fused(const void* dout, const void* dout2, const void* dp
   BwdArgs a{(const bf16_t*)dout, (const bf16_t*)dout2, (const bf16_t*)dpre, (const bf16_t*)y,
             (const bf16_t*)res, stats, (bf16_t*)dy, (bf16_t*)dres, dgamma, dbeta, sums,
             (BnRegion*)region, (unsigned*)err, (int)M, (int)C, (int)act, (const bf16_t*)ry,
-            rstats, (BnRegion*)rregion};
+            rstats, (BnRegion*)rregion, vres};
   const int C8 = (int)C / 8;
   const int rpi = 256 / C8;
   const int64_t rows_iter = (M + rpi - 1) / rpi;       // block-iterations of work
@@ -1171,12 +1228,12 @@ MDA_API int mda_bn_bwd_apply_reg(const void* dout, const void* dpre, const void*
                                  const float* stats, int64_t M, int64_t C, int64_t act,
                                  void* region, void* dy, void* dres, float* dgamma, float* dbeta,
                                  float* sums, const void* ry, const float* rstats, void* rregion,
-                                 hipStream_t st) {
+                                 const float* vres, hipStream_t st) {
   if (C % 8 || C > SLOT_CMAX || M <= 0 || M >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
   BwdArgs a{(const bf16_t*)dout, nullptr, (const bf16_t*)dpre, (const bf16_t*)y,
             (const bf16_t*)res, stats, (bf16_t*)dy, (bf16_t*)dres, dgamma, dbeta, sums,
             (BnRegion*)region, nullptr, (int)M, (int)C, (int)act, (const bf16_t*)ry, rstats,
-            (BnRegion*)rregion};
+            (BnRegion*)rregion, vres};
   const int nb = apply_blocks(M * C / 8, APPLY_V);
   if (rregion != nullptr && (dres == nullptr || ry == nullptr || rstats == nullptr ||
                              256 % (C / 8) != 0))

@@ -88,6 +88,9 @@ struct ConvParams {
   const float* bnb_stats;
   BnRegion* bnb_slot;
   int bnb_act;
+  // optional: bnb_res is the RAW input of another training BN applied inside
+  // this layer's apply (mda_bn_apply_fin_vr): residual = res*vres[2C+c] + vres[3C+c]
+  const float* bnb_vres;
   // grouped conv (glds kernel only): Cin above is the channels of ONE group,
   // x rows hold ldx channels, each group owns cout_g consecutive output
   // channels, and a block's N tile never leaves its group (grid.y = groups x
@@ -323,13 +326,15 @@ __device__ __forceinline__ void conv_epilogue_bnb(const ConvParams& p, float* Cs
   const int mlim = has_pc ? pc.Mc : p.M;
   const bool cok = co < group_nlim(p, n0);
   const bool zres = p.bnb_res != nullptr && p.bnb_act != ACT_NONE;
-  float mu[8], rs[8], sc[8], sh[8];
+  float mu[8], rs[8], sc[8], sh[8], vsc[8], vsh[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     mu[e] = cok ? p.bnb_stats[co + e] : 0.f;
     rs[e] = cok ? p.bnb_stats[C + co + e] : 0.f;
     sc[e] = cok ? p.bnb_stats[2 * C + co + e] : 0.f;
     sh[e] = cok ? p.bnb_stats[3 * C + co + e] : 0.f;
+    vsc[e] = (cok && p.bnb_vres) ? p.bnb_vres[2 * C + co + e] : 1.f;
+    vsh[e] = (cok && p.bnb_vres) ? p.bnb_vres[3 * C + co + e] : 0.f;
   }
   uint4 yv[RPT], rv[RPT], gv[RPT];
   int mrow[RPT];
@@ -371,7 +376,7 @@ __device__ __forceinline__ void conv_epilogue_bnb(const ConvParams& p, float* Cs
         const float yf = h ? __uint_as_float(yw[w] & 0xffff0000u) : __uint_as_float(yw[w] << 16);
         if (p.bnb_act != ACT_NONE) {
           float z = yf * sc[e] + sh[e];
-          if (zres) z += h ? __uint_as_float(rw[w] & 0xffff0000u) : __uint_as_float(rw[w] << 16);
+          if (zres) z += (h ? __uint_as_float(rw[w] & 0xffff0000u) : __uint_as_float(rw[w] << 16)) * vsc[e] + vsh[e];
           d *= bnb_act_grad(z, p.bnb_act);
         }
         s1[e] += d;
@@ -1959,7 +1964,7 @@ MDA_API int mda_conv_dgrad_bnsum_g(const void* dy, const void* wt, void* dx, flo
                                    int64_t stride, int64_t pad, int64_t Kp, int64_t tile,
                                    int64_t splits, const void* bn_y, const void* bn_res,
                                    const float* bn_stats, int64_t bn_act, void* region,
-                                   int64_t groups, hipStream_t st);
+                                   int64_t groups, const float* bn_vres, hipStream_t st);
 
 MDA_API int mda_conv_dgrad(const void* dy, const void* wt, void* dx, float* partial, int64_t N,
                            int64_t H, int64_t W, int64_t Cin, int64_t Ho, int64_t Wo,
@@ -1996,7 +2001,7 @@ MDA_API int mda_conv_dgrad_bnsum(const void* dy, const void* wt, void* dx, float
                                  hipStream_t st) {
   return mda_conv_dgrad_bnsum_g(dy, wt, dx, partial, res, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
                                 stride, pad, Kp, tile, splits, bn_y, bn_res, bn_stats, bn_act,
-                                region, 1, st);
+                                region, 1, nullptr, st);
 }
 
 // Grouped dgrad (groups > 1): dx[.., g*Cin/G + ci] sums only group g's output
@@ -2008,7 +2013,7 @@ MDA_API int mda_conv_dgrad_bnsum_g(const void* dy, const void* wt, void* dx, flo
                                    int64_t stride, int64_t pad, int64_t Kp, int64_t tile,
                                    int64_t splits, const void* bn_y, const void* bn_res,
                                    const float* bn_stats, int64_t bn_act, void* region,
-                                   int64_t groups, hipStream_t st) {
+                                   int64_t groups, const float* bn_vres, hipStream_t st) {
   if (Cout % 8 || groups < 1 || Cin % groups || Cout % groups) return (int)hipErrorInvalidValue;
   if (region != nullptr && (splits != 1 || Cin % 8 || Cin > SLOT_CMAX || bn_y == nullptr ||
                             bn_stats == nullptr))
@@ -2019,6 +2024,7 @@ MDA_API int mda_conv_dgrad_bnsum_g(const void* dy, const void* wt, void* dx, flo
   p.bnb_stats = bn_stats;
   p.bnb_slot = (BnRegion*)region;
   p.bnb_act = (int)bn_act;
+  p.bnb_vres = bn_res != nullptr ? bn_vres : nullptr;
   p.x = (const bf16_t*)dy; p.w = (const bf16_t*)wt; p.scale = nullptr; p.bias = nullptr;
   p.res = (const bf16_t*)res; p.y = (bf16_t*)dx; p.preact = nullptr; p.partial = partial;
   // GEMM view: rows = dx pixels, cols = Cin, k = (tap, co); "input" image = dy

@@ -20,6 +20,7 @@
 // optional BN-backward sums of the pooled map's producer (pool_fc_bwd_kernel)
 struct HeadBn {
   const bf16_t* y; const bf16_t* res; const float* stats; BnRegion* reg; int act;
+  const float* vres;  // res is a virtual residual (see BwdArgs::vres in bn.hip)
 };
 
 namespace {
@@ -144,7 +145,10 @@ pool_fc_bwd_kernel(const T* __restrict__ dl, const T* __restrict__ dpooled,
   }
   // ---- dx[n, p, :] = (dpooled[n, :] + dl[n, :] @ W) / HW   for every p
   const int n = blockIdx.x - J;
-  for (int j = threadIdx.x; j < J; j += blockDim.x) sh[j] = io<T>::ld(dl, (int64_t)n * J + j);
+  float* sdl = sh;                                   // [J]
+  float* sv = sh + (N > J ? N : J);                  // [C] the stored (rounded) dx value
+  float* sred = sv + C;                              // [2][P][C] BN partials
+  for (int j = threadIdx.x; j < J; j += blockDim.x) sdl[j] = io<T>::ld(dl, (int64_t)n * J + j);
   __syncthreads();
   T* dxn = dx + (int64_t)n * HW * C;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
@@ -152,16 +156,91 @@ pool_fc_bwd_kernel(const T* __restrict__ dl, const T* __restrict__ dpooled,
     int j = 0;
     for (; j + 8 <= J; j += 8)
 #pragma unroll
-      for (int u = 0; u < 8; ++u) a[u] += sh[j + u] * W[(int64_t)(j + u) * C + c];
-    for (; j < J; ++j) a[0] += sh[j] * W[(int64_t)j * C + c];
+      for (int u = 0; u < 8; ++u) a[u] += sdl[j + u] * W[(int64_t)(j + u) * C + c];
+    for (; j < J; ++j) a[0] += sdl[j] * W[(int64_t)j * C + c];
     const float acc = (dpooled ? io<T>::ld(dpooled, (int64_t)n * C + c) : 0.f) +
                       (((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7])));
-    const float v = acc * inv_hw;
+    T r;
+    io<T>::st(&r, 0, acc * inv_hw);
+    sv[c] = io<T>::ld(&r, 0);
+  }
+  __syncthreads();
+  const int CG = C / 8;
+  if (sizeof(T) == 2 && (C & 7) == 0 && CG <= 256) {
+    // 8 channels x a pixel group per thread: 16-byte dx stores and BN-input
+    // loads (one scalar channel per thread walking all pixels took 39 us for
+    // the 8x8x256 head of ResNet8x4)
+    const int P = 256 / CG;
+    const int cg = threadIdx.x % CG, pg = threadIdx.x / CG;
+    const int c0 = cg * 8;
+    float s1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, s2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (pg < P) {
+      float d[8];
+      uint32_t dw[4];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d[e] = sv[c0 + e];
+#pragma unroll
+      for (int w = 0; w < 4; ++w) dw[w] = pack_bf16x2(d[2 * w], d[2 * w + 1]);
+      const uint4 dv = make_uint4(dw[0], dw[1], dw[2], dw[3]);
+      float mu[8], rs[8], sc[8], sf[8], vsc[8], vsh[8];
+      if (bn.reg != nullptr) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          mu[e] = bn.stats[c0 + e]; rs[e] = bn.stats[C + c0 + e];
+          sc[e] = bn.stats[2 * C + c0 + e]; sf[e] = bn.stats[3 * C + c0 + e];
+          vsc[e] = bn.vres ? bn.vres[2 * C + c0 + e] : 1.f;
+          vsh[e] = bn.vres ? bn.vres[3 * C + c0 + e] : 0.f;
+        }
+      }
+      const bf16_t* yn = bn.y ? bn.y + (int64_t)n * HW * C : nullptr;
+      const bf16_t* rn = bn.res ? bn.res + (int64_t)n * HW * C : nullptr;
+      for (int p = pg; p < HW; p += P) {
+        const int64_t o = (int64_t)p * C + c0;
+        *(uint4*)(dxn + o) = dv;
+        if (bn.reg != nullptr) {
+          const uint4 yv = *(const uint4*)(yn + o);
+          const uint4 rv = rn ? *(const uint4*)(rn + o) : make_uint4(0u, 0u, 0u, 0u);
+          const uint32_t yw[4] = {yv.x, yv.y, yv.z, yv.w}, rw[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const uint32_t u = yw[e >> 1], q = rw[e >> 1];
+            const float yf = (e & 1) ? __uint_as_float(u & 0xffff0000u) : __uint_as_float(u << 16);
+            float z = yf * sc[e] + sf[e];
+            if (rn) z += ((e & 1) ? __uint_as_float(q & 0xffff0000u) : __uint_as_float(q << 16)) * vsc[e] + vsh[e];
+            const float g = bn.act == 1 ? (z > 0.f ? d[e] : 0.f)
+                            : bn.act == 2 ? ((z > 0.f && z < 6.f) ? d[e] : 0.f) : d[e];
+            s1[e] += g;
+            s2[e] += g * ((yf - mu[e]) * rs[e]);
+          }
+        }
+      }
+    }
+    if (bn.reg == nullptr) return;
+    const int PP = 256 / CG;
+    if (pg < PP) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        sred[(0 * PP + pg) * C + c0 + e] = s1[e];
+        sred[(1 * PP + pg) * C + c0 + e] = s2[e];
+      }
+    }
+    __syncthreads();
+    const int shard = n % slot_shards(C);
+    for (int t = threadIdx.x; t < 2 * C; t += blockDim.x) {
+      const int q = t / C, c = t - q * C;
+      float a = 0.f;
+      for (int r = 0; r < PP; ++r) a += sred[(q * PP + r) * C + c];
+      acc_add(region_acc(bn.reg, C, shard, q) + c, (double)a);
+    }
+    return;
+  }
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const float v = sv[c];
     for (int p = 0; p < HW; ++p) io<T>::st(dxn, (int64_t)p * C + c, v);
     if (bn.reg != nullptr) {
       // dx is the whole output gradient of the training BN that produced the
       // pooled map: its sum dz / sum dz*xhat over this sample's pixels
-      const float d = io<T>::ld(dxn, c);  // the stored (rounded) value
+      const float d = v;  // the stored (rounded) value
       const float mu = bn.stats[c], rs = bn.stats[C + c], sc = bn.stats[2 * C + c],
                   shf = bn.stats[3 * C + c];
       float s1 = 0.f, s2 = 0.f;
@@ -170,7 +249,8 @@ pool_fc_bwd_kernel(const T* __restrict__ dl, const T* __restrict__ dpooled,
       for (int p = 0; p < HW; ++p) {
         const float yv = bf2f(yn[(int64_t)p * C + c]);
         float z = yv * sc + shf;
-        if (rn) z += bf2f(rn[(int64_t)p * C + c]);
+        if (rn) z += bn.vres ? bf2f(rn[(int64_t)p * C + c]) * bn.vres[2 * C + c] + bn.vres[3 * C + c]
+                             : bf2f(rn[(int64_t)p * C + c]);
         const float g = bn.act == 1 ? (z > 0.f ? d : 0.f)
                         : bn.act == 2 ? ((z > 0.f && z < 6.f) ? d : 0.f) : d;
         s1 += g;
@@ -369,13 +449,13 @@ MDA_API int mda_pool_fc_bwd_bn(int64_t dt, const void* dl, const void* dpooled, 
                                const float* W, float* dW, float* db, void* dx, int64_t N,
                                int64_t HW, int64_t C, int64_t J, int64_t accum, const void* bn_y,
                                const void* bn_res, const float* bn_stats, int64_t bn_act,
-                               void* bn_region, hipStream_t st);
+                               void* bn_region, const float* bn_vres, hipStream_t st);
 
 MDA_API int mda_pool_fc_bwd(int64_t dt, const void* dl, const void* dpooled, const void* pooled,
                             const float* W, float* dW, float* db, void* dx, int64_t N, int64_t HW,
                             int64_t C, int64_t J, int64_t accum, hipStream_t st) {
   return mda_pool_fc_bwd_bn(dt, dl, dpooled, pooled, W, dW, db, dx, N, HW, C, J, accum, nullptr,
-                            nullptr, nullptr, 0, nullptr, st);
+                            nullptr, nullptr, 0, nullptr, nullptr, st);
 }
 
 // mda_pool_fc_bwd that also adds the BN backward sums of the layer whose
@@ -386,9 +466,10 @@ MDA_API int mda_pool_fc_bwd_bn(int64_t dt, const void* dl, const void* dpooled, 
                                const float* W, float* dW, float* db, void* dx, int64_t N,
                                int64_t HW, int64_t C, int64_t J, int64_t accum, const void* bn_y,
                                const void* bn_res, const float* bn_stats, int64_t bn_act,
-                               void* bn_region, hipStream_t st) {
+                               void* bn_region, const float* bn_vres, hipStream_t st) {
   if (N <= 0 || C <= 0 || J <= 0 || N > 16384 || J > 16384) return (int)hipErrorInvalidValue;
-  HeadBn bn{(const bf16_t*)bn_y, (const bf16_t*)bn_res, bn_stats, (BnRegion*)bn_region, (int)bn_act};
+  HeadBn bn{(const bf16_t*)bn_y, (const bf16_t*)bn_res, bn_stats, (BnRegion*)bn_region, (int)bn_act,
+            bn_res != nullptr ? bn_vres : nullptr};
   if (bn_region != nullptr && (dt == DT_F32 || (int64_t)J * C > (1 << 16) || C > SLOT_CMAX))
     return (int)hipErrorInvalidValue;
   if ((int64_t)J * C > (1 << 16)) {  // large head: tiled GEMM blocks
@@ -406,7 +487,10 @@ MDA_API int mda_pool_fc_bwd_bn(int64_t dt, const void* dl, const void* dpooled, 
                          nW);
     MDA_CHECK_LAUNCH();
   }
-  const size_t lds = (size_t)(N > J ? N : J) * sizeof(float);
+  // [max(N, J)] dl column / row + [C] dx values + [2][256 / (C/8)][C] BN partials
+  const int64_t pp = (C % 8 == 0 && C / 8 <= 256) ? 256 / (C / 8) : 0;
+  const size_t lds = (size_t)((N > J ? N : J) + C + 2 * pp * C) * sizeof(float);
+  if (lds > 64 * 1024) return (int)hipErrorInvalidValue;
   const dim3 grid((unsigned)(J + N));
   if (dt == DT_F32)
     hipLaunchKernelGGL(pool_fc_bwd_kernel<float>, grid, dim3(256), lds, st, (const float*)dl,

@@ -262,10 +262,11 @@ class BnLink:
     accumulates into it in place.
     """
 
-    __slots__ = ("y", "res", "stats", "act", "M", "C", "dout", "ver", "region")
+    __slots__ = ("y", "res", "stats", "act", "M", "C", "dout", "ver", "region", "vres")
 
-    def __init__(self, y, res, stats, act, M, C):
+    def __init__(self, y, res, stats, act, M, C, vres=None):
         self.y, self.res, self.stats, self.act, self.M, self.C = y, res, stats, act, M, C
+        self.vres = vres if res is not None else None  # res is a virtual residual (VirtualBN)
         self.dout = self.region = None
         self.ver = -1
 
@@ -284,6 +285,7 @@ class BnLink:
 
 
 _BNB_COUNT = [0, 0]  # BN backwards on dgrad-epilogue sums / armed links that fell back
+_LAST_VBN = [None]
 _BNB_ON = [os.environ.get("MDA_BN_DGRAD_SUMS", "1") != "0"]
 _LAST_LINK = [None]
 
@@ -302,7 +304,7 @@ def bn_dgrad_sums_count(reset: bool = False):
 
 
 def _bn_bwd(dout, dpre, y, res, stats, gamma, beta, M, C, act, need_res, direct_gb, link=None,
-            res_link=None):
+            res_link=None, vres=None):
     """BN (+ residual) (+ activation) backward -> (dy, dres or None, sums or
     None).  Fused: ONE grid-barrier launch (mda_bn_bwd_fused); else the
     partial-rows reduce + finalize + apply (3 launches).  dgamma / dbeta are
@@ -323,17 +325,19 @@ def _bn_bwd(dout, dpre, y, res, stats, gamma, beta, M, C, act, need_res, direct_
     if reg is not None and dpre is None:
         sums = None if direct_gb else torch.empty(2, C, dtype=torch.float32, device=dev)
         _ext.call("mda_bn_bwd_apply_reg", dout, None, y, res, stats, M, C, act, reg, dy, dres,
-                  dg, db, sums, ry, rst, rreg)
+                  dg, db, sums, ry, rst, rreg, vres)
         if rl is not None:
             rl.arm(dres, rreg)
         return dy, dres, sums
     if _BN_FUSED[0]:
         sums = None if direct_gb else torch.empty(2, C, dtype=torch.float32, device=dev)
         _ext.call("mda_bn_bwd_fused", dout, None, dpre, y, res, stats, M, C, act, _region(C, dev),
-                  _err_word(dev), dy, dres, dg, db, sums, ry, rst, rreg)
+                  _err_word(dev), dy, dres, dg, db, sums, ry, rst, rreg, vres)
         if rl is not None:
             rl.arm(dres, rreg)
         return dy, dres, sums
+    if vres is not None:
+        raise RuntimeError("virtual residuals need the fused BN kernels (MDA_BN_FUSED=1)")
     sums = torch.empty(2, C, dtype=torch.float32, device=dev)
     _bn_bwd_reduce(dout, dpre, y, res, stats, M, C, act, ws, sums, dg, db)
     _ext.call("mda_bn_bwd_apply", dout, dpre, y, res, stats[2], stats[3], stats[0], stats[1],
@@ -655,10 +659,46 @@ def _fork_sum(fork, g):
     return g if other is None else g + other
 
 
+class VirtualBN:
+    """A training conv + BN whose apply pass was folded into its consumer's.
+
+    A projection shortcut's BN has no activation and its only consumer is the
+    block's last apply (``act(bn2(y2) + bn_sc(y_sc))``): the shortcut conv
+    only accumulates its batch sums (``region``), its autograd output is the
+    RAW conv output ``y_sc``, and the consumer's ``mda_bn_apply_fin_vr``
+    finalizes both BNs and adds ``y_sc * scale_sc + shift_sc`` -- one apply
+    launch per downsampling block instead of two.  Every later pass that
+    recomputes the block's pre-activation (the BN backward, the consumer
+    dgrad's BN-sum epilogue, the pool+FC head) gets the shortcut's [4][C]
+    stats as ``vres`` and applies the same affine to the raw residual.
+    """
+
+    __slots__ = ("reg", "gamma", "beta", "bn", "stats")
+
+    def __init__(self, reg, gamma, beta, bn, stats):
+        self.reg, self.gamma, self.beta, self.bn, self.stats = reg, gamma, beta, bn, stats
+
+
+_VRES_ON = [os.environ.get("MDA_VIRTUAL_RES", "1") != "0"]
+
+
+def set_virtual_residual(on: bool) -> None:
+    """Projection-shortcut BN applied inside the block's last apply (VirtualBN) on / off (A/B)."""
+    _VRES_ON[0] = bool(on)
+
+
+def can_defer_residual(h, conv, bn) -> bool:
+    """The block's residual consumer (conv ``conv`` + ``bn`` on input ``h``)
+    runs on the native training kernels, so a projection shortcut may hand it
+    a :class:`VirtualBN` output."""
+    return (_VRES_ON[0] and _BN_FUSED[0] and h is not None and h.is_cuda and conv.groups == 1
+            and train_supported(h, conv, bn))
+
+
 class _ConvBNActTrain(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, gamma, beta, residual, meta, bn, want_preact, forks=(None, None),
-                cbias=None):
+                cbias=None, defer=False):
         # an unused output (the pre-activation) must not be materialised as a
         # zero gradient + layout copy: the kernels take null dout / dpre
         ctx.set_materialize_grads(False)
@@ -732,7 +772,13 @@ class _ConvBNActTrain(torch.autograd.Function):
         ws = _ws(dev)
         stats = torch.empty(4, Cout, dtype=torch.float32, device=dev)  # mean, rstd, scale, shift
         res = _cl_bf16(residual) if residual is not None else None
-        out = torch.empty_like(y)
+        rv = getattr(residual, "_mda_vbn", None) if residual is not None else None
+        if rv is not None and res is not residual:
+            raise RuntimeError("a virtual residual must reach its consumer unchanged (bf16 NHWC)")
+        defer = bool(defer) and (_BN_FUSED[0] or gc) and act == 0 and residual is None \
+            and not want_preact and G == 1
+        ctx.vbn = None
+        out = y if defer else torch.empty_like(y)
         pre = torch.empty_like(y) if want_preact else None
         if _BN_FUSED[0] or gc:
             # conv whose epilogue adds the BN sums into the stream's slot, then
@@ -740,10 +786,22 @@ class _ConvBNActTrain(torch.autograd.Function):
             reg = _region(Cout, dev)
             _ext.call("mda_conv_fwd_bnacc_g", x, wf, y, part, reg, N, H, W, Cin, Ho, Wo, Cout,
                       KH, KW, stride, pad, Kp, tile, splits, G if gc else 1)
-            _ext.call("mda_bn_apply_fin", y, reg, M, Cout, gamma.detach(), beta.detach(),
-                      bn.running_mean, bn.running_var, stats, float(bn.momentum), float(bn.eps),
-                      bn.num_batches_tracked, res, out, pre, act)
+            if defer:
+                # no apply: the consumer's apply finalizes this BN (VirtualBN)
+                ctx.vbn = VirtualBN(reg, gamma.detach(), beta.detach(), bn, stats)
+            elif rv is not None:
+                _ext.call("mda_bn_apply_fin_vr", y, reg, M, Cout, gamma.detach(), beta.detach(),
+                          bn.running_mean, bn.running_var, stats, float(bn.momentum),
+                          float(bn.eps), bn.num_batches_tracked, res, out, pre, act, rv.reg,
+                          rv.gamma, rv.beta, rv.bn.running_mean, rv.bn.running_var, rv.stats,
+                          float(rv.bn.momentum), float(rv.bn.eps), rv.bn.num_batches_tracked)
+            else:
+                _ext.call("mda_bn_apply_fin", y, reg, M, Cout, gamma.detach(), beta.detach(),
+                          bn.running_mean, bn.running_var, stats, float(bn.momentum), float(bn.eps),
+                          bn.num_batches_tracked, res, out, pre, act)
         else:
+            if rv is not None:
+                raise RuntimeError("virtual residuals need the fused BN kernels (MDA_BN_FUSED=1)")
             # conv whose epilogue emits the BN statistics partials + finalize (2 launches)
             _ext.call("mda_conv_fwd_bnstats", x, wf, y, part, ws.partial, ws.partial.numel(), N, H,
                       W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, Kp, tile, splits, gamma.detach(),
@@ -753,6 +811,7 @@ class _ConvBNActTrain(torch.autograd.Function):
             _ext.call("mda_bn_apply", y, stats[2], stats[3], res, out, pre, M, Cout, act)
         ctx.save_for_backward(x, wt, weight, gamma, beta, y, res, stats)
         ctx.meta = (N, Cin, H, W, Cout, Ho, Wo, KH, KW, stride, pad, Kp, KpT, act)
+        ctx.vres = rv.stats if rv is not None else None
         ctx.gc = gc
         ctx.has_res = residual is not None
         ctx.link_in = link_in if (link_in is not None and link_in.C == Cin
@@ -766,8 +825,9 @@ class _ConvBNActTrain(torch.autograd.Function):
         # output: its gradient would join dz after the consumer's epilogue)
         ctx.bnlink = None
         if not want_preact and Cout <= 2048:
-            ctx.bnlink = BnLink(y, res if act != 0 else None, stats, act, M, Cout)
+            ctx.bnlink = BnLink(y, res if act != 0 else None, stats, act, M, Cout, ctx.vres)
         _LAST_LINK[0] = ctx.bnlink
+        _LAST_VBN[0] = ctx.vbn
         ctx.cbias = cbias is not None
         if cbias is not None:
             # BN(y + b) == BN(y) in training; the running mean tracks mean(y) + b
@@ -790,7 +850,8 @@ class _ConvBNActTrain(torch.autograd.Function):
         direct_gb = gamma.grad is not None and beta.grad is not None
         need_res = ctx.has_res and ctx.needs_input_grad[4]
         dy, dres, sums = _bn_bwd(dout, dpre, y, res, stats, gamma, beta, M, Cout, act, need_res,
-                                 direct_gb, ctx.bnlink, getattr(ctx, "res_link", None))
+                                 direct_gb, ctx.bnlink, getattr(ctx, "res_link", None),
+                                 getattr(ctx, "vres", None))
         x_fork, res_fork = ctx.forks
         if need_res:
             dres = _fork_sum(res_fork, dres)
@@ -810,16 +871,16 @@ class _ConvBNActTrain(torch.autograd.Function):
                           Cout, KH, KW, stride, pad, KpT, tile, splits,
                           link.y if reg is not None else None, link.res if reg is not None else None,
                           link.stats if reg is not None else None, link.act if reg is not None else 0,
-                          reg, ctx.groups)
+                          reg, ctx.groups, link.vres if reg is not None else None)
                 if reg is not None:
                     link.arm(dx, reg)
             elif link is not None and not parks and splits == 1:
                 # dx is the whole output gradient of the BN layer that made x:
                 # its backward sums come out of this epilogue (BnLink)
                 reg = _region(Cin, dev)
-                _ext.call("mda_conv_dgrad_bnsum", dy, wt, dx, part, other, N, H, W, Cin, Ho, Wo,
+                _ext.call("mda_conv_dgrad_bnsum_g", dy, wt, dx, part, other, N, H, W, Cin, Ho, Wo,
                           Cout, KH, KW, stride, pad, KpT, tile, splits, link.y, link.res,
-                          link.stats, link.act, reg)
+                          link.stats, link.act, reg, 1, link.vres)
                 link.arm(dx, reg)
             else:
                 _ext.call("mda_conv_dgrad_res", dy, wt, dx, part, other, N, H, W, Cin, Ho, Wo,
@@ -846,7 +907,7 @@ class _ConvBNActTrain(torch.autograd.Function):
         dbeta = None if direct_gb else sums[0].clone()
         dcb = torch.zeros(Cout, dtype=torch.float32, device=dev) if (
             ctx.cbias and ctx.needs_input_grad[9]) else None
-        return dx, dw, dgamma, dbeta, dres, None, None, None, None, dcb
+        return dx, dw, dgamma, dbeta, dres, None, None, None, None, dcb, None
 
 
 def _bn_train_forward(y, M, C, gamma, beta, bn, residual, act, want_preact, reg=None):
@@ -960,7 +1021,7 @@ def _dw_backward(ctx, dout, dpre):
         dw = None if direct_w else target
         if direct_w:
             notify_grad(weight)
-    return dx, dw, dgamma, dbeta, dres, None, None, None, None, None
+    return dx, dw, dgamma, dbeta, dres, None, None, None, None, None, None
 
 
 def pack_weights(weight, dgrad=True):
@@ -1219,10 +1280,13 @@ def conv_trainbn_nograd(x, conv, bn, act, residual, want_preact):
     return out, pre
 
 
-def conv_bn_act_train(x, conv, bn, act, residual, want_preact, fork=None, res_fork=None):
+def conv_bn_act_train(x, conv, bn, act, residual, want_preact, fork=None, res_fork=None,
+                      defer_apply=False):
     """``fork``: the :class:`GradFork` of ``x`` (another consumer of x sums
     its gradient into this layer's dgrad, or vice versa); ``res_fork``: the
-    fork of ``residual`` (identity shortcut)."""
+    fork of ``residual`` (identity shortcut).  ``defer_apply``: return the raw
+    conv output as a :class:`VirtualBN` (the caller guarantees its one
+    consumer is a native conv + BN that takes it as ``residual``)."""
     meta = (conv.stride[0], conv.padding[0], _ACT[act])
     if is_depthwise(conv):
         meta = meta + ("dw",)
@@ -1232,9 +1296,14 @@ def conv_bn_act_train(x, conv, bn, act, residual, want_preact, fork=None, res_fo
     if residual is None:
         res_fork = None
     _LAST_LINK[0] = None
+    _LAST_VBN[0] = None
     out, pre = _ConvBNActTrain.apply(x, conv.weight, bn.weight, bn.bias, residual, meta, bn,
-                                     bool(want_preact), (fork, res_fork), conv.bias)
+                                     bool(want_preact), (fork, res_fork), conv.bias,
+                                     bool(defer_apply) and conv.bias is None)
     link, _LAST_LINK[0] = _LAST_LINK[0], None
+    vbn, _LAST_VBN[0] = _LAST_VBN[0], None
     if link is not None:
         out._mda_bnlink = link
+    if vbn is not None:
+        out._mda_vbn = vbn
     return out, pre

@@ -57,12 +57,16 @@ def _bn(x: torch.Tensor, bn: nn.BatchNorm2d) -> torch.Tensor:
 
 def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d | None = None,
                 act: str = "relu", residual: torch.Tensor | None = None,
-                want_preact: bool = False, fork=None, res_fork=None):
+                want_preact: bool = False, fork=None, res_fork=None, defer_apply: bool = False):
     """``act(bn(conv(x)) + residual)``; returns ``(out, preact_or_None)``.
 
     ``fork`` / ``res_fork`` (:class:`ops.hip_train.GradFork`, optional): x /
     residual also feed another native layer; their gradients are summed
-    inside the native backward (no autograd add) -- ignored off that path."""
+    inside the native backward (no autograd add) -- ignored off that path.
+    ``defer_apply`` (a projection shortcut, ``act="none"``): on the native
+    training path the BN apply is left to the one consumer, which must be a
+    native conv + BN taking the result as ``residual``
+    (:class:`ops.hip_train.VirtualBN`; see :func:`ops.hip_train.can_defer_residual`)."""
     if hip_enabled_for(x):
         from . import hip_layers
         if hip_layers.conv_supported(x, conv, bn):
@@ -70,7 +74,12 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d | None = No
         from . import hip_train
         if _TRAIN_KERNELS["on"] and hip_train.train_supported(x, conv, bn):
             return hip_train.conv_bn_act_train(x, conv, bn, act, residual, want_preact, fork,
-                                               res_fork)
+                                               res_fork, defer_apply)
+    if residual is not None and getattr(residual, "_mda_vbn", None) is not None:
+        raise RuntimeError("a VirtualBN residual reached a non-native consumer "
+                           "(check ops.hip_train.can_defer_residual at the call site)")
+    if hip_enabled_for(x):
+        from . import hip_train
         if _TRAIN_KERNELS["on"] and bn is None and hip_train.conv_train_supported(x, conv):
             return hip_train.conv_act_train(x, conv, act, residual, want_preact)
         if hip_train.trainbn_nograd_supported(x, conv, bn):
@@ -237,7 +246,7 @@ class _PoolFC(torch.autograd.Function):
             from .hip_train import _region
             reg = _region(C, dev)
             _ext.call("mda_pool_fc_bwd_bn", dt, dlogits, dpooled, pooled, weight.detach(), dw, db,
-                      dx, N, H * W, C, J, 1, link.y, link.res, link.stats, link.act, reg)
+                      dx, N, H * W, C, J, 1, link.y, link.res, link.stats, link.act, reg, link.vres)
             link.arm(dx, reg)
         else:
             _ext.call("mda_pool_fc_bwd", dt, dlogits, dpooled, pooled, weight.detach(), dw, db, dx,

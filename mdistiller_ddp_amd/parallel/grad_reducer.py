@@ -99,6 +99,11 @@ class GradReducer:
         self._hooks = []
         self._armed = False
         self._error = None
+        # captured-backward overlap (DIST.GRAPH_COMM=events, see arm_capture)
+        self._cap = None           # events recorded so far while capturing: [(bucket, event)]
+        self._cap_flush = None     # called before a bucket's event is recorded
+        self.graph_events = None   # [(bucket, event)] of the captured graph, bucket order
+        self._comm = None
         if self.overlap:
             for i, p in enumerate(flat.params):
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
@@ -133,9 +138,12 @@ class GradReducer:
         # strictly in bucket order: every rank issues the same collective
         # sequence even if two buckets complete in a different order
         while self._next < len(self.buckets) and self._pending[self._next] <= 0:
-            self._launch(self._next, async_op=True)
+            if self._cap is not None:
+                self._signal(self._next)
+            else:
+                self._launch(self._next, async_op=True)
+                self.early_launches += 1
             self._next += 1
-            self.early_launches += 1
 
     def ready_param(self, p) -> None:
         i = self._index.get(id(p))
@@ -209,6 +217,81 @@ class GradReducer:
         err, self._error = self._error, None
         if err is not None:
             raise RuntimeError(err)
+
+    # ------------------------------------------------------------------
+    # Overlap under hipGraphs (DIST.GRAPH_COMM=events).  RCCL collectives
+    # captured INSIDE the step graph make it a multi-branch graph, which ROCm's
+    # executor runs slowly (scripts/launch_floor_probe.py); instead the captured
+    # backward records one external event per bucket at the point where the
+    # bucket's last gradient is written, and after launching the replay the
+    # host enqueues, on a comm stream, "wait for bucket k's event, all-reduce
+    # bucket k" for every bucket in order: the all-reduce of the head's
+    # buckets runs while the replay is still computing the stem's gradients.
+    def arm_capture(self, flush=None) -> None:
+        """Call inside the capture, before the backward.  ``flush`` (optional)
+        runs before each bucket's event is recorded (the deferred weight-gradient
+        reductions: their layers' gradients are only final after it)."""
+        if not self.enabled or self._expected is None:
+            raise RuntimeError("GradReducer.arm_capture: needs a calibrated eager step first")
+        self._works = {}
+        self._next = 0
+        self._armed = True
+        self._cap = []
+        self._cap_flush = flush
+        self._pending = [sum(self._expected[i] for i in idx) for (_, _, idx) in self.buckets]
+        _ARMED.append(self)
+
+    def _signal(self, b) -> None:
+        if self._cap_flush is not None:
+            self._cap_flush()
+        ev = torch.cuda.Event(external=True)
+        ev.record()
+        self._cap.append((b, ev))
+
+    def finish_capture(self) -> None:
+        """End of the captured backward: events for the buckets not signalled
+        yet (all their gradients are written by now)."""
+        try:
+            if any(p < 0 for p in self._pending):
+                raise RuntimeError(f"GradReducer: bucket contribution counts went negative "
+                                   f"{self._pending} in the captured backward")
+            while self._next < len(self.buckets):
+                self._signal(self._next)
+                self._next += 1
+            self.graph_events = list(self._cap)
+        finally:
+            self._cap = None
+            self._cap_flush = None
+            self._armed = False
+            if self in _ARMED:
+                _ARMED.remove(self)
+
+    def launch_from_events(self) -> None:
+        """After the replay of a graph captured with :meth:`arm_capture`: every
+        bucket's all-reduce on the comm stream, each behind its event; the
+        caller then runs :meth:`wait_launched` before the optimizer."""
+        if self._comm is None:
+            from ..runtime.streams import _fresh_stream
+            self._comm = _fresh_stream(torch.cuda.current_device())
+        # (no wait on the current stream: that would wait for the whole replay;
+        # each all-reduce waits only for its bucket's event)
+        self._works = {}
+        with torch.cuda.stream(self._comm):
+            for b, ev in self.graph_events:
+                self._comm.wait_event(ev)
+                self._launch(b, async_op=True)
+                self.early_launches += 1
+
+    def wait_launched(self) -> None:
+        cur = torch.cuda.current_stream()
+        if self._comm is not None:
+            cur.wait_stream(self._comm)  # the wire copies / waits enqueued there
+        for b, (work, t, tb) in self._works.items():
+            if work is not None:
+                work.wait()  # the current stream waits for the collective
+            if tb is not None:
+                t.copy_(tb)
+        self._works = {}
 
     def reduce_all(self) -> None:
         """Non-overlapped reduction of the currently bound gradient set."""

@@ -222,6 +222,27 @@ class TeacherFeed:
             else:
                 self._joined = out
 
+    def capture_pipe(self, teacher, graph, pool, stream, autocast):
+        """Capture the teacher forward of :attr:`next_image` as its OWN
+        single-chain graph on ``stream`` (``RUNTIME.TEACHER_GRAPH=split``).
+
+        Its outputs ``T`` live in the graph's private pool; the training step
+        copies them into ``X`` (the buffers the student graph reads) at the
+        start of the next step, in the same launch as its input copies.  A
+        graph with two parallel branches costs ROCm's executor ~2.5 us per
+        kernel and serialised the branches in this process
+        (``scripts/launch_floor_probe.py``); two single-chain graphs on two
+        streams are two hardware queues.  Returns the flat (T, X) lists."""
+        with torch.cuda.stream(stream), torch.no_grad(), autocast():
+            self._keep(teacher(self.next_image))  # warm-up on the stream (handles, caches)
+        torch.cuda.synchronize()
+        with torch.cuda.graph(graph, pool=pool, stream=stream), torch.no_grad(), autocast():
+            T = self._keep(teacher(self.next_image))
+        t_list, x_list = _tensors(T, []), _tensors(self.X, [])
+        if len(t_list) != len(x_list) or any(a.shape != b.shape for a, b in zip(t_list, x_list)):
+            raise RuntimeError("TeacherFeed: pipelined teacher outputs do not match the primed buffers")
+        return t_list, x_list
+
     def commit(self) -> None:
         """Copy a result joined by ``finish(copy=False)`` into ``X``."""
         out = getattr(self, "_joined", None)

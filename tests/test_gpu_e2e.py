@@ -243,9 +243,10 @@ def test_native_bf16_tracks_fp32_over_300_steps(typ):
     assert abs(l_n - l_r) / abs(l_r) < 0.05, curves
 
 
-@pytest.mark.parametrize("typ,trainer", [("DKD", "base"), ("FITNET", "base"), ("REVIEWKD", "base"),
-                                         ("KD", "dot")])
-def test_teacher_lookahead_matches_inline_teacher(typ, trainer):
+@pytest.mark.parametrize("typ,trainer,tgraph", [("DKD", "base", "split"), ("DKD", "base", "fork"),
+                                                 ("FITNET", "base", "split"),
+                                                 ("REVIEWKD", "base", "split"), ("KD", "dot", "split")])
+def test_teacher_lookahead_matches_inline_teacher(typ, trainer, tgraph):
     """The captured step with the teacher look-ahead (teacher of batch t+1 beside
     the student step t, runtime/streams.py::TeacherFeed) trains like the inline
     teacher: same batches, same teacher outputs, same updates.  The native path
@@ -261,6 +262,7 @@ def test_teacher_lookahead_matches_inline_teacher(typ, trainer):
             d = copy.deepcopy(d0)
             c = cfg.clone()
             c.RUNTIME.TEACHER_LOOKAHEAD = "on" if la else "off"
+            c.RUNTIME.TEACHER_GRAPH = tgraph
             d.train()
             st = TrainStep(d, c, "cuda", trainer=trainer, use_graph=True, dtype=torch.bfloat16)
             torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
@@ -273,6 +275,8 @@ def test_teacher_lookahead_matches_inline_teacher(typ, trainer):
                 st.step(b, next_batch=nb)
             torch.cuda.synchronize()
             assert (st._pipe is not None) == la
+            # split: the teacher is its own graph on the teacher stream (not DOT's dual replay)
+            assert (st._tsplit is not None) == (la and tgraph == "split" and trainer != "dot")
             outs.append((st.flat.data.clone(), st.meters.summary(reduce=False)))
     finally:
         torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det

@@ -1,0 +1,104 @@
+"""Projection-shortcut BN applied inside the block's last apply
+(ops/hip_train.py VirtualBN, bn.hip mda_bn_apply_fin_vr): the shortcut conv
+hands its RAW output on, and every pass that needs the block's residual --
+bn2's apply, bn2's backward, the next block's dgrad BN-sum epilogue and the
+pool + FC head's BN sums -- applies the shortcut BN's affine itself.
+
+Checked against the same model with the virtual residual off (every output,
+input gradient, parameter gradient and BN running statistic) and against an
+fp32 PyTorch reference of the whole ResNet8x4 student."""
+import copy
+
+import pytest
+import torch
+import torch.nn as nn
+
+from mdistiller_ddp_amd.ops import hip_train
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+def _run(model, x, g, backend="hip"):
+    from mdistiller_ddp_amd.ops.backend import use_backend
+    xx = x.clone().requires_grad_(True)
+    with use_backend(backend), torch.autocast("cuda", dtype=torch.bfloat16, enabled=backend == "hip"):
+        logits, feats = model(xx if backend == "hip" else xx.float())
+    (logits.float() * g).sum().backward()
+    torch.cuda.synchronize()
+    return logits, xx.grad
+
+
+@pytest.mark.parametrize("name", ["resnet8x4", "resnet20"])
+def test_student_virtual_residual_matches_materialised(name):
+    from mdistiller_ddp_amd.models import cifar_model_dict
+    torch.manual_seed(11)
+    m = cifar_model_dict[name][0](num_classes=100).cuda().to(memory_format=torch.channels_last)
+    m.train()
+    off, ref = copy.deepcopy(m), copy.deepcopy(m)
+    x = torch.randn(64, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    g = torch.randn(64, 100, device="cuda")
+
+    calls = {"n": 0}
+    orig = hip_train.VirtualBN.__init__
+
+    def counting(self, *a):
+        calls["n"] += 1
+        orig(self, *a)
+    hip_train.VirtualBN.__init__ = counting
+    try:
+        out, dx = _run(m, x, g)
+    finally:
+        hip_train.VirtualBN.__init__ = orig
+    n_ds = sum(1 for mod in m.modules() if getattr(mod, "downsample", None) is not None)
+    assert calls["n"] == n_ds > 0, calls  # every projection shortcut went virtual
+
+    hip_train.set_virtual_residual(False)
+    try:
+        out_off, dx_off = _run(off, x, g)
+    finally:
+        hip_train.set_virtual_residual(True)
+    # same kernels and arithmetic up to the residual's rounding (it is no longer
+    # stored in bf16 before the add)
+    assert _rel(out, out_off) < 2e-2
+    assert _rel(dx, dx_off) < 3e-2
+    for (n, p), (_, q) in zip(m.named_parameters(), off.named_parameters()):
+        assert _rel(p.grad, q.grad) < 3e-2, n
+    for (n, b), (_, c) in zip(m.named_buffers(), off.named_buffers()):
+        if b.dtype == torch.int64:
+            assert torch.equal(b, c), n  # num_batches_tracked of the shortcut BN too
+        else:
+            assert _rel(b, c) < 1e-2, n  # running stats of every BN, shortcut BNs included
+
+    # fp32 PyTorch reference of the same student
+    out_r, dx_r = _run(ref, x, g, backend="torch")
+    assert _rel(out, out_r) < 5e-2
+    assert _rel(dx, dx_r) < 8e-2
+    for (n, p), (_, q) in zip(m.named_parameters(), ref.named_parameters()):
+        assert _rel(p.grad, q.grad) < 8e-2, n
+    for (n, b), (_, c) in zip(m.named_buffers(), ref.named_buffers()):
+        if b.dtype != torch.int64:
+            assert _rel(b, c) < 2e-2, n
+
+
+def test_virtual_residual_refuses_a_non_native_consumer():
+    """A VirtualBN output must never reach a PyTorch consumer silently."""
+    from mdistiller_ddp_amd.ops.backend import use_backend
+    from mdistiller_ddp_amd.ops.nn import conv_bn_act
+    torch.manual_seed(3)
+    c1 = nn.Conv2d(64, 128, 1, 2, bias=False).cuda()
+    b1 = nn.BatchNorm2d(128).cuda()
+    c2 = nn.Conv2d(128, 128, 3, 1, 2, dilation=2, bias=False).cuda()  # not a native consumer
+    b2 = nn.BatchNorm2d(128).cuda()
+    x = torch.randn(8, 64, 16, 16, device="cuda").to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last).requires_grad_(True)
+    with use_backend("hip"), torch.autocast("cuda", dtype=torch.bfloat16):
+        r, _ = conv_bn_act(x, c1, b1, "none", defer_apply=True)
+        assert getattr(r, "_mda_vbn", None) is not None
+        h = torch.randn(8, 128, 8, 8, device="cuda").to(torch.bfloat16).contiguous(
+            memory_format=torch.channels_last)
+        with pytest.raises(RuntimeError):
+            conv_bn_act(h, c2, b2, "relu", residual=r)

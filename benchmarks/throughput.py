@@ -43,6 +43,11 @@ CONFIGS = {
     "dkd_cifar_vgg13_mv2": ("configs/cifar100/dkd/vgg13_mv2.yaml", 64, [], None),
     "reviewkd_imagenet_r34_r18": ("configs/imagenet/r34_r18/reviewkd.yaml", 32, [], None),
     "dkd_imagenet_r50_mv1": ("configs/imagenet/r50_mv1/dkd.yaml", 64, [], None),
+    # the DOT configurations of the reference README (BASELINE.md accuracy table)
+    "dot_cifar_vgg13_vgg8": ("configs/cifar100/dot/vgg13_vgg8.yaml", 64, [], None),
+    "dot_cifar_res32x4_shuv2": ("configs/cifar100/dot/res32x4_shuv2.yaml", 64, [], None),
+    "dot_tiny_r18_mv2": ("configs/tiny_imagenet/dot/r18_mv2.yaml", 256, [], None),
+    "dot_tiny_r18_shuv2": ("configs/tiny_imagenet/dot/r18_shuv2.yaml", 256, [], None),
 }
 
 

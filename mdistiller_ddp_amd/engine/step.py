@@ -229,6 +229,8 @@ class TrainStep:
         self._wg_auto = False
         self._wg_stream = None
         self.wgrad_defer = self.device.type == "cuda" and bool(cfg.RUNTIME.get("WGRAD_DEFER", True))
+        self.wgrad_xgraph = int(cfg.RUNTIME.get("WGRAD_XGRAPH", 0)) if self.device.type == "cuda" else 0
+        self._wgraph = None     # (wgrad graph, its stream, queued launches) of the two-graph backward
 
     def _graph_comm_mode(self, cfg):
         """How the gradient all-reduce meets the captured step at world > 1.
@@ -240,7 +242,7 @@ class TrainStep:
         its bucket's event, so they overlap the rest of the backward
         (GradReducer.arm_capture).  ``True`` (capture): the all-reduce inside
         the single step graph (a multi-branch graph, slow on ROCm's executor).
-        ``auto`` = events with RCCL, split otherwise (gloo reduces on the host).
+        ``auto`` = split.
         """
         if self.world <= 1 or not self.use_graph:
             return False
@@ -251,9 +253,9 @@ class TrainStep:
             if not rccl:
                 raise ValueError("DIST.GRAPH_COMM=capture needs the RCCL (nccl) backend")
             return True
-        if mode == "events" or (mode == "auto" and rccl):
+        if mode == "events":
             return "events"
-        return False  # split
+        return False  # split (auto: events only once validated on a multi-GPU node)
 
     # ------------------------------------------------------------------
     def set_epoch(self, epoch: float) -> None:
@@ -328,6 +330,7 @@ class TrainStep:
                     # a bucket's deferred weight-gradient reductions are flushed
                     # before its event, so the event marks final gradients
                     self.reducer.arm_capture(hip_train.flush_wgrad_reduces if deferred else None)
+                    events = "armed"
                 elif overlap_comm:
                     self.reducer.arm()
                 # backward of the loss terms with unit seeds straight into each term
@@ -335,11 +338,15 @@ class TrainStep:
                 terms = [v for v in losses.values() if v.requires_grad]
                 if terms:
                     torch.autograd.backward(terms, [self._unit(v) for v in terms])
+        except BaseException:
+            if events == "armed":
+                self.reducer.abort_capture()
+            raise
         finally:
             self._flush_wgrad_defer(deferred)
             self._join_wgrad_stream(armed)
             join_branches()
-        if events:
+        if events == "armed":
             self.reducer.finish_capture()
         self._post_backward()
         feed = self.distiller.__dict__.get("_teacher_feed")
@@ -571,6 +578,8 @@ class TrainStep:
 
     def _capture_step(self, static, pool, s):
         g1 = torch.cuda.CUDAGraph()
+        if self.wgrad_xgraph and not self.is_dot and self.graph_comm is not True:
+            return self._capture_step_xgraph(static, pool, s)
         if self.world <= 1:
             with torch.cuda.graph(g1, pool=pool, stream=s):
                 preds, losses = self._fwd_bwd(static, overlap_comm=False)
@@ -596,6 +605,70 @@ class TrainStep:
         self._graphs = (g1, g2)
         self._static = (static, preds.detach(), {k: v.detach() for k, v in losses.items()})
 
+    def _capture_step_xgraph(self, static, pool, s):
+        """Two-queue backward (RUNTIME.WGRAD_XGRAPH = G > 0 groups): the step
+        graph without the weight-gradient GEMMs -- each conv backward adds an
+        event-record node once its dy exists -- then the queued wgrad launches
+        captured as G small graphs on their own stream and memory pool.  A
+        replay enqueues, on that stream, "wait for the last event of group g,
+        replay group g's graph" for every group (a wait on a node of a replayed
+        graph from outside it works on this ROCm; a wait NODE in another graph
+        does not, scripts/graph_external_event_probe.py), then the update graph
+        once both streams are done."""
+        from ..ops import hip_train
+        from ..runtime.streams import _fresh_stream
+        g1, g_u = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g1, pool=pool, stream=s):
+            hip_train.set_wgrad_xgraph(True)
+            try:
+                preds, losses = self._fwd_bwd(static, overlap_comm=False)
+            finally:
+                items = hip_train.take_wgrad_xgraph()
+        ws = self._wg_stream = self._wg_stream or _fresh_stream(self.device.index or 0, (s,))
+        ws.wait_stream(s)
+        G = max(1, min(int(self.wgrad_xgraph), len(items)))
+        bounds = [round(i * len(items) / G) for i in range(G + 1)]
+        wpool = torch.cuda.graph_pool_handle()
+        groups = []
+        hip_train.set_wgrad_defer(True)
+        try:
+            for gi in range(G):
+                part = items[bounds[gi]:bounds[gi + 1]]
+                if not part:
+                    continue
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=wpool, stream=ws):
+                    for _, fn, _ in part:
+                        fn()
+                    if gi == G - 1:
+                        hip_train.flush_wgrad_reduces()  # every layer's split reduction
+                groups.append((part[-1][0], g))
+        finally:
+            hip_train.set_wgrad_defer(False)
+        s.wait_stream(ws)
+        with torch.cuda.graph(g_u, pool=pool, stream=s):
+            self._update(preds, static["target"], losses)
+        self._bn_end()
+        self._graphs = (g1, g_u)
+        self._wgraph = (groups, ws, items)
+        self._static = (static, preds.detach(), {k: v.detach() for k, v in losses.items()})
+
+    def _replay_main(self):
+        """Replay the captured step graph(s) on the current stream (+ the wgrad
+        graph on its stream, + the eager collectives between graphs)."""
+        g1, g2 = self._graphs
+        g1.replay()
+        if self._wgraph is not None:
+            groups, ws, _ = self._wgraph
+            for ev, g in groups:
+                ev.wait(ws)  # the replay has reached this group's last dy
+                with torch.cuda.stream(ws):
+                    g.replay()
+            torch.cuda.current_stream().wait_stream(ws)
+        if g2 is not None:
+            self._reduce(replay=True)
+            g2.replay()
+
     def _capture_dot_dual(self, static, pool, s, out):
         """DOT: the task (CE) and KD backwards are independent -- both only read
         the forward's saved tensors and write their own half of the ``[2, n]``
@@ -615,6 +688,9 @@ class TrainStep:
             # (beside both backward passes); the KD backward does not read them
             feed = self._capture_teacher_feed(static, pool, s)
             feed.mode = "use"
+        # split: the next batch's teacher is its own graph on the teacher stream
+        # (not a branch of the CE graph); the copy into X happens before the step
+        in_graph = feed is not None and not self.teacher_split
         g_fwd, g_kd, g_ce, g_opt = (torch.cuda.CUDAGraph() for _ in range(4))
         with torch.cuda.graph(g_fwd, pool=pool, stream=s):
             preds, losses = self._fwd(static)
@@ -633,7 +709,7 @@ class TrainStep:
             with torch.cuda.stream(s):
                 hip_train._ws(self.device)  # the tagged scratch exists before the capture
             with torch.cuda.graph(g_ce, pool=torch.cuda.graph_pool_handle(), stream=s):
-                if feed is not None:
+                if in_graph:
                     with _autocast(self.device, self.dtype):
                         feed.prefetch(self.distiller.teacher)
                 self.flat.bind_grads(0)
@@ -645,7 +721,7 @@ class TrainStep:
                     self._flush_wgrad_defer(deferred)
                     self._join_wgrad_stream(armed)
                     join_branches()
-                if feed is not None:
+                if in_graph:
                     # join only: the KD-backward graph may still be replaying on the
                     # main stream; the copy into the teacher-output buffers it was
                     # built from happens in g_opt, after the two streams joined
@@ -657,9 +733,9 @@ class TrainStep:
         if self.world > 1:
             # split mode: the bucketed all-reduce runs eagerly between the backward
             # graphs (+ the post-backward hook, if any) and the optimizer graph
-            if getattr(self.distiller, "post_backward", None) is not None or feed is not None:
+            if getattr(self.distiller, "post_backward", None) is not None or in_graph:
                 with torch.cuda.graph(g_opt, pool=pool, stream=s):
-                    if feed is not None:
+                    if in_graph:
                         feed.commit()
                     self._post_backward()
             else:
@@ -669,15 +745,19 @@ class TrainStep:
                 self._update(preds, static["target"], losses)
         else:
             with torch.cuda.graph(g_opt, pool=pool, stream=s):
-                if feed is not None:
+                if in_graph:
                     feed.commit()
                 self._post_backward()
                 self._update(preds, static["target"], losses)
             g_upd = None
         self._bn_end()
-        self._dual = (g_fwd, g_kd, g_ce, g_opt, g_upd, torch.cuda.Stream(), torch.cuda.Event())
+        from ..runtime.streams import _fresh_stream, side_stream
+        s2 = _fresh_stream(self.device.index or 0, (s, side_stream(self.device)))
+        self._dual = (g_fwd, g_kd, g_ce, g_opt, g_upd, s2, torch.cuda.Event())
         self._graphs = (None, None)
         self._static = (static, preds.detach(), {k: v.detach() for k, v in losses.items()})
+        if feed is not None and self.teacher_split:
+            self._capture_teacher_split(feed)
         return out
 
     def _replay_dot_dual(self):
@@ -693,7 +773,7 @@ class TrainStep:
         if g_opt is not None:
             g_opt.replay()
         if g_upd is not None:
-            self._reduce()
+            self._reduce(replay=True)
             g_upd.replay()
 
     def step(self, batch: dict, next_batch: dict = None):
@@ -733,7 +813,7 @@ class TrainStep:
             out = self._eager(b)
             self.steps_done += 1
             return out
-        if self._tsplit is not None and self._pipe is not None and self._dual is None:
+        if self._tsplit is not None and self._pipe is not None:
             return self._step_split(batch, b, next_batch, static, preds, losses)
         # the step's input copies in one multi-tensor launch (each separate copy is a
         # ~5 us kernel ahead of the graph)
@@ -771,11 +851,7 @@ class TrainStep:
             self._replay_dot_dual()
             self.steps_done += 1
             return preds, losses
-        g1, g2 = self._graphs
-        g1.replay()
-        if g2 is not None:  # split mode: eager all-reduce between the graphs
-            self._reduce(replay=True)
-            g2.replay()
+        self._replay_main()  # (split mode: eager all-reduce between the graphs)
         self.steps_done += 1
         return preds, losses
 
@@ -832,11 +908,10 @@ class TrainStep:
 
         if nimg is not None and self.teacher_first:
             launch_teacher()
-        g1, g2 = self._graphs
-        g1.replay()
-        if g2 is not None:
-            self._reduce(replay=True)
-            g2.replay()
+        if self._dual is not None:
+            self._replay_dot_dual()
+        else:
+            self._replay_main()
         if nimg is not None and not self.teacher_first:
             launch_teacher()
         self.steps_done += 1
@@ -845,6 +920,7 @@ class TrainStep:
     def invalidate_graph(self) -> None:
         """Drop captured graphs (shape change, e.g. the last partial batch)."""
         self._graphs = None
+        self._wgraph = None
         self._static = None
         self._dual = None
         self._drop_feed()

@@ -12,7 +12,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ...ops.nn import conv_bn_act, channel_gather, channel_shuffle, grad_fork, pool_linear
+from ...ops.nn import conv_bn_act, channel_gather, channel_shuffle, grad_fork, pool_linear, shuffle_tail
 from .._base import ModelBase, PreactStage
 from .resnet import Stage
 
@@ -113,16 +113,17 @@ class BottleneckV1(nn.Module):
         return out
 
     def forward(self, x):
-        # stride 1: x feeds conv1 and the residual; their gradients are summed in
-        # conv1's dgrad epilogue (GradFork) instead of an autograd add
-        fork = grad_fork(x) if self.stride == 1 else None
+        # x feeds conv1 and the residual (stride 1) or the pooled shortcut
+        # (stride 2); their gradients are summed in conv1's dgrad epilogue
+        # (GradFork) instead of an autograd add
+        fork = grad_fork(x)
         out, _ = conv_bn_act(x, self.conv1, self.bn1, "relu", fork=fork)
         out = channel_gather(out, self._fmap, self._bmap)
         out, _ = conv_bn_act(out, self.conv2, self.bn2, "relu")
         if self.stride == 2:
             out, _ = conv_bn_act(out, self.conv3, self.bn3, "none")
-            preact = torch.cat([out, self.shortcut(x)], 1)
-            return F.relu(preact), preact
+            # cat([out, avgpool3x3s2(x)]) + relu: one native pass (ops.nn.shuffle_tail)
+            return shuffle_tail(out, x, fork)
         return conv_bn_act(out, self.conv3, self.bn3, "relu", residual=x,
                            want_preact=self.is_last and self._need_preact, res_fork=fork)
 

@@ -39,6 +39,11 @@ SIGNATURES = {
     "mda_relation_core": "piiiipps",
     "mda_rkd_loss": "piiii" + "fff" + "pppppps",
     "mda_gram_bwd": "ppppiis",
+    # graph-external events (csrc/events.hip)
+    "mda_event_create": "p",
+    "mda_event_destroy": "p",
+    "mda_event_record": "pis",
+    "mda_stream_wait_event": "pis",
     # convolution (csrc/conv_igemm.hip)
     "mda_conv_fwd": "pppppppp" + "i" * 15 + "s",
     "mda_conv_plan": "iiipp",
@@ -64,6 +69,8 @@ SIGNATURES = {
     # max pooling (csrc/pool.hip)
     "mda_maxpool_fwd": "ppp" + "i" * 9 + "s",
     "mda_maxpool_bwd": "ppp" + "i" * 9 + "s",
+    "mda_shuffle_tail_fwd": "pppp" + "i" * 7 + "s",
+    "mda_shuffle_tail_bwd": "ppppp" + "i" * 7 + "s",
     "mda_pack_conv_weights_pad": "pp" + "i" * 6 + "s",
     "mda_wgrad_plan": "iiiiiip",
     "mda_pack_conv_weights": "ppp" + "i" * 6 + "s",

@@ -1794,12 +1794,29 @@ MDA_API int mda_conv_plan(int64_t M, int64_t Cout, int64_t Kp, int64_t* tile, in
   return 0;
 }
 
+extern "C" int mda_conv1x1_stream_try(const void* x, const void* w, const float* scale,
+                                      const float* bias, const void* res, void* y, void* preact,
+                                      void* slot, int64_t N, int64_t H, int64_t W, int64_t K,
+                                      int64_t Kp, int64_t Ho, int64_t Wo, int64_t Cout,
+                                      int64_t stride, int64_t act, hipStream_t st);
+
 namespace {
 
 int dispatch(ConvParams& p, int mode, int64_t tile, int64_t splits, hipStream_t st, int halo = 0) {
   if (p.Kp % BK || p.Kp < p.K) return (int)hipErrorInvalidValue;
   if (p.ldx <= 0) p.ldx = p.Cin;
   if (p.cout_g <= 0) p.cout_g = p.Cout;
+  // memory-bound 1x1 convs (and stride-1 1x1 dgrads): the streaming kernel
+  // (conv1x1.hip) -- transposed MFMA, resident weights, stores straight from
+  // the accumulators; -1 = shape not served, fall through
+  if (p.KH == 1 && p.KW == 1 && p.pad == 0 && p.cout_g >= p.Cout && p.ldx == p.Cin &&
+      p.bnb_slot == nullptr && p.stats_part == nullptr && p.stamps == nullptr &&
+      (mode == LOAD_FAST || (mode == LOAD_DGRAD_FAST && p.stride == 1))) {
+    const int rc = mda_conv1x1_stream_try(p.x, p.w, p.scale, p.bias, p.res, p.y, p.preact,
+                                          p.stats_slot, p.N, p.H, p.W, p.Cin, p.Kp, p.Ho, p.Wo,
+                                          p.Cout, mode == LOAD_FAST ? p.stride : 1, p.act, st);
+    if (rc != -1) return rc;
+  }
   p.xcd = use_xcd_remap() ? 1 : 0;
   if (p.cout_g < p.Cout) {  // grouped: group-aligned tiles on the glds kernel only
     if (p.Cout % p.cout_g || p.ldx != p.Cin * (p.Cout / p.cout_g) || p.cout_g % 8 || p.Cin % 8)

@@ -204,3 +204,157 @@ MDA_API int mda_channel_gather(const void* x, void* y, const int* map, int64_t M
   MDA_CHECK_LAUNCH();
 }
 
+
+// ---------------------------------------------------------------------------
+// ShuffleNetV1 stride-2 unit tail (reference ShuffleNetv1.py:49,57):
+//   pre = cat([y3, avg_pool3x3_s2_p1(x)], channels); out = relu(pre)
+// in ONE pass (the torch path ran avg_pool2d, cat and clamp: 3 launches), and
+// its backward in one more: dz = dout * (pre > 0) (+ dpre); dy3 = dz[:, :C3];
+// dxp = avg_pool backward of dz[:, C3:] as a gather over the <= 4 output
+// pixels whose window covers each input pixel (count_include_pad: / 9).
+// 8 channels per thread, 16-byte I/O; C3, Cx % 8 == 0.
+namespace {
+
+__device__ __forceinline__ void unpack8(const uint4& v, float (&f)[8]) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    f[2 * k] = __uint_as_float(w[k] << 16);
+    f[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
+  return make_uint4(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]),
+                    pack_bf16x2(f[6], f[7]));
+}
+
+__global__ void __launch_bounds__(256)
+shuffle_tail_fwd_kernel(const bf16_t* __restrict__ y3, const bf16_t* __restrict__ x,
+                        bf16_t* __restrict__ pre, bf16_t* __restrict__ out, int N, int H, int W,
+                        int Ho, int Wo, int C3, int Cx) {
+  const int C = C3 + Cx, C8 = C / 8;
+  const int64_t total = (int64_t)N * Ho * Wo * C8;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = i / C8;
+    const int c = (int)(i - m * C8) * 8;
+    float v[8];
+    if (c < C3) {
+      unpack8(*(const uint4*)(y3 + m * C3 + c), v);
+    } else {
+      const int cx = c - C3;
+      const int n = (int)(m / ((int64_t)Ho * Wo));
+      const int r = (int)(m - (int64_t)n * Ho * Wo);
+      const int oh = r / Wo, ow = r - (r / Wo) * Wo;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = 0.f;
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const int ih = 2 * oh - 1 + kh, iw = 2 * ow - 1 + kw;
+          if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) {
+            float t[8];
+            unpack8(*(const uint4*)(x + ((int64_t)(n * H + ih) * W + iw) * Cx + cx), t);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += t[e];
+          }
+        }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= (1.f / 9.f);
+    }
+    const uint4 pv = pack8(v);
+    *(uint4*)(pre + m * C + c) = pv;
+    float o[8];
+    unpack8(pv, o);  // relu of the stored (rounded) pre-activation
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = fmaxf(o[e], 0.f);
+    *(uint4*)(out + m * C + c) = pack8(o);
+  }
+}
+
+__global__ void __launch_bounds__(256)
+shuffle_tail_bwd_kernel(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ dpre,
+                        const bf16_t* __restrict__ pre, bf16_t* __restrict__ dy3,
+                        bf16_t* __restrict__ dx, int N, int H, int W, int Ho, int Wo, int C3,
+                        int Cx) {
+  const int C = C3 + Cx;
+  const int64_t n3 = (int64_t)N * Ho * Wo * (C3 / 8);
+  const int64_t nx = (int64_t)N * H * W * (Cx / 8);
+  auto dz8 = [&](int64_t o, float (&d)[8]) {
+    float g[8], p[8];
+    unpack8(*(const uint4*)(dout + o), g);
+    unpack8(*(const uint4*)(pre + o), p);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) d[e] = p[e] > 0.f ? g[e] : 0.f;
+    if (dpre) {
+      float q[8];
+      unpack8(*(const uint4*)(dpre + o), q);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d[e] += q[e];
+    }
+  };
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n3 + nx;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    if (i < n3) {
+      const int64_t m = i / (C3 / 8);
+      const int c = (int)(i - m * (C3 / 8)) * 8;
+      float d[8];
+      dz8(m * C + c, d);
+      *(uint4*)(dy3 + m * C3 + c) = pack8(d);
+    } else {
+      const int64_t j = i - n3;
+      const int64_t px = j / (Cx / 8);
+      const int cx = (int)(j - px * (Cx / 8)) * 8;
+      const int n = (int)(px / ((int64_t)H * W));
+      const int r = (int)(px - (int64_t)n * H * W);
+      const int ih = r / W, iw = r - (r / W) * W;
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        const int th = ih + 1 - kh;  // = 2 * oh
+        if (th < 0 || (th & 1) || (th >> 1) >= Ho) continue;
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const int tw = iw + 1 - kw;
+          if (tw < 0 || (tw & 1) || (tw >> 1) >= Wo) continue;
+          float d[8];
+          dz8(((int64_t)(n * Ho + (th >> 1)) * Wo + (tw >> 1)) * C + C3 + cx, d);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[e] += d[e];
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] *= (1.f / 9.f);
+      *(uint4*)(dx + px * Cx + cx) = pack8(acc);
+    }
+  }
+}
+
+inline int tail_blocks(int64_t work) {
+  int64_t b = (work + 255) / 256;
+  return (int)(b < 4096 ? (b < 1 ? 1 : b) : 4096);
+}
+
+}  // namespace
+
+MDA_API int mda_shuffle_tail_fwd(const void* y3, const void* x, void* pre, void* out, int64_t N,
+                                 int64_t H, int64_t W, int64_t Ho, int64_t Wo, int64_t C3,
+                                 int64_t Cx, hipStream_t st) {
+  if (C3 % 8 || Cx % 8 || Ho != (H + 1) / 2 || Wo != (W + 1) / 2) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(shuffle_tail_fwd_kernel, dim3(tail_blocks(N * Ho * Wo * (C3 + Cx) / 8)), dim3(256),
+                     0, st, (const bf16_t*)y3, (const bf16_t*)x, (bf16_t*)pre, (bf16_t*)out, (int)N,
+                     (int)H, (int)W, (int)Ho, (int)Wo, (int)C3, (int)Cx);
+  MDA_CHECK_LAUNCH();
+}
+
+MDA_API int mda_shuffle_tail_bwd(const void* dout, const void* dpre, const void* pre, void* dy3,
+                                 void* dx, int64_t N, int64_t H, int64_t W, int64_t Ho, int64_t Wo,
+                                 int64_t C3, int64_t Cx, hipStream_t st) {
+  if (C3 % 8 || Cx % 8 || Ho != (H + 1) / 2 || Wo != (W + 1) / 2) return (int)hipErrorInvalidValue;
+  const int64_t work = N * Ho * Wo * C3 / 8 + N * H * W * Cx / 8;
+  hipLaunchKernelGGL(shuffle_tail_bwd_kernel, dim3(tail_blocks(work)), dim3(256), 0, st,
+                     (const bf16_t*)dout, (const bf16_t*)dpre, (const bf16_t*)pre, (bf16_t*)dy3,
+                     (bf16_t*)dx, (int)N, (int)H, (int)W, (int)Ho, (int)Wo, (int)C3, (int)Cx);
+  MDA_CHECK_LAUNCH();
+}

@@ -184,6 +184,56 @@ def channel_gather(x: torch.Tensor, fmap: torch.Tensor, bmap: torch.Tensor) -> t
     return y * (fmap >= 0).to(y.dtype).reshape(1, -1, 1, 1)
 
 
+class _ShuffleTail(torch.autograd.Function):
+    """ShuffleNetV1 stride-2 unit tail ``pre = cat([y3, avgpool3x3s2(x)]);
+    out = relu(pre)`` in one HIP pass, backward in one more (csrc/pool.hip).
+    ``fork``: x also feeds conv1; the pooled path's gradient is parked and
+    summed in conv1's dgrad epilogue (ops.hip_train.GradFork)."""
+
+    @staticmethod
+    def forward(ctx, y3, x, fork):
+        from . import _ext
+        ctx.set_materialize_grads(False)
+        y3 = y3.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        N, C3, Ho, Wo = y3.shape
+        _, Cx, H, W = x.shape
+        pre = torch.empty((N, C3 + Cx, Ho, Wo), dtype=torch.bfloat16, device=x.device,
+                          memory_format=torch.channels_last)
+        out = torch.empty_like(pre)
+        _ext.call("mda_shuffle_tail_fwd", y3, x, pre, out, N, H, W, Ho, Wo, C3, Cx)
+        ctx.save_for_backward(pre)
+        ctx.meta = (N, H, W, Ho, Wo, C3, Cx)
+        ctx.fork = fork.join() if fork is not None else None
+        return out, pre
+
+    @staticmethod
+    def backward(ctx, dout, dpre):
+        from . import _ext
+        from .hip_train import _fork_sum
+        pre, = ctx.saved_tensors
+        N, H, W, Ho, Wo, C3, Cx = ctx.meta
+        cl = torch.channels_last
+        if dout is None:
+            dout = torch.zeros_like(pre)
+        dout = dout.to(torch.bfloat16).contiguous(memory_format=cl)
+        dpre = dpre.to(torch.bfloat16).contiguous(memory_format=cl) if dpre is not None else None
+        dy3 = torch.empty((N, C3, Ho, Wo), dtype=torch.bfloat16, device=pre.device, memory_format=cl)
+        dx = torch.empty((N, Cx, H, W), dtype=torch.bfloat16, device=pre.device, memory_format=cl)
+        _ext.call("mda_shuffle_tail_bwd", dout, dpre, pre, dy3, dx, N, H, W, Ho, Wo, C3, Cx)
+        return dy3, _fork_sum(ctx.fork, dx), None
+
+
+def shuffle_tail(y3: torch.Tensor, x: torch.Tensor, fork=None):
+    """``(relu(pre), pre)`` with ``pre = cat([y3, avg_pool2d(x, 3, 2, 1)], 1)``."""
+    if (hip_enabled_for(x) and x.dim() == 4 and y3.shape[1] % 8 == 0 and x.shape[1] % 8 == 0
+            and y3.shape[2] == (x.shape[2] + 1) // 2 and y3.shape[3] == (x.shape[3] + 1) // 2
+            and x.dtype in (torch.bfloat16, torch.float32) and y3.dtype in (torch.bfloat16, torch.float32)):
+        return _ShuffleTail.apply(y3, x, fork)
+    pre = torch.cat([y3, F.avg_pool2d(x, 3, stride=2, padding=1).to(y3.dtype)], 1)
+    return F.relu(pre), pre
+
+
 def channel_shuffle(x: torch.Tensor, groups: int) -> torch.Tensor:
     n, c, h, w = x.shape
     if (hip_enabled_for(x) and x.dtype == torch.bfloat16 and c % groups == 0 and c % 2 == 0

@@ -244,9 +244,20 @@ class GradReducer:
     def _signal(self, b) -> None:
         if self._cap_flush is not None:
             self._cap_flush()
-        ev = torch.cuda.Event(external=True)
-        ev.record()
+        from ..runtime.streams import HipEvent
+        ev = HipEvent()  # (torch.cuda.Event(external=True) is refused on ROCm)
+        ev.record(external=True)
         self._cap.append((b, ev))
+
+    def abort_capture(self) -> None:
+        """A capture failed mid-backward: leave the capture mode (the eager
+        fallback step must launch its buckets normally)."""
+        self._cap = None
+        self._cap_flush = None
+        self._armed = False
+        self.graph_events = None
+        if self in _ARMED:
+            _ARMED.remove(self)
 
     def finish_capture(self) -> None:
         """End of the captured backward: events for the buckets not signalled
@@ -278,7 +289,7 @@ class GradReducer:
         self._works = {}
         with torch.cuda.stream(self._comm):
             for b, ev in self.graph_events:
-                self._comm.wait_event(ev)
+                ev.wait(self._comm)
                 self._launch(b, async_op=True)
                 self.early_launches += 1
 

@@ -24,6 +24,45 @@ _streams: dict = {}
 _lock = threading.Lock()
 
 
+class HipEvent:
+    """A raw HIP event whose record inside a stream capture becomes an
+    EXTERNAL event-record node of the graph (csrc/events.hip): a stream
+    outside the graph can wait on it after the replay has been launched.
+    (PyTorch's ROCm build refuses ``torch.cuda.Event(external=True)``.)"""
+
+    def __init__(self):
+        import ctypes
+        from ..ops import _ext
+        h = ctypes.c_void_p(0)
+        _ext.call("mda_event_create", h)
+        self.handle = h.value
+
+    # how an external record / wait is put into a capture: 2 = an explicit
+    # event node added to the capturing graph (csrc/events.hip), 1 = the
+    # hipEventRecordExternal / hipEventWaitExternal flags
+    MODE = 2
+
+    def record(self, external: bool = True, stream=None) -> None:
+        from ..ops import _ext
+        _ext.call("mda_event_record", self.handle, self.MODE if external else 0,
+                  stream=None if stream is None else stream.cuda_stream)
+
+    def wait(self, stream=None, external: bool = False) -> None:
+        """Make ``stream`` (default: the current one) wait for the last record
+        (``external``: as a wait node of the graph the stream is capturing)."""
+        from ..ops import _ext
+        _ext.call("mda_stream_wait_event", self.handle, self.MODE if external else 0,
+                  stream=None if stream is None else stream.cuda_stream)
+
+    def __del__(self):
+        try:
+            from ..ops import _ext
+            if self.handle:
+                _ext.call("mda_event_destroy", self.handle)
+        except Exception:  # noqa: BLE001 -- interpreter shutdown
+            pass
+
+
 def set_enabled(flag: bool) -> None:
     _state["enabled"] = bool(flag)
 

@@ -1,5 +1,6 @@
 """Can a stream outside a replayed hipGraph wait on an event recorded in the
-MIDDLE of that graph (``torch.cuda.Event(external=True)``)?
+MIDDLE of that graph?  (``hipEventRecordExternal`` through csrc/events.hip:
+PyTorch's ROCm build refuses ``torch.cuda.Event(external=True)``.)
 
 This is what an all-reduce overlapped with a captured backward needs: the
 graph records "bucket k complete" and the comm stream, enqueued by the host
@@ -7,7 +8,13 @@ right after the replay, waits on it.  Checks ordering (the snapshot taken on
 the side stream equals the value at the record point of THIS replay, never an
 older one) and timing (the side work finishes well before the graph does).
 """
+import os
+import sys
+
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from mdistiller_ddp_amd.runtime.streams import HipEvent  # noqa: E402
 
 
 def main():
@@ -18,7 +25,7 @@ def main():
     y = torch.zeros(1, device=dev)
     z = torch.zeros(1, device=dev)
     n = 200
-    ev = torch.cuda.Event(external=True)
+    ev = HipEvent()
     with torch.cuda.stream(s):
         x.add_(1)
     torch.cuda.synchronize()
@@ -27,7 +34,7 @@ def main():
     with torch.cuda.graph(g, stream=s):
         for _ in range(n):
             x.add_(1)
-        ev.record(s)
+        ev.record(external=True)
         for _ in range(n):
             y.add_(1)
     torch.cuda.synchronize()
@@ -42,7 +49,7 @@ def main():
         with torch.cuda.stream(s):
             g.replay()
         t2.record(s)
-        side.wait_event(ev)
+        ev.wait(side)
         with torch.cuda.stream(side):
             z.copy_(x)
             t1.record(side)
@@ -58,7 +65,14 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    for mode in (2, 1):
+        HipEvent.MODE = mode
+        try:
+            print(f"-- record/wait mode {mode}", flush=True)
+            main()
+        except RuntimeError as e:
+            print(f"mode {mode}: {e}", flush=True)
+    HipEvent.MODE = 2
 
 
 def two_graph_events():
@@ -70,7 +84,7 @@ def two_graph_events():
     x = torch.zeros(1, device=dev)
     snaps = torch.zeros(10, device=dev)
     w = torch.zeros(1, device=dev)
-    evs = [torch.cuda.Event(external=True) for _ in range(10)]
+    evs = [HipEvent() for _ in range(10)]
     ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
     with torch.cuda.stream(sa):
         x.add_(1)
@@ -79,10 +93,10 @@ def two_graph_events():
         for e in evs:
             for _ in range(20):
                 x.add_(1)
-            e.record(sa)
+            e.record(external=True)
     with torch.cuda.graph(gb, stream=sb):
         for i, e in enumerate(evs):
-            sb.wait_event(e)
+            e.wait(external=True)
             snaps[i].copy_(x[0])
             for _ in range(5):
                 w.add_(1)
@@ -126,4 +140,10 @@ def two_graph_events():
 
 
 if __name__ == "__main__":
-    two_graph_events()
+    for mode in (2, 1):
+        HipEvent.MODE = mode
+        try:
+            print(f"-- two graphs, mode {mode}", flush=True)
+            two_graph_events()
+        except RuntimeError as e:
+            print(f"mode {mode}: {e}", flush=True)

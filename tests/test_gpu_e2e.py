@@ -132,9 +132,10 @@ def test_validation_sees_updated_weights(tmp_path):
     assert abs(v2[0] - v2_ref[0]) <= 3.0, (v2, v2_ref)
 
 
-@pytest.mark.parametrize("trainer,student", [("base", "resnet8x4"), ("dot", "resnet8x4"),
-                                             ("base", "MobileNetV2"), ("base", "ShuffleV1")])
-def test_native_bf16_graph_matches_eager(trainer, student):
+@pytest.mark.parametrize("trainer,student,xgraph", [("base", "resnet8x4", False), ("dot", "resnet8x4", False),
+                                                    ("base", "MobileNetV2", False), ("base", "ShuffleV1", False),
+                                                    ("base", "resnet8x4", True), ("base", "MobileNetV2", True)])
+def test_native_bf16_graph_matches_eager(trainer, student, xgraph):
     """20 steps of the NATIVE bf16 path (HIP conv/BN/loss/optimizer kernels):
     hipGraph replay vs eager launches of the same kernels (the captured step
     defers every dense and depthwise weight-gradient reduction into one
@@ -143,6 +144,8 @@ def test_native_bf16_graph_matches_eager(trainer, student):
     torch.manual_seed(0)
     cfg = _cfg("DKD" if trainer == "base" else "KD", trainer)
     cfg.DISTILLER.STUDENT = student
+    # xgraph: the weight gradients as a second graph behind external events
+    cfg.RUNTIME.WGRAD_XGRAPH = 3 if xgraph else 0
     d1 = build_distiller(cfg, 100, "cuda")
     d2 = copy.deepcopy(d1)
     outs = []
@@ -155,6 +158,8 @@ def test_native_bf16_graph_matches_eager(trainer, student):
             st.step(b)
         torch.cuda.synchronize()
         assert (st._graphs is not None) == g
+        if g:
+            assert (st._wgraph is not None) == xgraph
         outs.append(st.flat.data.clone())
     rel = (outs[0] - outs[1]).norm() / outs[1].norm()
     assert rel < 1e-2, rel
@@ -275,8 +280,8 @@ def test_teacher_lookahead_matches_inline_teacher(typ, trainer, tgraph):
                 st.step(b, next_batch=nb)
             torch.cuda.synchronize()
             assert (st._pipe is not None) == la
-            # split: the teacher is its own graph on the teacher stream (not DOT's dual replay)
-            assert (st._tsplit is not None) == (la and tgraph == "split" and trainer != "dot")
+            # split: the teacher is its own graph on the teacher stream (DOT's dual replay too)
+            assert (st._tsplit is not None) == (la and tgraph == "split")
             outs.append((st.flat.data.clone(), st.meters.summary(reduce=False)))
     finally:
         torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det

@@ -62,3 +62,27 @@ def test_channel_shuffle_native(C, g):
     xr = x.float().clone().requires_grad_(True)
     (xr.reshape(n, g, c // g, h, w).transpose(1, 2).reshape(n, c, h, w) * go.to(torch.bfloat16).float()).sum().backward()
     torch.testing.assert_close(xh.grad.float(), xr.grad, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("N,C3,Cx,H", [(8, 216, 24, 32), (4, 240, 240, 16), (3, 480, 480, 8), (2, 16, 8, 7)])
+def test_shuffle_tail_matches_torch(N, C3, Cx, H):
+    """ShuffleNetV1 stride-2 tail (csrc/pool.hip mda_shuffle_tail_*): cat with
+    the 3x3/s2 average-pooled shortcut + ReLU, and its backward, vs PyTorch fp32."""
+    import torch.nn.functional as F
+    from mdistiller_ddp_amd.ops.nn import shuffle_tail
+    torch.manual_seed(0)
+    Ho = (H + 1) // 2
+    y3 = torch.randn(N, C3, Ho, Ho, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x = torch.randn(N, Cx, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    a, b = y3.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    out, pre = shuffle_tail(a, b)
+    ar, br = y3.float().requires_grad_(True), x.float().requires_grad_(True)
+    pre_r = torch.cat([ar, F.avg_pool2d(br, 3, stride=2, padding=1)], 1)
+    out_r = F.relu(pre_r)
+    rel = lambda u, v: ((u.float() - v.float()).norm() / v.float().norm()).item()  # noqa: E731
+    assert rel(pre, pre_r) < 1e-2 and rel(out, out_r) < 1e-2
+    g, gp = torch.randn_like(out_r), torch.randn_like(out_r)
+    ((out.float() * g).sum() + (pre.float() * gp).sum()).backward()
+    ((out_r * g).sum() + (pre_r * gp).sum()).backward()
+    assert rel(a.grad, ar.grad) < 1e-2
+    assert rel(b.grad, br.grad) < 1e-2

@@ -61,27 +61,21 @@ def test_student_virtual_residual_matches_materialised(name):
         out_off, dx_off = _run(off, x, g)
     finally:
         hip_train.set_virtual_residual(True)
-    # same kernels and arithmetic up to the residual's rounding (it is no longer
-    # stored in bf16 before the add)
-    assert _rel(out, out_off) < 2e-2
-    assert _rel(dx, dx_off) < 3e-2
-    for (n, p), (_, q) in zip(m.named_parameters(), off.named_parameters()):
-        assert _rel(p.grad, q.grad) < 3e-2, n
-    for (n, b), (_, c) in zip(m.named_buffers(), off.named_buffers()):
+    out_r, dx_r = _run(ref, x, g, backend="torch")  # fp32 PyTorch reference
+    # the virtual residual is the same arithmetic except that the shortcut's BN
+    # output is no longer rounded to bf16 before the add: it must be as close to
+    # fp32 as the materialised path is (bf16 noise through relu masks makes the
+    # two bf16 runs differ from each other by a few %, scripts/debug/vres_probe.py)
+    assert _rel(out, out_r) <= 1.25 * _rel(out_off, out_r) + 2e-3
+    assert _rel(dx, dx_r) <= 1.25 * _rel(dx_off, dx_r) + 5e-3
+    for (n, p), (_, q), (_, r) in zip(m.named_parameters(), off.named_parameters(), ref.named_parameters()):
+        assert _rel(p.grad, r.grad) <= 1.25 * _rel(q.grad, r.grad) + 5e-3, n
+    for (n, b), (_, c), (_, r) in zip(m.named_buffers(), off.named_buffers(), ref.named_buffers()):
         if b.dtype == torch.int64:
             assert torch.equal(b, c), n  # num_batches_tracked of the shortcut BN too
         else:
-            assert _rel(b, c) < 1e-2, n  # running stats of every BN, shortcut BNs included
-
-    # fp32 PyTorch reference of the same student
-    out_r, dx_r = _run(ref, x, g, backend="torch")
-    assert _rel(out, out_r) < 5e-2
-    assert _rel(dx, dx_r) < 8e-2
-    for (n, p), (_, q) in zip(m.named_parameters(), ref.named_parameters()):
-        assert _rel(p.grad, q.grad) < 8e-2, n
-    for (n, b), (_, c) in zip(m.named_buffers(), ref.named_buffers()):
-        if b.dtype != torch.int64:
-            assert _rel(b, c) < 2e-2, n
+            # running stats of every BN, shortcut BNs included
+            assert _rel(b, r) <= 1.25 * _rel(c, r) + 2e-3, n
 
 
 def test_virtual_residual_refuses_a_non_native_consumer():

@@ -83,6 +83,9 @@ CFG.RUNTIME.DTYPE = "bf16"           # bf16 | fp32           (compute dtype on G
 CFG.RUNTIME.HIP_GRAPH = True         # capture fwd+bwd+step into a hipGraph
 CFG.RUNTIME.TEACHER_STREAM = True    # teacher forward on its own HIP stream
 CFG.RUNTIME.DOT_DUAL_STREAM = True   # DOT: replay the task / KD backwards as concurrent graphs
+# DOT: both backwards as ONE pass over two stacked cotangents (auto = CIFAR
+# ResNet students on the HIP kernels; otherwise the two-pass path above)
+CFG.RUNTIME.DOT_SINGLE_PASS = "auto"
 CFG.RUNTIME.TEACHER_LOOKAHEAD = "auto"  # auto | on | off: captured steps run the teacher of batch t+1
                                         # beside the student step t (auto: off for >= 128 px feature KD)
 CFG.RUNTIME.TEACHER_GRAPH = "split"  # split | fork: the look-ahead teacher as its OWN single-chain graph

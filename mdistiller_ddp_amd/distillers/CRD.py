@@ -47,6 +47,47 @@ class Normalize(nn.Module):
         return x.div(norm)
 
 
+class _EmbedFn(torch.autograd.Function):
+    """``l2norm(x W^T + b)`` on csrc/embed.hip: one launch forward, two
+    backward (dgamma-style accumulation of dW / db straight into bound flat
+    gradients), instead of the linear + normalise chain and its autograd."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        from ..ops import _ext
+        x = x.contiguous()
+        N, K = x.shape
+        D = weight.shape[0]
+        out = torch.empty(N, D, dtype=torch.float32, device=x.device)
+        norm = torch.empty(N, dtype=torch.float32, device=x.device)
+        _ext.call("mda_embed_fwd", x, weight.detach(), bias.detach() if bias is not None else None,
+                  out, norm, N, K, D)
+        ctx.save_for_backward(x, weight, bias, out, norm)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        from ..ops import _ext
+        from ..parallel.grad_reducer import notify_grad
+        x, weight, bias, out, norm = ctx.saved_tensors
+        N, K = x.shape
+        D = weight.shape[0]
+        need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        need_b = bias is not None and ctx.needs_input_grad[2]
+        direct = (need_w and weight.grad is not None and weight.grad.is_contiguous()
+                  and (not need_b or bias.grad is not None))
+        dw = weight.grad if direct else (torch.zeros_like(weight) if need_w else None)
+        db = (bias.grad if direct else torch.zeros_like(bias)) if need_b else None
+        dx = torch.empty_like(x) if need_x else None
+        dy = torch.empty(N, D, dtype=torch.float32, device=x.device)
+        _ext.call("mda_embed_bwd", dout.float().contiguous(), out, norm, x, weight.detach(), dy, dx,
+                  dw, db, N, K, D)
+        if direct:
+            notify_grad(weight, *([bias] if need_b else []))
+            return dx, None, None
+        return dx, dw, db
+
+
 class Embed(nn.Module):
     def __init__(self, dim_in=1024, dim_out=128):
         super().__init__()
@@ -55,6 +96,10 @@ class Embed(nn.Module):
 
     def forward(self, x):
         x = x.reshape(x.shape[0], -1).float()
+        from ..ops.backend import hip_enabled_for
+        if (hip_enabled_for(x) and x.shape[1] <= 2048 and x.shape[1] % 4 == 0
+                and self.linear.out_features <= 1024):
+            return _EmbedFn.apply(x, self.linear.weight, self.linear.bias)
         return self.l2norm(nn.functional.linear(x, self.linear.weight, self.linear.bias))
 
 

@@ -26,6 +26,8 @@ from __future__ import annotations
 
 import contextlib
 
+import os
+
 import torch
 
 from ..parallel import GradReducer, get_world_size
@@ -205,6 +207,7 @@ class TrainStep:
         self._packs = None
         self._dual = None  # DOT: (fwd, kd-bwd, ce-bwd, opt, upd graphs, side stream, event)
         self.dot_dual = self.is_dot and bool(cfg.RUNTIME.get("DOT_DUAL_STREAM", True))
+        self.dot_single = self.is_dot and self._dot_single_ok(cfg)
         # measured (profiles/r2_wgrad_stream_ab.md): the forked wgrads pay off on ImageNet-sized
         # students (-4 %) and cost 5-9 % on the CIFAR ones, whose steps are too short for the
         # extra graph edges; "auto" = on for inputs of >= 128 px
@@ -299,6 +302,52 @@ class TrainStep:
             u = self._units[key] = torch.ones_like(v)
         return u
 
+    # module types whose whole backward runs on the native kernels that carry
+    # two stacked cotangents (ops/hip_train.py _Dual): the CIFAR ResNets
+    _DOT_SINGLE_MODULES = frozenset({"ResNet", "BasicBlock", "Bottleneck", "Conv2d", "BatchNorm2d",
+                                     "Linear", "ReLU", "Sequential", "ModuleList", "Identity", "Stage",
+                                     "AdaptiveAvgPool2d", "AvgPool2d"})
+
+    def _dot_single_ok(self, cfg) -> bool:
+        """``RUNTIME.DOT_SINGLE_PASS`` (auto | True | False): DOT's KD and task
+        backwards as ONE pass over two stacked cotangents (reference
+        trainer.py:425-432 runs two).  auto = the trainer is plain DOT, the
+        student's modules are all on the list above and the HIP kernels run."""
+        v = cfg.RUNTIME.get("DOT_SINGLE_PASS", "auto")
+        v = v.lower() if isinstance(v, str) else bool(v)
+        if v in (False, "false", "0", "off") or self.trainer != "dot" or self.device.type != "cuda":
+            return False
+        if self.dtype != torch.bfloat16:
+            return False  # the native training kernels are the bf16 path
+        student = getattr(self.distiller, "student", None)
+        if student is None:
+            return False
+        from ..ops.backend import hip_enabled_for
+        from ..ops import hip_train
+        if not (hip_enabled_for(self.flat.data) and hip_train._BN_FUSED[0]):
+            return False
+        for m in student.modules():
+            name = type(m).__name__
+            if name not in self._DOT_SINGLE_MODULES:
+                return False
+            if name == "Conv2d" and (m.groups != 1 or m.bias is not None):
+                return False
+        return True
+
+    def _dot_single_backward(self, losses):
+        """Both DOT gradient sets from one backward (``self.dot_single``): the
+        bound set is the KD one, the CE set sits ``gstride`` floats away."""
+        from ..ops import hip_train
+        self.flat.bind_grads(1)
+        g = self.flat.grads
+        gstride = (g[0].data_ptr() - g[1].data_ptr()) // g.element_size()
+        terms = [losses["loss_kd"], losses["loss_ce"]]
+        hip_train.set_dual(gstride)
+        try:
+            torch.autograd.backward(terms, [self._unit(v) for v in terms])
+        finally:
+            hip_train.set_dual(None)
+
     def _dot_reachability(self, losses):
         """Which params receive task / KD gradients (DOT's momentum branches)."""
         ps = self.flat.params
@@ -319,7 +368,9 @@ class TrainStep:
         deferred = (not armed) and self._arm_wgrad_defer()
         events = overlap_comm == "events" and not self.is_dot
         try:
-            if self.is_dot:
+            if self.is_dot and self.dot_single:
+                self._dot_single_backward(losses)
+            elif self.is_dot:
                 self.flat.bind_grads(1)
                 losses["loss_kd"].backward(retain_graph=True)
                 self.flat.bind_grads(0)
@@ -448,6 +499,8 @@ class TrainStep:
         if self.is_dot:
             self.reducer.reduce_sets((0, 1))
         elif replay and self.graph_comm == "events" and self.reducer.graph_events is not None:
+            if os.environ.get("MDA_EVENTS_SYNC") == "1":  # diagnostic: the replay drained first
+                torch.cuda.current_stream().synchronize()
             self.reducer.launch_from_events()
             self.reducer.wait_launched()
         else:
@@ -504,7 +557,7 @@ class TrainStep:
             # back to MIOpen on some layer): stay eager for good
             self.use_graph = False
             return out
-        if self.is_dot and self.dot_dual and self.graph_comm is not True:
+        if self.is_dot and self.dot_dual and not self.dot_single and self.graph_comm is not True:
             return self._capture_dot_dual(static, pool, s, out)
         feed = None
         if self._lookahead_on(static) and getattr(self.distiller, "teacher", None) is not None:

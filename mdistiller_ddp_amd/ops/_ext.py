@@ -52,7 +52,7 @@ SIGNATURES = {
     "mda_conv_dgrad": "pppp" + "i" * 14 + "s",
     "mda_conv_dgrad_res": "ppppp" + "i" * 14 + "s",
     "mda_conv_dgrad_bnsum": "ppppp" + "i" * 14 + "ppp" + "i" + "p" + "s",
-    "mda_conv_dgrad_bnsum_g": "ppppp" + "i" * 14 + "ppp" + "i" + "p" + "i" + "p" + "s",
+    "mda_conv_dgrad_bnsum_g": "ppppp" + "i" * 14 + "ppp" + "i" + "p" + "i" + "p" + "ii" + "s",
     "mda_conv_fwd_bnacc_g": "ppppp" + "i" * 14 + "i" + "s",
     "mda_pack_conv_weights_gc": "ppp" + "i" * 7 + "s",
     "mda_channel_gather": "ppp" + "iii" + "s",
@@ -61,8 +61,8 @@ SIGNATURES = {
     "mda_nst_fwd": "p" + "ii" + "p" + "s",
     "mda_dw_fwd_bnacc": "pppp" + "i" * 10 + "s",
     "mda_nst_bwd": "p" + "ii" + "pp" + "s",
-    "mda_conv_wgrad": "pppp" + "i" * 13 + "fiiis",
-    "mda_conv_wgrad_nored": "pppp" + "i" * 13 + "fiiis",
+    "mda_conv_wgrad": "pppp" + "i" * 13 + "fiii" + "ii" + "s",
+    "mda_conv_wgrad_nored": "pppp" + "i" * 13 + "fiii" + "i" + "s",
     "mda_wgrad_reduce_multi": "pis",
     "mda_pack_conv_weights_grouped": "ppp" + "i" * 7 + "s",
     "mda_pad_channels": "ippiiis",
@@ -96,17 +96,21 @@ SIGNATURES = {
     "mda_bn_stats_acc": "piips",
     "mda_bn_apply_fin": "ppii" + "ppppp" + "ff" + "p" + "ppp" + "i" + "s",
     "mda_bn_apply_fin_vr": "ppii" + "ppppp" + "ff" + "p" + "ppp" + "i" + "pppppp" + "ff" + "p" + "s",
-    "mda_bn_bwd_fused": "ppppp" + "p" + "iii" + "pp" + "pp" + "ppp" + "ppp" + "p" + "s",
-    "mda_bn_bwd_apply_reg": "pppp" + "p" + "iii" + "p" + "pp" + "ppp" + "ppp" + "p" + "s",
+    "mda_bn_bwd_fused": "ppppp" + "p" + "iii" + "pp" + "pp" + "ppp" + "ppp" + "p" + "iiii" + "s",
+    "mda_bn_bwd_apply_reg": "pppp" + "p" + "iii" + "p" + "pp" + "ppp" + "ppp" + "p" + "iiii" + "s",
     "mda_conv_fwd_bnacc": "ppppp" + "i" * 14 + "s",
     # CRD memory (csrc/crd.hip)
     "mda_crd_scores": "ppppiiifs",
     "mda_crd_grad": "ppppppiiifs",
     "mda_crd_update": "pppiifs",
+    "mda_embed_fwd": "ppppp" + "iii" + "s",
+    "mda_embed_bwd": "ppppp" + "pppp" + "iii" + "s",
     # classifier head + metrics (csrc/head.hip)
     "mda_pool_fc_fwd": "ipppppiiiis",
     "mda_pool_fc_bwd": "ippppppp" + "iiiii" + "s",
     "mda_sym_eig": "piiipp" + "s",
+    # KDSVD alignment + RBF + L2 after the eigensolver (csrc/kdsvd.hip)
+    "mda_kdsvd_post": "ppppp" + "iii" + "pp" + "s",
     "mda_pool_fc_bwd_bn": "ippppppp" + "iiiii" + "pppip" + "p" + "s",
     "mda_meters_update": "ippii" + "pppp" + "ips",
     # ReviewKD HCL + ABF (csrc/reviewkd.hip)

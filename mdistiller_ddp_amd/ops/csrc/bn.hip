@@ -803,7 +803,27 @@ struct BwdArgs {
   // the residual value is res * vres[2C + c] + vres[3C + c] (vres = that
   // layer's [4][C] stats)
   const float* vres;
+  // DOT single-pass backward (two stacked cotangents): gridDim.y = 2 sets;
+  // set 1's dout / dout2 / dpre / dy / dres start dd elements later, its
+  // dgamma / dbeta / sums dg floats later (the other gradient set of the flat
+  // buffer, may be negative) and its reg / rreg dr bytes later.  y, res, ry
+  // and every stats operand are the forward's, shared by both sets.
+  int64_t dd, dg, dr;
 };
+
+__device__ __forceinline__ void dual_shift(BwdArgs& a) {
+  if (blockIdx.y == 0) return;
+  if (a.dout) a.dout += a.dd;
+  if (a.dout2) a.dout2 += a.dd;
+  if (a.dpre) a.dpre += a.dd;
+  if (a.dy) a.dy += a.dd;
+  if (a.dres) a.dres += a.dd;
+  if (a.dgamma) a.dgamma += a.dg;
+  if (a.dbeta) a.dbeta += a.dg;
+  if (a.sums) a.sums += a.dg;
+  if (a.reg) a.reg = (BnRegion*)((char*)a.reg + a.dr);
+  if (a.rreg) a.rreg = (BnRegion*)((char*)a.rreg + a.dr);
+}
 
 // res-producer sums of one 8-channel vector (dz = the stored dres values)
 __device__ __forceinline__ void rsum_add8(const BwdArgs& a, int64_t o, int c0, const uint32_t (&ro)[4],
@@ -857,6 +877,7 @@ __device__ __forceinline__ void bwd_dz8(const BwdArgs& a, const Raw8& v, const f
 template <int VPT, bool HOLD>
 __global__ void __launch_bounds__(256)
 bn_bwd_fused_kernel(BwdArgs a) {
+  dual_shift(a);
   __shared__ float s_m0[SLOT_CMAX], s_m1[SLOT_CMAX];
   const int C = a.C, M = a.M;
   const int C8 = C / 8;
@@ -995,6 +1016,7 @@ bn_bwd_fused_kernel(BwdArgs a) {
 // re-read y / dout with 4 waves per CU (70 us for a 64 x 112^2 x 64 layer).
 __global__ void __launch_bounds__(256)
 bn_bwd_sums_kernel(BwdArgs a) {
+  dual_shift(a);
   const int C = a.C, M = a.M;
   const int C8 = C / 8;
   const int rpi = 256 / C8;
@@ -1036,6 +1058,7 @@ _Pragma("unroll")
 // prologue reads the region, so both latencies overlap.
 __global__ void __launch_bounds__(256)
 bn_bwd_apply_reg_kernel(BwdArgs a) {
+  dual_shift(a);
   // per-channel operands in LDS: a thread's channel group changes along the
   // grid stride when C / 8 is not a power of two (MobileNetV2 widths)
   __shared__ float s_m0[SLOT_CMAX], s_m1[SLOT_CMAX], s_st[4][SLOT_CMAX], s_vr[2][SLOT_CMAX];
@@ -1189,36 +1212,39 @@ MDA_API int mda_bn_bwd_fused(const void* dout, const void* dout2, const void* dp
                              int64_t act, void* region, void* err, void* dy, void* dres,
                              float* dgamma, float* dbeta, float* sums, const void* ry,
                              const float* rstats, void* rregion, const float* vres,
-                             hipStream_t st) {
+                             int64_t nsets, int64_t dd, int64_t dg, int64_t dr, hipStream_t st) {
   if (C % 8 || C > SLOT_CMAX || M <= 0 || M >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
   if (rregion != nullptr && (dres == nullptr || ry == nullptr || rstats == nullptr ||
                              256 % (C / 8) != 0))
     return (int)hipErrorInvalidValue;
+  if (nsets != 1 && (nsets != 2 || dr <= 0)) return (int)hipErrorInvalidValue;
   BwdArgs a{(const bf16_t*)dout, (const bf16_t*)dout2, (const bf16_t*)dpre, (const bf16_t*)y,
             (const bf16_t*)res, stats, (bf16_t*)dy, (bf16_t*)dres, dgamma, dbeta, sums,
             (BnRegion*)region, (unsigned*)err, (int)M, (int)C, (int)act, (const bf16_t*)ry,
-            rstats, (BnRegion*)rregion, vres};
+            rstats, (BnRegion*)rregion, vres, dd, dg, dr};
   const int C8 = (int)C / 8;
   const int rpi = 256 / C8;
   const int64_t rows_iter = (M + rpi - 1) / rpi;       // block-iterations of work
-  // at most one block per CU: every block of the grid barrier is resident
-  const int maxb = num_cus();
+  // at most one block per CU over BOTH sets: every block of each set's grid
+  // barrier is resident
+  const int maxb = std::max(1, num_cus() / (int)nsets);
   const int nb = (int)std::min<int64_t>(rows_iter, maxb);
   const int64_t per = (rows_iter + nb - 1) / nb;     // row iterations per thread
+  const unsigned ns = (unsigned)nsets;
   if (per > 8) {
     // too many rows to hold: sums with a full grid, then one streaming pass
     const int nbr = reduce_blocks(M, C, BWD2_VPT, BWD2_MAXB);
-    hipLaunchKernelGGL(bn_bwd_sums_kernel, dim3(nbr), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(bn_bwd_sums_kernel, dim3(nbr, ns), dim3(256), 0, st, a);
     { const int rc_ = (int)hipGetLastError(); if (rc_) return rc_; }
     a.err = nullptr;
-    hipLaunchKernelGGL(bn_bwd_apply_reg_kernel, dim3(apply_blocks(M * C / 8, APPLY_V)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(bn_bwd_apply_reg_kernel, dim3(apply_blocks(M * C / 8, APPLY_V), ns), dim3(256), 0, st, a);
     MDA_CHECK_LAUNCH();
   }
-  if (per <= 1) hipLaunchKernelGGL((bn_bwd_fused_kernel<1, true>), dim3(nb), dim3(256), 0, st, a);
-  else if (per <= 2) hipLaunchKernelGGL((bn_bwd_fused_kernel<2, true>), dim3(nb), dim3(256), 0, st, a);
-  else if (per <= 4) hipLaunchKernelGGL((bn_bwd_fused_kernel<4, true>), dim3(nb), dim3(256), 0, st, a);
-  else if (per <= 8) hipLaunchKernelGGL((bn_bwd_fused_kernel<8, true>), dim3(nb), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((bn_bwd_fused_kernel<1, false>), dim3(nb), dim3(256), 0, st, a);
+  if (per <= 1) hipLaunchKernelGGL((bn_bwd_fused_kernel<1, true>), dim3(nb, ns), dim3(256), 0, st, a);
+  else if (per <= 2) hipLaunchKernelGGL((bn_bwd_fused_kernel<2, true>), dim3(nb, ns), dim3(256), 0, st, a);
+  else if (per <= 4) hipLaunchKernelGGL((bn_bwd_fused_kernel<4, true>), dim3(nb, ns), dim3(256), 0, st, a);
+  else if (per <= 8) hipLaunchKernelGGL((bn_bwd_fused_kernel<8, true>), dim3(nb, ns), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((bn_bwd_fused_kernel<1, false>), dim3(nb, ns), dim3(256), 0, st, a);
   MDA_CHECK_LAUNCH();
 }
 
@@ -1228,16 +1254,18 @@ MDA_API int mda_bn_bwd_apply_reg(const void* dout, const void* dpre, const void*
                                  const float* stats, int64_t M, int64_t C, int64_t act,
                                  void* region, void* dy, void* dres, float* dgamma, float* dbeta,
                                  float* sums, const void* ry, const float* rstats, void* rregion,
-                                 const float* vres, hipStream_t st) {
+                                 const float* vres, int64_t nsets, int64_t dd, int64_t dg,
+                                 int64_t dr, hipStream_t st) {
   if (C % 8 || C > SLOT_CMAX || M <= 0 || M >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
+  if (nsets != 1 && (nsets != 2 || dr <= 0)) return (int)hipErrorInvalidValue;
   BwdArgs a{(const bf16_t*)dout, nullptr, (const bf16_t*)dpre, (const bf16_t*)y,
             (const bf16_t*)res, stats, (bf16_t*)dy, (bf16_t*)dres, dgamma, dbeta, sums,
             (BnRegion*)region, nullptr, (int)M, (int)C, (int)act, (const bf16_t*)ry, rstats,
-            (BnRegion*)rregion, vres};
+            (BnRegion*)rregion, vres, dd, dg, dr};
   const int nb = apply_blocks(M * C / 8, APPLY_V);
   if (rregion != nullptr && (dres == nullptr || ry == nullptr || rstats == nullptr ||
                              256 % (C / 8) != 0))
     return (int)hipErrorInvalidValue;  // a thread must keep one channel group
-  hipLaunchKernelGGL(bn_bwd_apply_reg_kernel, dim3(nb), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(bn_bwd_apply_reg_kernel, dim3(nb, (unsigned)nsets), dim3(256), 0, st, a);
   MDA_CHECK_LAUNCH();
 }

@@ -91,6 +91,12 @@ struct ConvParams {
   // optional: bnb_res is the RAW input of another training BN applied inside
   // this layer's apply (mda_bn_apply_fin_vr): residual = res*vres[2C+c] + vres[3C+c]
   const float* bnb_vres;
+  // DOT single-pass backward: dy / dx hold two stacked cotangents (2N images);
+  // rows >= bnb_mh belong to set 1, read bnb_y / bnb_res at row - bnb_mh (the
+  // forward's N images) and add their sums into the region bnb_rstride bytes
+  // past bnb_slot.  0 = one set.
+  int bnb_mh;
+  int64_t bnb_rstride;
   // grouped conv (glds kernel only): Cin above is the channels of ONE group,
   // x rows hold ldx channels, each group owns cout_g consecutive output
   // channels, and a block's N tile never leaves its group (grid.y = groups x
@@ -338,6 +344,7 @@ __device__ __forceinline__ void conv_epilogue_bnb(const ConvParams& p, float* Cs
   }
   uint4 yv[RPT], rv[RPT], gv[RPT];
   int mrow[RPT];
+  const int mh = p.bnb_mh;
 #pragma unroll
   for (int k = 0; k < RPT; ++k) {
     const int r0 = rr + k * RPP;
@@ -345,15 +352,19 @@ __device__ __forceinline__ void conv_epilogue_bnb(const ConvParams& p, float* Cs
     const bool ok = cok && r0 < rows && m < mlim;
     if (ok && has_pc) m = par_row(p, pc, m);
     mrow[k] = ok ? m : -1;
+    const int ma = (mh > 0 && m >= mh) ? m - mh : m;  // the forward's row
     const int64_t o = (int64_t)(ok ? m : 0) * C + (cok ? co : 0);
-    yv[k] = ok ? *(const uint4*)(p.bnb_y + o) : make_uint4(0u, 0u, 0u, 0u);
-    rv[k] = (ok && zres) ? *(const uint4*)(p.bnb_res + o) : make_uint4(0u, 0u, 0u, 0u);
+    const int64_t oa = (int64_t)(ok ? ma : 0) * C + (cok ? co : 0);
+    yv[k] = ok ? *(const uint4*)(p.bnb_y + oa) : make_uint4(0u, 0u, 0u, 0u);
+    rv[k] = (ok && zres) ? *(const uint4*)(p.bnb_res + oa) : make_uint4(0u, 0u, 0u, 0u);
     gv[k] = (ok && p.res) ? *(const uint4*)(p.res + o) : make_uint4(0u, 0u, 0u, 0u);
   }
   float s1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, s2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float t1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, t2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int k = 0; k < RPT; ++k) {
     if (mrow[k] < 0) continue;
+    const bool set1 = mh > 0 && mrow[k] >= mh;
     const int r0 = rr + k * RPP;
     const float4 lo = *(const float4*)&Cs[r0 * CS + c8 * 8];
     const float4 hi = *(const float4*)&Cs[r0 * CS + c8 * 8 + 4];
@@ -379,29 +390,34 @@ __device__ __forceinline__ void conv_epilogue_bnb(const ConvParams& p, float* Cs
           if (zres) z += (h ? __uint_as_float(rw[w] & 0xffff0000u) : __uint_as_float(rw[w] << 16)) * vsc[e] + vsh[e];
           d *= bnb_act_grad(z, p.bnb_act);
         }
-        s1[e] += d;
-        s2[e] += d * ((yf - mu[e]) * rs[e]);
+        const float xh = d * ((yf - mu[e]) * rs[e]);
+        if (set1) { t1[e] += d; t2[e] += xh; } else { s1[e] += d; s2[e] += xh; }
       }
     }
     *(uint4*)(p.y + (int64_t)mrow[k] * C + co) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
   }
   __syncthreads();  // every read of the C tile is done: reuse it for the reduction
   float* red = Cs;  // [2][RPP][BN]
+  const int nsets = mh > 0 ? 2 : 1;  // (block-uniform)
+  for (int set = 0; set < nsets; ++set) {
+    if (set) __syncthreads();  // set 0's reads of `red` are done
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    red[(0 * RPP + rr) * BN + c8 * 8 + e] = s1[e];
-    red[(1 * RPP + rr) * BN + c8 * 8 + e] = s2[e];
-  }
-  __syncthreads();
-  if (tid < 2 * BN) {
-    const int q = tid / BN, c = tid - q * BN;
-    float a0 = 0.f, a1 = 0.f;
-    for (int r = 0; r < RPP; r += 2) {
-      a0 += red[(q * RPP + r) * BN + c];
-      a1 += red[(q * RPP + r + 1) * BN + c];
+    for (int e = 0; e < 8; ++e) {
+      red[(0 * RPP + rr) * BN + c8 * 8 + e] = set ? t1[e] : s1[e];
+      red[(1 * RPP + rr) * BN + c8 * 8 + e] = set ? t2[e] : s2[e];
     }
-    if (n0 + c < group_nlim(p, n0))
-      acc_add(region_acc(p.bnb_slot, C, (int)blockIdx.x % slot_shards(C), q) + n0 + c, (double)(a0 + a1));
+    __syncthreads();
+    if (tid < 2 * BN) {
+      const int q = tid / BN, c = tid - q * BN;
+      float a0 = 0.f, a1 = 0.f;
+      for (int r = 0; r < RPP; r += 2) {
+        a0 += red[(q * RPP + r) * BN + c];
+        a1 += red[(q * RPP + r + 1) * BN + c];
+      }
+      BnRegion* slot = (BnRegion*)((char*)p.bnb_slot + (set ? p.bnb_rstride : 0));
+      if (n0 + c < group_nlim(p, n0))
+        acc_add(region_acc(slot, C, (int)blockIdx.x % slot_shards(C), q) + n0 + c, (double)(a0 + a1));
+    }
   }
 }
 
@@ -1981,7 +1997,8 @@ MDA_API int mda_conv_dgrad_bnsum_g(const void* dy, const void* wt, void* dx, flo
                                    int64_t stride, int64_t pad, int64_t Kp, int64_t tile,
                                    int64_t splits, const void* bn_y, const void* bn_res,
                                    const float* bn_stats, int64_t bn_act, void* region,
-                                   int64_t groups, const float* bn_vres, hipStream_t st);
+                                   int64_t groups, const float* bn_vres, int64_t bn_mh,
+                                   int64_t bn_rstride, hipStream_t st);
 
 MDA_API int mda_conv_dgrad(const void* dy, const void* wt, void* dx, float* partial, int64_t N,
                            int64_t H, int64_t W, int64_t Cin, int64_t Ho, int64_t Wo,
@@ -2018,7 +2035,7 @@ MDA_API int mda_conv_dgrad_bnsum(const void* dy, const void* wt, void* dx, float
                                  hipStream_t st) {
   return mda_conv_dgrad_bnsum_g(dy, wt, dx, partial, res, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
                                 stride, pad, Kp, tile, splits, bn_y, bn_res, bn_stats, bn_act,
-                                region, 1, nullptr, st);
+                                region, 1, nullptr, 0, 0, st);
 }
 
 // Grouped dgrad (groups > 1): dx[.., g*Cin/G + ci] sums only group g's output
@@ -2030,12 +2047,18 @@ MDA_API int mda_conv_dgrad_bnsum_g(const void* dy, const void* wt, void* dx, flo
                                    int64_t stride, int64_t pad, int64_t Kp, int64_t tile,
                                    int64_t splits, const void* bn_y, const void* bn_res,
                                    const float* bn_stats, int64_t bn_act, void* region,
-                                   int64_t groups, const float* bn_vres, hipStream_t st) {
+                                   int64_t groups, const float* bn_vres, int64_t bn_mh,
+                                   int64_t bn_rstride, hipStream_t st) {
   if (Cout % 8 || groups < 1 || Cin % groups || Cout % groups) return (int)hipErrorInvalidValue;
   if (region != nullptr && (splits != 1 || Cin % 8 || Cin > SLOT_CMAX || bn_y == nullptr ||
                             bn_stats == nullptr))
     return (int)hipErrorInvalidValue;
+  // two stacked sets: dx rows [mh, 2 mh) are set 1 (N holds both sets' images)
+  if (bn_mh != 0 && (region == nullptr || bn_mh * 2 != N * H * W || bn_rstride <= 0))
+    return (int)hipErrorInvalidValue;
   ConvParams p{};
+  p.bnb_mh = (int)bn_mh;
+  p.bnb_rstride = bn_rstride;
   p.bnb_y = (const bf16_t*)bn_y;
   p.bnb_res = (const bf16_t*)bn_res;
   p.bnb_stats = bn_stats;

@@ -58,6 +58,10 @@ struct WgParams {
   int N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, K, Kp, M, m_per_split;
   int x_bytes, dy_bytes;
   FastDiv div_howo, div_wo;
+  // splits per gradient set: gridDim.z = sets x zsp.  Set k (DOT single-pass
+  // backward: two stacked cotangents) reads dy k*M*Cout elements in and owns
+  // partial sets [k*zsp, (k+1)*zsp); x is shared.
+  int zsp;
 };
 
 constexpr uint32_t OOB = 0x80000000u;
@@ -101,11 +105,12 @@ conv_wgrad_kernel(const WgParams p) {
   const int wm = wid >> 1, wn = wid & 1;
   const int co0 = blockIdx.x * TC;
   const int k0 = blockIdx.y * TK;
-  const int m_begin = blockIdx.z * p.m_per_split;
+  const int zset = (int)blockIdx.z / p.zsp;
+  const int m_begin = ((int)blockIdx.z - zset * p.zsp) * p.m_per_split;
   const int m_end = min(p.M, m_begin + p.m_per_split);
   const int chunk = tid & 7, row = tid >> 3;  // 32 rows x 8 chunks per pass, 2 passes
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(p.x, p.x_bytes);
-  const __amdgpu_buffer_rsrc_t dr = make_rsrc(p.dy, p.dy_bytes);
+  const __amdgpu_buffer_rsrc_t dr = make_rsrc(p.dy + (int64_t)zset * p.M * p.Cout, p.dy_bytes);
 
   // this thread's im2col column (fixed for the whole block): tap and channel
   int tap, c;
@@ -287,8 +292,10 @@ conv_wgrad_glds_kernel(const WgParams p) {
   const int wm = wid >> 1, wn = wid & 1;
   const int co0 = blockIdx.x * TCo;
   const int k0 = blockIdx.y * TKk;
-  const int m_begin = blockIdx.z * p.m_per_split;
+  const int zset = (int)blockIdx.z / p.zsp;
+  const int m_begin = ((int)blockIdx.z - zset * p.zsp) * p.m_per_split;
   const int m_end = min(p.M, m_begin + p.m_per_split);
+  const bf16_t* const dyp = p.dy + (int64_t)zset * p.M * p.Cout;
   const uint32_t wave_off = (uint32_t)__builtin_amdgcn_readfirstlane(wid) * 1024u;
   const bf16_t* const zero = (const bf16_t*)g_wg_zero16;
 
@@ -337,7 +344,7 @@ conv_wgrad_glds_kernel(const WgParams p) {
       const int ow = rr - oh * p.Wo;
 #pragma unroll
       for (int sc = 0; sc < SC; ++sc) {
-        const bf16_t* src = (mok && dy_ok[sc][d]) ? p.dy + ((int64_t)mm * p.Cout + dy_col[sc][d]) : zero;
+        const bf16_t* src = (mok && dy_ok[sc][d]) ? dyp + ((int64_t)mm * p.Cout + dy_col[sc][d]) : zero;
         wg_glds16(src, base + (uint32_t)(sc * SUB + d * 4096));
       }
 #pragma unroll
@@ -804,8 +811,9 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* partial, float*
                            int64_t H, int64_t W, int64_t Cin, int64_t Ho, int64_t Wo, int64_t Cout,
                            int64_t KH, int64_t KW, int64_t stride, int64_t pad, int64_t Kp,
                            int64_t splits, float scale, int64_t accumulate, int64_t cin_keep,
-                           int64_t groups, hipStream_t st, bool reduce) {
-  if (Cout % 8 || Kp % TK) return (int)hipErrorInvalidValue;
+                           int64_t groups, hipStream_t st, bool reduce, int64_t nsets,
+                           int64_t gstride) {
+  if (Cout % 8 || Kp % TK || nsets < 1 || nsets > 2) return (int)hipErrorInvalidValue;
   if (cin_keep <= 0 || cin_keep > Cin) cin_keep = Cin;
   if (groups > 1 && (Cin % groups || Cout % groups)) return (int)hipErrorInvalidValue;
   WgParams p;
@@ -820,12 +828,13 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* partial, float*
   p.div_wo = make_fastdiv((uint32_t)Wo);
   if (splits <= 0) mda_wgrad_plan(p.M, Cout, Cin, KH, KW, Kp, &splits);
   p.m_per_split = (int)(((p.M + splits - 1) / splits + TM - 1) / TM * TM);
+  p.zsp = (int)splits;
   const int mode = (Cin % TK == 0) ? WG_FAST : (Cin % 8 == 0 ? WG_VEC8 : WG_SCALAR);
-  dim3 grid((int)((Cout + TC - 1) / TC), (int)(Kp / TK), (int)splits);
+  dim3 grid((int)((Cout + TC - 1) / TC), (int)(Kp / TK), (int)(splits * nsets));
   const int tile = mode == WG_SCALAR ? 0 : wg_tile(p.M, Cout, Cin, KH, KW, Kp);
   if (tile != 0) {
     const int tc = tile / 1000, tk = tile % 1000;
-    dim3 g2((int)((Cout + tc - 1) / tc), (int)((Kp + tk - 1) / tk), (int)splits);
+    dim3 g2((int)((Cout + tc - 1) / tc), (int)((Kp + tk - 1) / tk), (int)(splits * nsets));
     switch (tile) {
       case 128128: hipLaunchKernelGGL((conv_wgrad_glds_kernel<128, 128>), g2, dim3(256), 0, st, p); break;
       case 128064: hipLaunchKernelGGL((conv_wgrad_glds_kernel<128, 64>), g2, dim3(256), 0, st, p); break;
@@ -843,19 +852,24 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* partial, float*
   const int64_t total4 = Cout * Kp / 4;  // Kp % 64 == 0
   const int cp = wgr_cols((int)splits);
   const int blocks = (int)((total4 + cp - 1) / cp);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, partial, grad,
-                     (int)splits, (int)Cout, (int)Cin, (int)KH, (int)KW, (int)Kp, scale,
-                     (int)accumulate, (int)cin_keep, (int)(groups > 1 ? groups : 1));
-  MDA_CHECK_LAUNCH();
+  for (int64_t k = 0; k < nsets; ++k) {
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st,
+                       partial + k * splits * Cout * Kp, grad + k * gstride,
+                       (int)splits, (int)Cout, (int)Cin, (int)KH, (int)KW, (int)Kp, scale,
+                       (int)accumulate, (int)cin_keep, (int)(groups > 1 ? groups : 1));
+    const int rc2 = (int)hipGetLastError();
+    if (rc2) return rc2;
+  }
+  return 0;
 }
 
 MDA_API int mda_conv_wgrad(const void* x, const void* dy, float* partial, float* grad, int64_t N,
                            int64_t H, int64_t W, int64_t Cin, int64_t Ho, int64_t Wo, int64_t Cout,
                            int64_t KH, int64_t KW, int64_t stride, int64_t pad, int64_t Kp,
                            int64_t splits, float scale, int64_t accumulate, int64_t cin_keep,
-                           int64_t groups, hipStream_t st) {
+                           int64_t groups, int64_t nsets, int64_t gstride, hipStream_t st) {
   return conv_wgrad_impl(x, dy, partial, grad, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
-                         Kp, splits, scale, accumulate, cin_keep, groups, st, true);
+                         Kp, splits, scale, accumulate, cin_keep, groups, st, true, nsets, gstride);
 }
 
 // The weight-gradient GEMM only: its split partials stay in `partial` for a
@@ -866,9 +880,9 @@ MDA_API int mda_conv_wgrad_nored(const void* x, const void* dy, float* partial, 
                                  int64_t Wo, int64_t Cout, int64_t KH, int64_t KW, int64_t stride,
                                  int64_t pad, int64_t Kp, int64_t splits, float scale,
                                  int64_t accumulate, int64_t cin_keep, int64_t groups,
-                                 hipStream_t st) {
+                                 int64_t nsets, hipStream_t st) {
   return conv_wgrad_impl(x, dy, partial, grad, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
-                         Kp, splits, scale, accumulate, cin_keep, groups, st, false);
+                         Kp, splits, scale, accumulate, cin_keep, groups, st, false, nsets, 0);
 }
 
 // rows: n x 11 int64 {partial, grad, splits, Cout, Cin, KH, KW, Kp, accumulate, cin_keep,

@@ -489,12 +489,62 @@ def _align_rsv(a, b):
     return torch.matmul(a, mask), b
 
 
+class _KdsvdPost(torch.autograd.Function):
+    """The KDSVD loss from the stages' eigendecompositions (csrc/kdsvd.hip):
+    sign alignment of the k+3 leading student vectors to the k teacher ones,
+    teacher-singular-value scaling, inter-stage RBF and L2 -- one launch
+    forward, one backward (the PyTorch composition of :func:`kdsvd_loss`'s
+    fallback is ~450 elementwise kernels per step).  Inputs: k, the teacher
+    eigenvalue / eigenvector lists (no gradient), then the student
+    eigenvector batches [N, W, W] (columns)."""
+
+    @staticmethod
+    def forward(ctx, k, lt, vt, *vs):
+        S, N = len(vs), vs[0].shape[0]
+        vs = [v.contiguous() for v in vs]
+        vt = [v.contiguous() for v in vt]
+        lt = [v.contiguous() for v in lt]
+        W = [v.shape[-1] for v in vs]
+        part = torch.empty(N, dtype=torch.float32, device=vs[0].device)
+        tab = _kdsvd_table(vs, vt, lt, None, W)
+        _ext.call("mda_kdsvd_post", *tab, S, N, k, part, None)
+        ctx.save_for_backward(*vs, *vt, *lt)
+        ctx.meta = (k, S, N, W)
+        return part.sum()
+
+    @staticmethod
+    def backward(ctx, go):
+        k, S, N, W = ctx.meta
+        t = ctx.saved_tensors
+        vs, vt, lt = list(t[:S]), list(t[S:2 * S]), list(t[2 * S:])
+        dvs = [torch.empty_like(v) for v in vs]
+        tab = _kdsvd_table(vs, vt, lt, dvs, W)
+        _ext.call("mda_kdsvd_post", *tab, S, N, k, None, go.float().reshape(1).contiguous())
+        return (None, None, None) + tuple(dvs)
+
+
+def _kdsvd_table(vs, vt, lt, dvs, W):
+    """Host pointer arrays of :func:`mda_kdsvd_post` (kept alive by the caller's frame)."""
+    def arr(ts):
+        return torch.tensor([t.data_ptr() if t is not None else 0 for t in ts], dtype=torch.int64)
+    return (arr(vs), arr(vt), arr(lt), arr(dvs if dvs is not None else [None] * len(vs)),
+            torch.tensor(W, dtype=torch.int64))
+
+
+def kdsvd_fused_ok(g_s, g_t, k) -> bool:
+    """The one-launch post-processing serves: 2..4 stages, student and teacher
+    with equal Gram sizes k+3 <= W <= 63, k <= 8, on the GPU."""
+    return (2 <= len(g_s) <= 4 and 1 <= k <= 8 and g_s[0].is_cuda and _ext.available()
+            and all(fs.shape[-1] == ft.shape[-1] and k + 3 <= fs.shape[-1] <= 63
+                    for fs, ft in zip(g_s, g_t)))
+
+
 def kdsvd_native_ok(g_s, g_t) -> bool:
     """Every stage's SVD runs on the Gram eigensolver (graph-capturable)."""
     return all(_svd_native_ok(f) for f in list(g_s) + list(g_t))
 
 
-def kdsvd_loss(g_s, g_t, k, native: bool | None = None):
+def kdsvd_loss(g_s, g_t, k, native: bool | None = None, fused: bool | None = None):
     """`distillers/KDSVD.py:8-35`.  ``native`` (default: whenever the shapes
     allow): the SVDs through the Gram eigendecomposition (:class:`_GramEig`);
     else torch.linalg.svd (rocSOLVER, host-synchronising).  Singular vectors
@@ -504,6 +554,18 @@ def kdsvd_loss(g_s, g_t, k, native: bool | None = None):
     reference (parity is pinned on sign-invariant quantities)."""
     if native is None:
         native = kdsvd_native_ok(g_s, g_t)
+    if native and fused is not False and kdsvd_fused_ok(g_s, g_t, k):
+        lts, vts, vss = [], [], []
+        for f_s, f_t in zip(g_s, g_t):
+            N, C, H, W = f_t.shape
+            xt = f_t.detach().float().contiguous().reshape(N, C * H, W)
+            N, C, H, W = f_s.shape
+            xs = f_s.float().contiguous().reshape(N, C * H, W)
+            _, vec_s, lam_t, vec_t = _GramEig.apply(xs, xt)
+            lts.append(lam_t)
+            vts.append(vec_t)
+            vss.append(vec_s)
+        return _KdsvdPost.apply(int(k), lts, vts, *vss)
     v_sb = v_tb = None
     losses = []
     for i, (f_s, f_t) in enumerate(zip(g_s, g_t)):

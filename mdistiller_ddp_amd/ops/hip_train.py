@@ -130,6 +130,83 @@ def _region(C: int, device):
     return torch.zeros(need, dtype=torch.uint8, device=device)
 
 
+def _region_pair(C: int, device):
+    """Two adjacent zeroed regions (DOT single-pass backward: one per
+    gradient set); the second starts ``_region_bytes(C)`` bytes in."""
+    a = _arena(device)
+    need = 2 * _region_bytes(C)
+    if a.active:
+        start = a.off
+        a.off += need
+        a.high = max(a.high, a.off)
+        if a.off <= a.zeroed:
+            return a.buf[start:a.off]
+    return torch.zeros(need, dtype=torch.uint8, device=device)
+
+
+# ---------------------------------------------------------------------------
+# DOT single-pass backward.  DOT needs the task (CE) and distillation (KD)
+# gradients of every parameter separately (reference engine/dot.py:15-55,
+# trainer.py:425-432: two backward passes).  The backward is linear in the
+# cotangent, so both passes are run as ONE over two stacked cotangents: every
+# native backward of the student receives a gradient that is the first half
+# of a [2N, ...] buffer (set 0 = KD, set 1 = CE), processes both halves in the
+# same launches (dgrad over 2N images, BN backward with gridDim.y = 2 and one
+# region per set, wgrad into both gradient sets of the flat buffer) and hands
+# on the first half of a new stacked buffer.  The autograd engine only ever
+# sees the set-0 views, so its shape checks hold; any op outside the native
+# kernels that would touch such a gradient (a PyTorch add, a cast) breaks the
+# pairing, which :func:`dual_full` detects and refuses loudly.
+class _Dual:
+    __slots__ = ("gstride", "ptrs")
+
+    def __init__(self, gstride):
+        self.gstride = int(gstride)   # set-1 gradient = set-0 view + gstride floats
+        self.ptrs = set()             # bases of the stacked buffers of this backward
+
+
+_DUAL = [None]
+
+
+def set_dual(gstride) -> None:
+    """Arm (``gstride`` = float offset from the bound gradient set to the other
+    set of the flat buffer) or disarm (None) the single-pass DOT backward."""
+    _DUAL[0] = _Dual(gstride) if gstride is not None else None
+
+
+def dual_active() -> bool:
+    return _DUAL[0] is not None
+
+
+def dual_alloc(shape, dtype, device, channels_last=True):
+    """-> (stacked [2N, ...] buffer, its set-0 half)."""
+    fmt = torch.channels_last if (channels_last and len(shape) == 4) else torch.contiguous_format
+    full = torch.empty((2 * shape[0],) + tuple(shape[1:]), dtype=dtype, device=device,
+                       memory_format=fmt)
+    _DUAL[0].ptrs.add(full.data_ptr())
+    return full, full[:shape[0]]
+
+
+def dual_full(g):
+    """The stacked [2N, ...] buffer whose first half is the gradient ``g``."""
+    if g is None:
+        return None
+    D = _DUAL[0]
+    need = (g.storage_offset() + 2 * g.numel()) * g.element_size()
+    if (D is None or g.data_ptr() not in D.ptrs or g.storage_offset() != 0
+            or g.untyped_storage().nbytes() < need):
+        raise RuntimeError(
+            "DOT single-pass backward: a gradient reached a native layer without its stacked "
+            "second set (a non-native op in the student's backward?); set "
+            "RUNTIME.DOT_SINGLE_PASS=False for this model")
+    return g.as_strided((2 * g.shape[0],) + tuple(g.shape[1:]), g.stride())
+
+
+def dual_ptr(t, k: int):
+    """Device address of set ``k`` of a flat-gradient view ``t`` (set 0 = ``t``)."""
+    return t.data_ptr() + (4 * _DUAL[0].gstride if k else 0)
+
+
 def _err_word(device):
     return _arena(device).err
 
@@ -208,18 +285,22 @@ def flush_wgrad_reduces() -> None:
 
 
 def _conv_wgrad(x, dy, target, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, Kp, sp, direct,
-                cin_keep, groups):
-    """Weight gradient of one conv into ``target`` (accumulated when ``direct``)."""
-    part = torch.empty(sp * Cout * Kp, dtype=torch.float32, device=dy.device)
+                cin_keep, groups, nsets=1, gstride=0):
+    """Weight gradient of one conv into ``target`` (accumulated when ``direct``).
+    ``nsets`` = 2 (DOT single-pass backward): dy holds two stacked cotangents,
+    set 1's gradient goes ``gstride`` floats past ``target`` -- one launch."""
+    part = torch.empty(nsets * sp * Cout * Kp, dtype=torch.float32, device=x.device)
     if direct and _WG_DEFER[0] is not None:
         _ext.call("mda_conv_wgrad_nored", x, dy, part, target, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
-                  stride, pad, Kp, sp, 1.0, 1, cin_keep, groups)
-        _WG_DEFER[0].append([part.data_ptr(), target.data_ptr(), sp, Cout, Cin, KH, KW, Kp, 1,
-                             cin_keep, groups])
+                  stride, pad, Kp, sp, 1.0, 1, cin_keep, groups, nsets)
+        for k in range(nsets):
+            _WG_DEFER[0].append([part.data_ptr() + 4 * k * sp * Cout * Kp,
+                                 target.data_ptr() + 4 * k * gstride, sp, Cout, Cin, KH, KW, Kp, 1,
+                                 cin_keep, groups])
         _WG_KEEP.append(part)
         return
     _ext.call("mda_conv_wgrad", x, dy, part, target, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride,
-              pad, Kp, sp, 1.0, 1 if direct else 0, cin_keep, groups)
+              pad, Kp, sp, 1.0, 1 if direct else 0, cin_keep, groups, nsets, gstride)
 
 
 _WG_XG = [None]  # [(event, launch fn, inputs)] while a backward is captured for a wgrad graph
@@ -351,14 +432,14 @@ def _bn_bwd(dout, dpre, y, res, stats, gamma, beta, M, C, act, need_res, direct_
     if reg is not None and dpre is None:
         sums = None if direct_gb else torch.empty(2, C, dtype=torch.float32, device=dev)
         _ext.call("mda_bn_bwd_apply_reg", dout, None, y, res, stats, M, C, act, reg, dy, dres,
-                  dg, db, sums, ry, rst, rreg, vres)
+                  dg, db, sums, ry, rst, rreg, vres, 1, 0, 0, 0)
         if rl is not None:
             rl.arm(dres, rreg)
         return dy, dres, sums
     if _BN_FUSED[0]:
         sums = None if direct_gb else torch.empty(2, C, dtype=torch.float32, device=dev)
         _ext.call("mda_bn_bwd_fused", dout, None, dpre, y, res, stats, M, C, act, _region(C, dev),
-                  _err_word(dev), dy, dres, dg, db, sums, ry, rst, rreg, vres)
+                  _err_word(dev), dy, dres, dg, db, sums, ry, rst, rreg, vres, 1, 0, 0, 0)
         if rl is not None:
             rl.arm(dres, rreg)
         return dy, dres, sums
@@ -682,7 +763,14 @@ def _fork_sum(fork, g):
     if fork.park(g):
         return None
     other = fork.take()
-    return g if other is None else g + other
+    if other is None:
+        return g
+    if _DUAL[0] is not None:
+        gf, of = dual_full(g), dual_full(other)
+        full, half = dual_alloc(g.shape, g.dtype, g.device)
+        torch.add(gf, of, out=full)
+        return half
+    return g + other
 
 
 class VirtualBN:
@@ -864,6 +952,8 @@ class _ConvBNActTrain(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout, dpre):
+        if _DUAL[0] is not None:
+            return _conv_bn_backward_dual(ctx, dout, dpre)
         if ctx.kind == "dw":
             return _dw_backward(ctx, dout, dpre)
         x, wt, weight, gamma, beta, y, res, stats = ctx.saved_tensors
@@ -897,7 +987,7 @@ class _ConvBNActTrain(torch.autograd.Function):
                           Cout, KH, KW, stride, pad, KpT, tile, splits,
                           link.y if reg is not None else None, link.res if reg is not None else None,
                           link.stats if reg is not None else None, link.act if reg is not None else 0,
-                          reg, ctx.groups, link.vres if reg is not None else None)
+                          reg, ctx.groups, link.vres if reg is not None else None, 0, 0)
                 if reg is not None:
                     link.arm(dx, reg)
             elif link is not None and not parks and splits == 1:
@@ -906,7 +996,7 @@ class _ConvBNActTrain(torch.autograd.Function):
                 reg = _region(Cin, dev)
                 _ext.call("mda_conv_dgrad_bnsum_g", dy, wt, dx, part, other, N, H, W, Cin, Ho, Wo,
                           Cout, KH, KW, stride, pad, KpT, tile, splits, link.y, link.res,
-                          link.stats, link.act, reg, 1, link.vres)
+                          link.stats, link.act, reg, 1, link.vres, 0, 0)
                 link.arm(dx, reg)
             else:
                 _ext.call("mda_conv_dgrad_res", dy, wt, dx, part, other, N, H, W, Cin, Ho, Wo,
@@ -934,6 +1024,97 @@ class _ConvBNActTrain(torch.autograd.Function):
         dcb = torch.zeros(Cout, dtype=torch.float32, device=dev) if (
             ctx.cbias and ctx.needs_input_grad[9]) else None
         return dx, dw, dgamma, dbeta, dres, None, None, None, None, dcb, None
+
+
+def _bn_bwd_dual(dout, dpre, y, res, stats, gamma, beta, M, C, act, need_res, link, res_link, vres):
+    """Both gradient sets of :func:`_bn_bwd` in one launch (gridDim.y = 2):
+    (dy, dres) as set-0 halves of stacked buffers."""
+    D = _DUAL[0]
+    dev = y.device
+    if gamma.grad is None or beta.grad is None:
+        raise RuntimeError("DOT single-pass backward: BN parameters need bound flat gradients")
+    if not _BN_FUSED[0]:
+        raise RuntimeError("DOT single-pass backward needs the fused BN kernels (MDA_BN_FUSED=1)")
+    dual_full(dout)
+    if dpre is not None:
+        dual_full(dpre)
+    _, dy = dual_alloc(tuple(y.shape), torch.bfloat16, dev)
+    dres = dual_alloc(tuple(y.shape), torch.bfloat16, dev)[1] if need_res else None
+    reg = link.take(dout) if link is not None else None
+    rl = res_link if (need_res and res_link is not None and 256 % (C // 8) == 0) else None
+    rreg = _region_pair(C, dev) if rl is not None else None
+    ry, rst = (rl.y, rl.stats) if rl is not None else (None, None)
+    rb = _region_bytes(C)
+    if reg is not None and dpre is None:
+        _ext.call("mda_bn_bwd_apply_reg", dout, None, y, res, stats, M, C, act, reg, dy, dres,
+                  gamma.grad, beta.grad, None, ry, rst, rreg, vres, 2, M * C, D.gstride, rb)
+    else:
+        _ext.call("mda_bn_bwd_fused", dout, None, dpre, y, res, stats, M, C, act,
+                  _region_pair(C, dev), _err_word(dev), dy, dres, gamma.grad, beta.grad, None, ry,
+                  rst, rreg, vres, 2, M * C, D.gstride, rb)
+    if rl is not None:
+        rl.arm(dres, rreg)
+    return dy, dres
+
+
+def _conv_bn_backward_dual(ctx, dout, dpre):
+    """:meth:`_ConvBNActTrain.backward` over two stacked cotangents (see
+    :class:`_Dual`): the BN backward, dgrad (2N images, BN-sum epilogue with
+    one region per set) and both weight gradients."""
+    if ctx.kind == "dw" or ctx.gc or ctx.groups != 1 or ctx.cbias:
+        raise RuntimeError("DOT single-pass backward: depthwise / grouped convs and conv biases "
+                           "are not supported; set RUNTIME.DOT_SINGLE_PASS=False")
+    if dout is None:
+        raise RuntimeError("DOT single-pass backward: a layer output without a gradient")
+    x, wt, weight, gamma, beta, y, res, stats = ctx.saved_tensors
+    N, Cin, H, W, Cout, Ho, Wo, KH, KW, stride, pad, Kp, KpT, act = ctx.meta
+    M = N * Ho * Wo
+    dev = y.device
+    if dout.dtype != torch.bfloat16 or not dout.is_contiguous(memory_format=torch.channels_last):
+        raise RuntimeError("DOT single-pass backward: gradient not bf16 channels_last")
+    need_res = ctx.has_res and ctx.needs_input_grad[4]
+    dy, dres = _bn_bwd_dual(dout, dpre, y, res, stats, gamma, beta, M, Cout, act, need_res,
+                            ctx.bnlink, getattr(ctx, "res_link", None), getattr(ctx, "vres", None))
+    x_fork, res_fork = ctx.forks
+    if need_res:
+        dres = _fork_sum(res_fork, dres)
+    dx = None
+    if ctx.needs_input_grad[0]:
+        dx = dual_alloc((N, Cin, H, W), torch.bfloat16, dev)[1]
+        from .hip_layers import conv_plan
+        tile, splits = conv_plan(2 * N * H * W, Cin, KpT)
+        part = torch.empty(splits * 2 * N * H * W * Cin, dtype=torch.float32, device=dev) \
+            if splits > 1 else None
+        other = x_fork.take() if x_fork is not None else None
+        if other is not None:
+            dual_full(other)
+        parks = other is None and x_fork is not None and x_fork.armed
+        link = ctx.link_in
+        if link is not None and not parks and splits == 1:
+            reg = _region_pair(Cin, dev)
+            _ext.call("mda_conv_dgrad_bnsum_g", dy, wt, dx, part, other, 2 * N, H, W, Cin, Ho, Wo,
+                      Cout, KH, KW, stride, pad, KpT, tile, splits, link.y, link.res, link.stats,
+                      link.act, reg, 1, link.vres, N * H * W, _region_bytes(Cin))
+            link.arm(dx, reg)
+        else:
+            _ext.call("mda_conv_dgrad_res", dy, wt, dx, part, other, 2 * N, H, W, Cin, Ho, Wo,
+                      Cout, KH, KW, stride, pad, KpT, tile, splits)
+        if parks and x_fork.park(dx):
+            dx = None
+    if ctx.needs_input_grad[1]:
+        if weight.grad is None or not weight.grad.is_contiguous():
+            raise RuntimeError("DOT single-pass backward: conv weights need bound flat gradients")
+        Kw = ctx.kp_w
+        sp = _wgrad_splits(M, Cout, Cin, KH, KW, Kw)
+        target = weight.grad
+
+        def wg():  # both sets in one launch (x read by both)
+            _conv_wgrad(x, dy, target, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, Kw, sp,
+                        True, ctx.cin_keep, 1, 2, _DUAL[0].gstride)
+        _wgrad_launch(wg, True, x, dy)
+        notify_grad(weight)
+    notify_grad(gamma, beta)
+    return dx, None, None, None, dres, None, None, None, None, None, None
 
 
 def _bn_train_forward(y, M, C, gamma, beta, bn, residual, act, want_preact, reg=None):
@@ -1092,7 +1273,7 @@ def conv_wgrad(x, dy, weight_shape, stride, pad):
     part = torch.empty(sp * Cout * Kp, dtype=torch.float32, device=x.device)
     out = torch.empty(weight_shape, dtype=torch.float32, device=x.device)
     _ext.call("mda_conv_wgrad", x, dy, part, out, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
-              Kp, sp, 1.0, 0, 0, 1)
+              Kp, sp, 1.0, 0, 0, 1, 1, 0)
     return out
 
 

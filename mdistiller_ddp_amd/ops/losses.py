@@ -104,6 +104,20 @@ class _LogitLoss(torch.autograd.Function):
     @staticmethod
     def backward(ctx, go_ce, go_kd):
         g_ce, g_kd = ctx.saved_tensors
+        from .hip_train import _DUAL, dual_alloc
+        if _DUAL[0] is not None:
+            # DOT single-pass backward: [go_kd * g_kd ; go_ce * g_ce] stacked,
+            # the KD set first (ops/hip_train.py _Dual)
+            if ctx.mode == 0 or go_ce is None or go_kd is None:
+                raise RuntimeError("DOT single-pass backward needs both the CE and the KD loss")
+            full, half = dual_alloc(tuple(g_ce.shape), g_ce.dtype, g_ce.device)
+            B = g_ce.shape[0]
+            n = g_ce.numel()
+            _ext.call("mda_axpby", _DT[full.dtype], None, g_ce, go_kd.float().reshape(1).contiguous(),
+                      g_kd, full[:B], n)
+            _ext.call("mda_axpby", _DT[full.dtype], go_ce.float().reshape(1).contiguous(), g_ce,
+                      None, g_kd, full[B:], n)
+            return half, None, None, None, None, None, None, None, None, None, None
         out = torch.empty_like(g_ce)
         a = None if go_ce is None else go_ce.float().reshape(1).contiguous()
         b = None if (go_kd is None or ctx.mode == 0) else go_kd.float().reshape(1).contiguous()

@@ -254,6 +254,7 @@ class _PoolFC(torch.autograd.Function):
         from . import _ext
         N, C, H, W = x.shape
         J = weight.shape[0]
+        ctx.set_materialize_grads(False)  # an unused pooled output gets no zero gradient
         dt = 0 if x.dtype == torch.float32 else 1
         xc = x.contiguous(memory_format=torch.channels_last)
         pooled = torch.empty(N, C, dtype=x.dtype, device=x.device)
@@ -275,6 +276,9 @@ class _PoolFC(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dpooled, dlogits):
         from . import _ext
+        from .hip_train import _DUAL
+        if _DUAL[0] is not None:
+            return _PoolFC._backward_dual(ctx, dpooled, dlogits)
         pooled, weight, bias = ctx.saved_tensors
         N, C, H, W, J, dt, has_b = ctx.meta
         dev = pooled.device
@@ -305,6 +309,43 @@ class _PoolFC(torch.autograd.Function):
             from ..parallel.grad_reducer import notify_grad
             notify_grad(*([weight] if direct_w else []), *([bias] if direct_b else []))
         return (dx, None if direct_w else dw, None if direct_b else db)
+
+    @staticmethod
+    def _backward_dual(ctx, dpooled, dlogits):
+        """DOT single-pass backward (ops.hip_train._Dual): the head kernel once
+        per gradient set, into the two sets of the flat gradient and the two
+        halves of one stacked dx (with one BN-sum region per set)."""
+        from . import _ext
+        from .hip_train import dual_full, dual_alloc, dual_ptr, _region_pair, _region_bytes
+        pooled, weight, bias = ctx.saved_tensors
+        N, C, H, W, J, dt, has_b = ctx.meta
+        dev = pooled.device
+        if dpooled is not None or dlogits is None or dlogits.dtype != pooled.dtype:
+            raise RuntimeError("DOT single-pass backward: the head needs stacked logit gradients only")
+        dl = dual_full(dlogits)
+        if weight.grad is None or not weight.grad.is_contiguous() or (has_b and bias.grad is None):
+            raise RuntimeError("DOT single-pass backward: head parameters need bound flat gradients")
+        full, dx = dual_alloc((N, C, H, W), pooled.dtype, dev)
+        link = ctx.link
+        reg = _region_pair(C, dev) if link is not None else None
+        rb = _region_bytes(C)
+        for k in (0, 1):
+            dw = dual_ptr(weight.grad, k)
+            db = dual_ptr(bias.grad, k) if has_b else None
+            dxk = full.data_ptr() + k * N * H * W * C * full.element_size()
+            dlk = dl[k * N:(k + 1) * N]
+            if link is not None:
+                _ext.call("mda_pool_fc_bwd_bn", dt, dlk, None, pooled, weight.detach(), dw, db, dxk,
+                          N, H * W, C, J, 1, link.y, link.res, link.stats, link.act,
+                          reg.data_ptr() + k * rb, link.vres)
+            else:
+                _ext.call("mda_pool_fc_bwd", dt, dlk, None, pooled, weight.detach(), dw, db, dxk,
+                          N, H * W, C, J, 1)
+        if link is not None:
+            link.arm(dx, reg)
+        from ..parallel.grad_reducer import notify_grad
+        notify_grad(weight, *([bias] if has_b else []))
+        return dx, None, None
 
 
 def _pool_fc_native(x: torch.Tensor, fc: nn.Linear, kernel) -> bool:

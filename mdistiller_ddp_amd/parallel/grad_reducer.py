@@ -238,6 +238,10 @@ class GradReducer:
         self._armed = True
         self._cap = []
         self._cap_flush = flush
+        # the capturing stream: a bucket can complete inside a hook that the
+        # autograd engine runs with ANOTHER current stream (a leaf's
+        # AccumulateGrad runs on the stream the leaf was made on, not capturing)
+        self._cap_stream = torch.cuda.current_stream()
         self._pending = [sum(self._expected[i] for i in idx) for (_, _, idx) in self.buckets]
         _ARMED.append(self)
 
@@ -246,7 +250,7 @@ class GradReducer:
             self._cap_flush()
         from ..runtime.streams import HipEvent
         ev = HipEvent()  # (torch.cuda.Event(external=True) is refused on ROCm)
-        ev.record(external=True)
+        ev.record(external=True, stream=self._cap_stream)
         self._cap.append((b, ev))
 
     def abort_capture(self) -> None:

@@ -66,7 +66,8 @@ def main():
 
         def bwd_fused(i):
             _ext.call("mda_bn_bwd_fused", dout, None, None, y, res, stats, M, C, 1,
-                      regions[i * rb:(i + 1) * rb], err, dy, dres, dg, db, None, None, None, None, None)
+                      regions[i * rb:(i + 1) * rb], err, dy, dres, dg, db, None, None, None, None, None,
+                      1, 0, 0, 0)
 
         def bwd_old(i):
             _ext.call("mda_bn_bwd_reduce2", dout, None, y, res, stats[2], stats[3], stats[0], stats[1],

@@ -68,7 +68,7 @@ def main():
 
         def wg():
             _ext.call("mda_conv_wgrad_nored", x, dy, wpart, grad, N, H, H, Cin, Ho, Ho, Cout, k, k, s,
-                      p, Kp, sp, 1.0, 1, 0, 1)
+                      p, Kp, sp, 1.0, 1, 0, 1, 1)
 
         graphs = {}
         for name, fns, st in (("seq", (dg, wg), s1), ("d", (dg,), s1), ("w", (wg,), s2)):

@@ -214,14 +214,19 @@ def test_ofd_train_bn_teacher_not_served_natively_stays_eager():
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("typ", ["KD", "DKD"])
-def test_native_bf16_tracks_fp32_over_300_steps(typ):
+@pytest.mark.parametrize("typ,student", [("KD", "resnet8x4"), ("DKD", "resnet8x4"),
+                                         ("KD", "ShuffleV1"), ("KD", "MobileNetV2")])
+def test_native_bf16_tracks_fp32_over_300_steps(typ, student):
     """300 optimizer steps: the native bf16 hipGraph trajectory's loss tracks the
     fp32 PyTorch eager trajectory (last-50-step mean within 5 %) and both
-    actually learn (the 4 repeated synthetic batches get memorised)."""
+    actually learn (the 4 repeated synthetic batches get memorised).  The fp32
+    reference runs NCHW: this ROCm build's channels_last avg_pool2d backward
+    is shifted by a column (profiles/r4_rocm_avgpool_cl_bug.md), which is
+    ShuffleNetV1's stride-2 shortcut."""
     from mdistiller_ddp_amd.ops.backend import use_backend
     torch.manual_seed(0)
     cfg = _cfg(typ)
+    cfg.DISTILLER.STUDENT = student
     cfg.SOLVER.LR = 0.05
     d1 = build_distiller(cfg, 100, "cuda")
     d2 = copy.deepcopy(d1)
@@ -229,9 +234,10 @@ def test_native_bf16_tracks_fp32_over_300_steps(typ):
     for d, g, dt, be in ((d1, True, torch.bfloat16, "auto"), (d2, False, torch.float32, "torch")):
         with use_backend(be):
             d.train()
-            st = TrainStep(d, cfg, "cuda", use_graph=g, dtype=dt)
+            cl = be != "torch"
+            st = TrainStep(d, cfg, "cuda", use_graph=g, dtype=dt, channels_last=cl)
             st.set_epoch(30.0)
-            ld = SyntheticLoader("cifar100", 64, "cuda", steps_per_epoch=300, channels_last=True)
+            ld = SyntheticLoader("cifar100", 64, "cuda", steps_per_epoch=300, channels_last=cl)
             first = last = None
             for i, b in enumerate(ld):
                 if i == 50:

@@ -80,3 +80,22 @@ def test_kdsvd_training_graph_matches_eager():
         outs.append(st.flat.data.clone())
     rel = (outs[0] - outs[1]).norm() / outs[1].norm()
     assert rel < 5e-3, rel
+
+
+@pytest.mark.parametrize("k", [1, 2, 5])
+def test_kdsvd_fused_post_matches_torch_composition(k):
+    """csrc/kdsvd.hip (alignment + scaling + RBF + L2, forward and backward in
+    one launch each) == the PyTorch composition on the same eigensolver output."""
+    gs, gt = _feats(1, "cuda")
+    assert FL.kdsvd_fused_ok(gs, gt, k)
+    lf = FL.kdsvd_loss(gs, gt, k)  # fused (default)
+    lf.backward()
+    gf = [t.grad.clone() for t in gs]
+    for t in gs:
+        t.grad = None
+    lr = FL.kdsvd_loss(gs, gt, k, fused=False)
+    lr.backward()
+    torch.testing.assert_close(lf, lr, rtol=1e-4, atol=1e-6)
+    for a, t in zip(gf, gs):
+        rel = (a - t.grad).norm() / t.grad.norm().clamp_min(1e-30)
+        assert rel < 1e-3, rel

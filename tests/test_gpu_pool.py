@@ -76,13 +76,17 @@ def test_shuffle_tail_matches_torch(N, C3, Cx, H):
     x = torch.randn(N, Cx, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     a, b = y3.clone().requires_grad_(True), x.clone().requires_grad_(True)
     out, pre = shuffle_tail(a, b)
-    ar, br = y3.float().requires_grad_(True), x.float().requires_grad_(True)
+    # fp32 reference on the CPU, NCHW: this ROCm build's channels_last
+    # avg_pool2d backward on the GPU shifts the gradient by one column (its
+    # single-output border column lands at w = 0 instead of w = W - 1)
+    ar = y3.float().cpu().contiguous().requires_grad_(True)
+    br = x.float().cpu().contiguous().requires_grad_(True)
     pre_r = torch.cat([ar, F.avg_pool2d(br, 3, stride=2, padding=1)], 1)
     out_r = F.relu(pre_r)
-    rel = lambda u, v: ((u.float() - v.float()).norm() / v.float().norm()).item()  # noqa: E731
+    rel = lambda u, v: ((u.float().cpu() - v.float()).norm() / v.float().norm()).item()  # noqa: E731
     assert rel(pre, pre_r) < 1e-2 and rel(out, out_r) < 1e-2
     g, gp = torch.randn_like(out_r), torch.randn_like(out_r)
-    ((out.float() * g).sum() + (pre.float() * gp).sum()).backward()
+    ((out.float() * g.cuda()).sum() + (pre.float() * gp.cuda()).sum()).backward()
     ((out_r * g).sum() + (pre_r * gp).sum()).backward()
     assert rel(a.grad, ar.grad) < 1e-2
     assert rel(b.grad, br.grad) < 1e-2

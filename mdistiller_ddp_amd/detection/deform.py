@@ -48,9 +48,86 @@ def _bilinear_gather(x, py, px):
     return out
 
 
+class _DeformConvFn(torch.autograd.Function):
+    """Deformable conv on the HIP sampling kernels (ops/csrc/deform.hip): the
+    bilinear gather (and its scatter / coordinate-gradient backward) native,
+    the three GEMMs (out, dW, dcols) batched on hipBLASLt."""
+
+    @staticmethod
+    def forward(ctx, x, offset, mask, weight, bias, meta):
+        from ..ops import _ext
+        (sh, sw), (ph, pw), (dh, dw), groups, dg = meta
+        x = x.contiguous()
+        dt = x.dtype
+        off = offset.to(dt).contiguous()
+        m = mask.to(dt).contiguous() if mask is not None else None
+        N, C, H, W = x.shape
+        Cout, Cg, KH, KW = weight.shape
+        K = KH * KW
+        Ho = (H + 2 * ph - (dh * (KH - 1) + 1)) // sh + 1
+        Wo = (W + 2 * pw - (dw * (KW - 1) + 1)) // sw + 1
+        L = Ho * Wo
+        geom = torch.tensor([N, C, H, W, Ho, Wo, KH, KW, sh, sw, ph, pw, dh, dw, dg], dtype=torch.int64)
+        cols = torch.empty(N, C * K, L, dtype=dt, device=x.device)
+        code = 0 if dt == torch.float32 else 1
+        _ext.call("mda_deform_im2col", code, x, off, m, cols, geom)
+        w = weight.to(dt).reshape(groups, Cout // groups, Cg * K)
+        out = torch.matmul(w, cols.view(N, groups, Cg * K, L)).reshape(N, Cout, Ho, Wo)
+        if bias is not None:
+            out = out + bias.to(dt).view(1, Cout, 1, 1)
+        ctx.save_for_backward(x, off, m, weight, cols)
+        ctx.meta = (geom, groups, code, Ho, Wo, offset.dtype, mask.dtype if mask is not None else None,
+                    bias is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        from ..ops import _ext
+        x, off, m, weight, cols = ctx.saved_tensors
+        geom, groups, code, Ho, Wo, off_dt, mask_dt, has_b = ctx.meta
+        N, C, H, W = x.shape
+        Cout, Cg, KH, KW = weight.shape
+        K, L = KH * KW, Ho * Wo
+        dt = x.dtype
+        d = dout.to(dt).contiguous().view(N, groups, Cout // groups, L)
+        colsg = cols.view(N, groups, Cg * K, L)
+        dw = torch.matmul(d, colsg.transpose(-1, -2)).sum(0).reshape(weight.shape).to(weight.dtype)
+        w = weight.to(dt).reshape(groups, Cout // groups, Cg * K)
+        dcols = torch.matmul(w.transpose(-1, -2), d).reshape(N, C * K, L).contiguous()
+        dx = torch.zeros(N, C, H, W, dtype=torch.float32, device=x.device)
+        doff = torch.empty_like(off)
+        dmask = torch.empty_like(m) if m is not None else None
+        _ext.call("mda_deform_col2im", code, dcols, x, off, m, dx, doff, dmask, geom)
+        db = d.float().sum((0, 3)).reshape(Cout).to(weight.dtype) if has_b else None
+        return (dx.to(dt), doff.to(off_dt), dmask.to(mask_dt) if dmask is not None else None, dw,
+                db, None)
+
+
+def _native_ok(x, offset, weight):
+    from ..ops.backend import hip_enabled_for
+    return (x.dim() == 4 and hip_enabled_for(x) and x.dtype in (torch.float32, torch.bfloat16)
+            and weight.dtype in (torch.float32, torch.bfloat16))
+
+
 def deform_conv2d(x, offset, weight, bias=None, stride=1, padding=0, dilation=1, groups=1,
                   deformable_groups=1, mask=None):
-    """Deformable 2-D convolution (``mask`` given: modulated, DCN v2)."""
+    """Deformable 2-D convolution (``mask`` given: modulated, DCN v2).  On the
+    GPU the sampling runs on the HIP kernels (:class:`_DeformConvFn`), else as
+    the PyTorch gather below."""
+    if _native_ok(x, offset, weight):
+        N, C, H, W = x.shape
+        Cout, Cg, KH, KW = weight.shape
+        if C % deformable_groups or C != Cg * groups or Cout % groups:
+            raise ValueError(f"deform_conv2d: channels {C} / groups {groups} / deformable groups "
+                             f"{deformable_groups}")
+        meta = (_pair(stride), _pair(padding), _pair(dilation), groups, deformable_groups)
+        return _DeformConvFn.apply(x, offset, mask, weight, bias, meta)
+    return _deform_conv2d_torch(x, offset, weight, bias, stride, padding, dilation, groups,
+                                deformable_groups, mask)
+
+
+def _deform_conv2d_torch(x, offset, weight, bias=None, stride=1, padding=0, dilation=1, groups=1,
+                         deformable_groups=1, mask=None):
     sh, sw = _pair(stride)
     ph, pw = _pair(padding)
     dh, dw = _pair(dilation)

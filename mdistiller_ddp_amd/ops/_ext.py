@@ -56,6 +56,7 @@ SIGNATURES = {
     "mda_conv_fwd_bnacc_g": "ppppp" + "i" * 14 + "i" + "s",
     "mda_pack_conv_weights_gc": "ppp" + "i" * 7 + "s",
     "mda_channel_gather": "ppp" + "iii" + "s",
+    "mda_gather2": "pppp" + "iiii" + "s",
     "mda_vid_loss": "ppp" + "ii" + "f" + "pp" + "s",
     "mda_vid_bwd": "pppp" + "p" + "ii" + "f" + "pp" + "s",
     "mda_nst_fwd": "p" + "ii" + "p" + "s",
@@ -74,7 +75,7 @@ SIGNATURES = {
     "mda_pack_conv_weights_pad": "pp" + "i" * 6 + "s",
     "mda_wgrad_plan": "iiiiiip",
     "mda_pack_conv_weights": "ppp" + "i" * 6 + "s",
-    "mda_pack_conv_weights_multi": "piis",
+    "mda_pack_conv_weights_multi": "piiis",
     "mda_pack_tiles": "iiiip",
     # depthwise 3x3 conv (csrc/dwconv.hip)
     "mda_dw_pack": "pppiis",
@@ -126,6 +127,8 @@ SIGNATURES = {
     "mda_roi_align_fwd": "ii" + "pppppp" + "iiiiii" + "s",
     "mda_roi_align_bwd": "ii" + "pppppp" + "iiiiii" + "s",
     "mda_nms": "pifpipps",
+    "mda_deform_im2col": "i" + "pppp" + "p" + "s",
+    "mda_deform_col2im": "i" + "pppp" + "ppp" + "p" + "s",
     # data augmentation (csrc/aug.hip)
     "mda_crop_flip_norm": "ppppppp" + "iiiiii" + "s",
     # optimizers (csrc/optim.hip)

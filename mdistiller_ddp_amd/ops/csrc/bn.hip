@@ -571,6 +571,7 @@ MDA_API int mda_bn_finalize(const float* partial, int64_t nblk, int64_t M, int64
 // apply) launches per layer before; dout2 folds the gradient add of a
 // residual fork (two consumers of one activation) into the same pass.
 #include "bnslot.h"
+#include <cstdlib>
 
 namespace {
 
@@ -1228,7 +1229,14 @@ MDA_API int mda_bn_bwd_fused(const void* dout, const void* dout2, const void* dp
   // at most one block per CU over BOTH sets: every block of each set's grid
   // barrier is resident
   const int maxb = std::max(1, num_cus() / (int)nsets);
-  const int nb = (int)std::min<int64_t>(rows_iter, maxb);
+  // MDA_BN_BWD_PER = p > 1: small layers hold p row iterations per thread on
+  // rows_iter / p blocks -- a grid barrier over fewer blocks (A/B knob)
+  static const int min_per = [] {
+    const char* e = getenv("MDA_BN_BWD_PER");
+    const int v = e ? atoi(e) : 1;
+    return v < 1 ? 1 : (v > 8 ? 8 : v);
+  }();
+  const int nb = (int)std::min<int64_t>((rows_iter + min_per - 1) / min_per, maxb);
   const int64_t per = (rows_iter + nb - 1) / nb;     // row iterations per thread
   const unsigned ns = (unsigned)nsets;
   if (per > 8) {

@@ -1090,6 +1090,7 @@ conv_halo_kernel(const ConvParams p) {
   const int n0 = blockIdx.y * BN;
   const uint32_t wave_off = (uint32_t)__builtin_amdgcn_readfirstlane(wid) * 1024u;
   const bf16_t* const zero = (const bf16_t*)g_zero16;
+  stamp(p, 0);
 
   // block geometry: IMGS images of RH output rows each
   const int W = p.W, H = p.H;
@@ -1209,6 +1210,7 @@ conv_halo_kernel(const ConvParams p) {
   for (int j = 0; j < HALO_PIECES; ++j) issue_piece(c_begin, 0, j);
 #pragma unroll
   for (int s0 = 0; s0 < RING - 1; ++s0) issue_b(s0, s0);
+  stamp(p, 1);
   int pbuf = 0, bbuf = 0, step = 0;
   for (int cc = c_begin; cc < c_end; ++cc) {
 #pragma unroll
@@ -1228,6 +1230,7 @@ conv_halo_kernel(const ConvParams p) {
         if (tap == 0) vm_wait_barrier<2 * BLOADS>();
         else vm_wait_barrier<(RING - 2) * BLOADS>();
       }
+      if (step == 0) stamp(p, 2);
       int nb = bbuf + RING - 1;                  // (step + RING - 1) % RING
       if (nb >= RING) nb -= RING;
       issue_b(step + RING - 1, nb);
@@ -1239,7 +1242,12 @@ conv_halo_kernel(const ConvParams p) {
     pbuf ^= 1;
   }
   vm_wait_barrier<0>();
+  stamp(p, 3);
   conv_epilogue<BM, BN>(p, acc, smem, m0, n0, PB, ParClass{}, false, pre);
+  if (p.stamps != nullptr) {
+    __syncthreads();
+    stamp(p, 4);
+  }
 }
 
 // Single-chunk (Cin == 64) halo variant: the block's one patch is staged

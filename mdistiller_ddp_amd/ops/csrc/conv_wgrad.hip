@@ -627,10 +627,15 @@ __device__ __forceinline__ int pack_tile_dim(int khkw) {
   return khkw == 1 ? 32 : (khkw <= 9 ? 16 : 8);
 }
 
+// Dynamic LDS, sized on the host for THIS table (its rows and its largest
+// tile): a CIFAR student's table + a 3x3 tile is ~10 KB, so many blocks share
+// a CU and their load -> transpose -> store chains overlap (the static
+// worst-case 72 KB allowed two blocks per CU: 22 us for a ResNet8x4).
 __global__ void __launch_bounds__(256)
 pack_multi_kernel(const int64_t* __restrict__ table, int L) {
-  __shared__ int64_t tb[PACK_MAX_LAYERS * PACK_FIELDS];
-  __shared__ float sm[PACK_LDS_FLOATS];
+  extern __shared__ __attribute__((aligned(16))) char pack_dyn[];
+  int64_t* tb = (int64_t*)pack_dyn;
+  float* sm = (float*)(pack_dyn + ((L * PACK_FIELDS * 8 + 15) / 16) * 16);
   for (int i = threadIdx.x; i < L * PACK_FIELDS; i += blockDim.x) tb[i] = table[i];
   __syncthreads();
   int l = 0;
@@ -742,11 +747,19 @@ MDA_API int mda_pack_conv_weights_pad(const float* w, void* wf, int64_t Cout, in
 
 // total = number of tiles over all layers (see pack_multi_kernel; mda_pack_tiles
 // gives a layer's count).  The packed buffers' padding must already be zero.
+// khkw_max: the largest KH*KW of the table's layers (sizes the LDS tile).
 MDA_API int mda_pack_conv_weights_multi(const int64_t* table, int64_t L, int64_t total,
-                                        hipStream_t st) {
-  if (L <= 0 || L > PACK_MAX_LAYERS || total <= 0 || total > (1 << 30))
+                                        int64_t khkw_max, hipStream_t st) {
+  if (L <= 0 || L > PACK_MAX_LAYERS || total <= 0 || total > (1 << 30) || khkw_max < 1 ||
+      khkw_max > 49)
     return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(pack_multi_kernel, dim3((unsigned)total), dim3(256), 0, st, table, (int)L);
+  int tile_floats = 256;  // a depthwise row's tile needs none; keep a floor
+  for (int kk = 1; kk <= khkw_max; ++kk) {
+    const int T = kk == 1 ? 32 : (kk <= 9 ? 16 : 8);
+    tile_floats = std::max(tile_floats, T * (T * kk + 1));
+  }
+  const size_t lds = ((size_t)L * PACK_FIELDS * 8 + 15) / 16 * 16 + (size_t)tile_floats * 4;
+  hipLaunchKernelGGL(pack_multi_kernel, dim3((unsigned)total), dim3(256), lds, st, table, (int)L);
   MDA_CHECK_LAUNCH();
 }
 

@@ -194,6 +194,47 @@ channel_gather_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
 }
 }  // namespace
 
+// Two-source channel gather: y[m, c] = map[c] < 0 ? 0 : src_{map[c] >> 16}[m, map[c] & 0xffff]
+// with row strides ld0 / ld1 (elements) -- ShuffleNetV2's concat + channel
+// shuffle + split into the next unit's two (channel-padded) halves, and its
+// backward (the inverse maps, one call per source gradient).
+namespace {
+__global__ void __launch_bounds__(256)
+gather2_kernel(const bf16_t* __restrict__ x0, const bf16_t* __restrict__ x1, bf16_t* __restrict__ y,
+               const int* __restrict__ map, int64_t M, int ld0, int ld1, int Cy) {
+  __shared__ int smap[2048];
+  for (int c = threadIdx.x; c < Cy; c += blockDim.x) smap[c] = map[c];
+  __syncthreads();
+  const int64_t total2 = M * Cy / 2;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total2;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = (i * 2) / Cy;
+    const int c = (int)(i * 2 - m * Cy);
+    uint32_t v[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int e = smap[c + h];
+      v[h] = 0u;
+      if (e >= 0) {
+        const int src = e >> 16, ch = e & 0xffff;
+        v[h] = src ? (uint32_t)x1[m * ld1 + ch] : (uint32_t)x0[m * ld0 + ch];
+      }
+    }
+    *(uint32_t*)(y + i * 2) = v[0] | (v[1] << 16);
+  }
+}
+}  // namespace
+
+MDA_API int mda_gather2(const void* x0, const void* x1, void* y, const int* map, int64_t M,
+                        int64_t ld0, int64_t ld1, int64_t Cy, hipStream_t st) {
+  if (Cy % 2 || Cy > 2048 || M < 1) return (int)hipErrorInvalidValue;
+  int64_t blocks = (M * Cy / 2 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(gather2_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const bf16_t*)x0,
+                     (const bf16_t*)x1, (bf16_t*)y, map, M, (int)ld0, (int)ld1, (int)Cy);
+  MDA_CHECK_LAUNCH();
+}
+
 MDA_API int mda_channel_gather(const void* x, void* y, const int* map, int64_t M, int64_t Cx,
                                int64_t Cy, hipStream_t st) {
   if (Cy % 2 || Cy > 2048 || Cx <= 0 || M <= 0) return (int)hipErrorInvalidValue;

@@ -539,6 +539,7 @@ class PackCache:
             start += n
         self._table = torch.tensor(rows, dtype=torch.int64).to(device)
         self._total = start
+        self._khkw = max(r[5] * r[6] for r in rows)
         self._ptrs = [e["weight"].data_ptr() for e in self.entries.values()]
         self._dirty = False
 
@@ -554,7 +555,8 @@ class PackCache:
             if capturing:
                 return False
             self._build(device)
-        _ext.call("mda_pack_conv_weights_multi", self._table, self._table.shape[0], self._total)
+        _ext.call("mda_pack_conv_weights_multi", self._table, self._table.shape[0], self._total,
+                  self._khkw)
         self.armed = True
         return True
 

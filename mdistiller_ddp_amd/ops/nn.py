@@ -184,6 +184,100 @@ def channel_gather(x: torch.Tensor, fmap: torch.Tensor, bmap: torch.Tensor) -> t
     return y * (fmap >= 0).to(y.dtype).reshape(1, -1, 1, 1)
 
 
+class _Gather2(torch.autograd.Function):
+    """Up to two NHWC bf16 outputs gathered channel-wise from up to two
+    sources (csrc/pool.hip mda_gather2): ``y_d[:, j] = src_{f_d[j] >> 16}[:,
+    f_d[j] & 0xffff]`` (0 where f_d[j] < 0).  The maps are injective, so the
+    backward is the same gather with the inverse maps ``b_s[c] = (d << 16) | j``
+    -- one launch per source gradient, no autograd add."""
+
+    @staticmethod
+    def forward(ctx, x0, x1, fmaps, bmaps, couts):
+        from . import _ext
+        srcs = [t.contiguous(memory_format=torch.channels_last) for t in (x0, x1) if t is not None]
+        a = srcs[0]
+        b = srcs[1] if len(srcs) > 1 else srcs[0]
+        n, _, h, w = a.shape
+        ys = []
+        for f, c in zip(fmaps, couts):
+            y = torch.empty((n, c, h, w), dtype=torch.bfloat16, device=a.device,
+                            memory_format=torch.channels_last)
+            _ext.call("mda_gather2", a, b, y, f, n * h * w, a.shape[1], b.shape[1], c)
+            ys.append(y)
+        ctx.meta = (bmaps, [t.shape[1] for t in srcs], couts, n, h, w)
+        return tuple(ys) if len(ys) > 1 else ys[0]
+
+    @staticmethod
+    def backward(ctx, *dys):
+        from . import _ext
+        bmaps, cins, couts, n, h, w = ctx.meta
+        dys = [d.to(torch.bfloat16).contiguous(memory_format=torch.channels_last) if d is not None
+               else torch.zeros((n, c, h, w), dtype=torch.bfloat16, device=bmaps[0].device,
+                                memory_format=torch.channels_last) for d, c in zip(dys, couts)]
+        a = dys[0]
+        b = dys[1] if len(dys) > 1 else dys[0]
+        grads = []
+        for k, (bm, c) in enumerate(zip(bmaps, cins)):
+            if not ctx.needs_input_grad[k]:
+                grads.append(None)
+                continue
+            dx = torch.empty((n, c, h, w), dtype=torch.bfloat16, device=a.device,
+                             memory_format=torch.channels_last)
+            _ext.call("mda_gather2", a, b, dx, bm, n * h * w, a.shape[1], b.shape[1], c)
+            grads.append(dx)
+        while len(grads) < 2:
+            grads.append(None)
+        return grads[0], grads[1], None, None, None
+
+
+class ChannelRoute:
+    """A fixed channel routing ``outputs[d][j] <- sources[s][c]`` (or zero) for
+    :func:`gather2`: device maps for the HIP kernel + index maps for the
+    PyTorch fallback.  ``routes``: per output, a list of (s, c) or None."""
+
+    def __init__(self, routes, cins):
+        self.cins = list(cins)
+        self.couts = [len(r) for r in routes]
+        enc = lambda sc: -1 if sc is None else (sc[0] << 16) | sc[1]  # noqa: E731
+        self.f = [torch.tensor([enc(sc) for sc in r], dtype=torch.int32) for r in routes]
+        inv = [[-1] * c for c in self.cins]
+        for d, r in enumerate(routes):
+            for j, sc in enumerate(r):
+                if sc is not None:
+                    if inv[sc[0]][sc[1]] != -1:
+                        raise ValueError("ChannelRoute: a source channel is routed twice")
+                    inv[sc[0]][sc[1]] = (d << 16) | j
+        self.b = [torch.tensor(v, dtype=torch.int32) for v in inv]
+        # fallback: index into cat(sources + [zero column])
+        off = [0]
+        for c in self.cins:
+            off.append(off[-1] + c)
+        self.idx = [torch.tensor([off[-1] if sc is None else off[sc[0]] + sc[1] for sc in r],
+                                 dtype=torch.long) for r in routes]
+        self._dev = {}
+
+    def maps(self, device):
+        key = str(device)
+        v = self._dev.get(key)
+        if v is None:
+            v = self._dev[key] = ([t.to(device) for t in self.f], [t.to(device) for t in self.b],
+                                  [t.to(device) for t in self.idx])
+        return v
+
+
+def gather2(route: ChannelRoute, x0, x1=None):
+    """Apply ``route`` to the sources; returns one tensor or a tuple of two."""
+    f, b, idx = route.maps(x0.device)
+    srcs = [t for t in (x0, x1) if t is not None]
+    if (hip_enabled_for(x0) and all(t.dtype == torch.bfloat16 for t in srcs)
+            and all(c % 2 == 0 for c in route.couts)):
+        return _Gather2.apply(x0, x1, f, b, route.couts)
+    z = torch.zeros_like(srcs[0][:, :1])
+    cat = torch.cat(srcs + [z], 1)
+    ys = [cat.index_select(1, i) for i in idx]
+    return tuple(ys) if len(ys) > 1 else ys[0]
+
+
 class _ShuffleTail(torch.autograd.Function):
     """ShuffleNetV1 stride-2 unit tail ``pre = cat([y3, avgpool3x3s2(x)]);
     out = relu(pre)`` in one HIP pass, backward in one more (csrc/pool.hip).

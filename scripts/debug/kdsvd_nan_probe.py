@@ -22,17 +22,18 @@ cfg.DISTILLER.RANDOM_TEACHER = True
 d1 = build_distiller(cfg, 100, "cuda")
 d2 = copy.deepcopy(d1)
 orig = FL.kdsvd_loss
-for d, fused, dt in ((d1, True, torch.float32), (d2, False, torch.float32)):
+d3 = copy.deepcopy(d1)
+for d, fused, g in ((d1, True, True), (d2, False, True), (d3, True, False)):
     FL.kdsvd_loss = (lambda *a, _f=fused, **k: orig(*a, fused=_f, **k))
     d.train()
-    st = TrainStep(d, cfg, "cuda", use_graph=False, dtype=dt)
+    st = TrainStep(d, cfg, "cuda", use_graph=g, dtype=torch.float32)
     st.set_epoch(1.0)
     ld = SyntheticLoader("cifar100", 16, "cuda", steps_per_epoch=6, channels_last=True)
     for i, b in enumerate(ld):
         preds, losses = st.step(b)
         torch.cuda.synchronize()
         g = st.flat.grads
-        print(f"fused={fused} step {i}: loss_kd {float(losses['loss_kd']):.5g} ce {float(losses['loss_ce']):.4g} "
+        print(f"fused={fused} graph={g} step {i}: loss_kd {float(losses['loss_kd']):.5g} ce {float(losses['loss_ce']):.4g} "
               f"grad finite {bool(torch.isfinite(g).all())} |g| {float(torch.nan_to_num(g).norm()):.4g} "
               f"params finite {bool(torch.isfinite(st.flat.data).all())}", flush=True)
 FL.kdsvd_loss = orig

@@ -564,6 +564,7 @@ class TrainStep:
             feed = self._capture_teacher_feed(static, pool, s)
             if self.teacher_split:
                 feed.mode = "use"  # the step graph reads X; the teacher is a graph of its own
+                feed.track = set()  # which X the step graph reads (only those are refreshed)
         try:
             self._capture_step(static, pool, s)
         finally:
@@ -584,6 +585,7 @@ class TrainStep:
         ts.wait_stream(torch.cuda.current_stream())
         t_list, x_list = feed.capture_pipe(self.distiller.teacher, g, torch.cuda.graph_pool_handle(), ts,
                                            lambda: _autocast(self.device, self.dtype))
+        feed.track = None
         self._tsplit = (g, t_list, x_list, ts, torch.cuda.Event(), torch.cuda.Event())
         self._tp_inflight = False
         self._x_for = None

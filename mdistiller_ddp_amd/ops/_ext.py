@@ -56,7 +56,7 @@ SIGNATURES = {
     "mda_conv_fwd_bnacc_g": "ppppp" + "i" * 14 + "i" + "s",
     "mda_pack_conv_weights_gc": "ppp" + "i" * 7 + "s",
     "mda_channel_gather": "ppp" + "iii" + "s",
-    "mda_gather2": "pppp" + "iiii" + "s",
+    "mda_gather2": "pppp" + "i" + "ppi" + "iii" + "s",
     "mda_vid_loss": "ppp" + "ii" + "f" + "pp" + "s",
     "mda_vid_bwd": "pppp" + "p" + "ii" + "f" + "pp" + "s",
     "mda_nst_fwd": "p" + "ii" + "p" + "s",

@@ -194,16 +194,20 @@ channel_gather_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
 }
 }  // namespace
 
-// Two-source channel gather: y[m, c] = map[c] < 0 ? 0 : src_{map[c] >> 16}[m, map[c] & 0xffff]
-// with row strides ld0 / ld1 (elements) -- ShuffleNetV2's concat + channel
-// shuffle + split into the next unit's two (channel-padded) halves, and its
-// backward (the inverse maps, one call per source gradient).
+// Two-source, two-destination channel gather:
+//   y_d[m, c] = map_d[c] < 0 ? 0 : src_{map_d[c] >> 16}[m, map_d[c] & 0xffff]
+// (row strides ld0 / ld1, destinations dense with Cy0 / Cy1 channels; Cy1 may
+// be 0) -- ShuffleNetV2's concat + channel shuffle + split into the next
+// unit's two channel-padded halves in ONE launch, and its backward (the
+// inverse maps: both source gradients from both output gradients, one launch).
 namespace {
 __global__ void __launch_bounds__(256)
-gather2_kernel(const bf16_t* __restrict__ x0, const bf16_t* __restrict__ x1, bf16_t* __restrict__ y,
-               const int* __restrict__ map, int64_t M, int ld0, int ld1, int Cy) {
-  __shared__ int smap[2048];
-  for (int c = threadIdx.x; c < Cy; c += blockDim.x) smap[c] = map[c];
+gather2_kernel(const bf16_t* __restrict__ x0, const bf16_t* __restrict__ x1, bf16_t* __restrict__ y0,
+               bf16_t* __restrict__ y1, const int* __restrict__ map0, const int* __restrict__ map1,
+               int64_t M, int ld0, int ld1, int Cy0, int Cy1) {
+  __shared__ int smap[4096];
+  const int Cy = Cy0 + Cy1;
+  for (int c = threadIdx.x; c < Cy; c += blockDim.x) smap[c] = c < Cy0 ? map0[c] : map1[c - Cy0];
   __syncthreads();
   const int64_t total2 = M * Cy / 2;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total2;
@@ -220,18 +224,22 @@ gather2_kernel(const bf16_t* __restrict__ x0, const bf16_t* __restrict__ x1, bf1
         v[h] = src ? (uint32_t)x1[m * ld1 + ch] : (uint32_t)x0[m * ld0 + ch];
       }
     }
-    *(uint32_t*)(y + i * 2) = v[0] | (v[1] << 16);
+    bf16_t* dst = c < Cy0 ? y0 + m * Cy0 + c : y1 + m * Cy1 + (c - Cy0);
+    *(uint32_t*)dst = v[0] | (v[1] << 16);
   }
 }
 }  // namespace
 
-MDA_API int mda_gather2(const void* x0, const void* x1, void* y, const int* map, int64_t M,
-                        int64_t ld0, int64_t ld1, int64_t Cy, hipStream_t st) {
-  if (Cy % 2 || Cy > 2048 || M < 1) return (int)hipErrorInvalidValue;
-  int64_t blocks = (M * Cy / 2 + 255) / 256;
+MDA_API int mda_gather2(const void* x0, const void* x1, void* y0, const int* map0, int64_t Cy0,
+                        void* y1, const int* map1, int64_t Cy1, int64_t M, int64_t ld0, int64_t ld1,
+                        hipStream_t st) {
+  if (Cy0 % 2 || Cy1 % 2 || Cy0 < 2 || Cy0 + Cy1 > 4096 || M < 1 || (Cy1 > 0 && !y1))
+    return (int)hipErrorInvalidValue;
+  int64_t blocks = (M * (Cy0 + Cy1) / 2 + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(gather2_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const bf16_t*)x0,
-                     (const bf16_t*)x1, (bf16_t*)y, map, M, (int)ld0, (int)ld1, (int)Cy);
+                     (const bf16_t*)x1, (bf16_t*)y0, (bf16_t*)y1, map0, map1, M, (int)ld0, (int)ld1,
+                     (int)Cy0, (int)Cy1);
   MDA_CHECK_LAUNCH();
 }
 

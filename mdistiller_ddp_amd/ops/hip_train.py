@@ -638,7 +638,9 @@ def train_supported(x, conv, bn) -> bool:
     # a conv bias in front of a training BN only shifts the batch mean (BN
     # removes it; its gradient sum_m dy is exactly 0): the conv runs without it
     # and the running mean takes the shift (_ConvBNActTrain)
-    if conv.bias is not None and (conv.groups != 1 or conv.bias.dtype != torch.float32):
+    # (depthwise too: Tiny-ImageNet MobileNetV2's depthwise convs carry biases)
+    if conv.bias is not None and ((conv.groups != 1 and not is_depthwise(conv))
+                                  or conv.bias.dtype != torch.float32):
         return False
     if conv.groups != 1:
         if is_depthwise(conv):
@@ -821,8 +823,14 @@ class _ConvBNActTrain(torch.autograd.Function):
         stride, pad, act = meta[:3]
         if len(meta) > 3 and meta[3] == "dw":
             ctx.forks = (None, None)
-            return _dw_forward(ctx, x, weight, gamma, beta, residual, stride, pad, act, bn,
-                               want_preact)
+            ctx.cbias = cbias is not None
+            res = _dw_forward(ctx, x, weight, gamma, beta, residual, stride, pad, act, bn,
+                              want_preact)
+            if cbias is not None:
+                # BN(y + b) == BN(y) in training; the running mean (updated by the
+                # BN kernel above) tracks mean(y) + b (same algebra as the dense path)
+                bn.running_mean.add_(cbias.detach(), alpha=float(bn.momentum))
+            return res
         ctx.kind = "dense"
         ctx.forks = tuple(f.join() if f is not None else None for f in forks)
         G = meta[4] if len(meta) > 4 and meta[3] == "grouped" else 1

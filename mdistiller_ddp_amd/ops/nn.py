@@ -198,14 +198,14 @@ class _Gather2(torch.autograd.Function):
         a = srcs[0]
         b = srcs[1] if len(srcs) > 1 else srcs[0]
         n, _, h, w = a.shape
-        ys = []
-        for f, c in zip(fmaps, couts):
-            y = torch.empty((n, c, h, w), dtype=torch.bfloat16, device=a.device,
-                            memory_format=torch.channels_last)
-            _ext.call("mda_gather2", a, b, y, f, n * h * w, a.shape[1], b.shape[1], c)
-            ys.append(y)
+        ys = [torch.empty((n, c, h, w), dtype=torch.bfloat16, device=a.device,
+                          memory_format=torch.channels_last) for c in couts]
+        two = len(ys) > 1
+        _ext.call("mda_gather2", a, b, ys[0], fmaps[0], couts[0], ys[1] if two else None,
+                  fmaps[1] if two else None, couts[1] if two else 0, n * h * w, a.shape[1],
+                  b.shape[1])
         ctx.meta = (bmaps, [t.shape[1] for t in srcs], couts, n, h, w)
-        return tuple(ys) if len(ys) > 1 else ys[0]
+        return tuple(ys) if two else ys[0]
 
     @staticmethod
     def backward(ctx, *dys):
@@ -216,17 +216,18 @@ class _Gather2(torch.autograd.Function):
                                 memory_format=torch.channels_last) for d, c in zip(dys, couts)]
         a = dys[0]
         b = dys[1] if len(dys) > 1 else dys[0]
-        grads = []
-        for k, (bm, c) in enumerate(zip(bmaps, cins)):
-            if not ctx.needs_input_grad[k]:
-                grads.append(None)
-                continue
-            dx = torch.empty((n, c, h, w), dtype=torch.bfloat16, device=a.device,
-                             memory_format=torch.channels_last)
-            _ext.call("mda_gather2", a, b, dx, bm, n * h * w, a.shape[1], b.shape[1], c)
-            grads.append(dx)
-        while len(grads) < 2:
-            grads.append(None)
+        want = [k for k in range(len(cins)) if ctx.needs_input_grad[k]]
+        grads = [None, None]
+        if want:
+            outs = [torch.empty((n, cins[k], h, w), dtype=torch.bfloat16, device=a.device,
+                                memory_format=torch.channels_last) for k in want]
+            two = len(want) > 1
+            # both source gradients from both output gradients: one launch
+            _ext.call("mda_gather2", a, b, outs[0], bmaps[want[0]], cins[want[0]],
+                      outs[1] if two else None, bmaps[want[1]] if two else None,
+                      cins[want[1]] if two else 0, n * h * w, a.shape[1], b.shape[1])
+            for k, o in zip(want, outs):
+                grads[k] = o
         return grads[0], grads[1], None, None, None
 
 
@@ -270,7 +271,8 @@ def gather2(route: ChannelRoute, x0, x1=None):
     f, b, idx = route.maps(x0.device)
     srcs = [t for t in (x0, x1) if t is not None]
     if (hip_enabled_for(x0) and all(t.dtype == torch.bfloat16 for t in srcs)
-            and all(c % 2 == 0 for c in route.couts)):
+            and all(c % 2 == 0 for c in route.couts + route.cins)
+            and sum(route.couts) <= 4096 and sum(route.cins) <= 4096):
         return _Gather2.apply(x0, x1, f, b, route.couts)
     z = torch.zeros_like(srcs[0][:, :1])
     cat = torch.cat(srcs + [z], 1)

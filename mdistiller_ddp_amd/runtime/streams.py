@@ -170,6 +170,51 @@ def run_teacher(teacher, image, train_bn: bool = False):
     return run_teacher_async(teacher, image, train_bn).get()
 
 
+class _TrackDict(dict):
+    """A teacher-output dict that records which entries are read
+    (TeacherFeed.track): reading a key marks EVERY tensor under it (a list
+    handed on may be consumed by C++ code -- torch.cat, zip -- that no Python
+    hook sees, so the granularity stays the key: FitNet reads "feats", not
+    "preact_feats")."""
+
+    def __init__(self, items, used):
+        super().__init__(items)
+        self._used = used
+
+    def _mark(self, v):
+        for t in _tensors(v, []):
+            self._used.add(id(t))
+        return v
+
+    def __getitem__(self, k):
+        return self._mark(super().__getitem__(k))
+
+    def get(self, k, default=None):
+        return self._mark(super().get(k, default))
+
+    def values(self):
+        return [self._mark(v) for v in super().values()]
+
+    def items(self):
+        return [(k, self._mark(v)) for k, v in super().items()]
+
+    def __iter__(self):
+        return iter(list(self.keys()))
+
+
+def _track_struct(obj, used):
+    """Wrap the dicts of a teacher-output structure; every tensor outside a
+    dict (the logits) counts as read."""
+    if isinstance(obj, torch.Tensor):
+        used.add(id(obj))
+        return obj
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_track_struct(o, used) for o in obj)
+    if isinstance(obj, dict):
+        return _TrackDict(obj, used)
+    return obj
+
+
 def _clone_struct(obj):
     if isinstance(obj, torch.Tensor):
         return obj.detach().clone(memory_format=torch.preserve_format)
@@ -217,6 +262,10 @@ class TeacherFeed:
         self.X = None
         self.logits_only = logits_only
         self._pending = None
+        # while a set: ids of the X tensors the consumer reads (the split
+        # teacher graph's per-step X <- T copy then skips the others: FitNet
+        # reads one teacher feature map of the ten the teacher returns)
+        self.track = None
 
     def _keep(self, out):
         if self.logits_only and isinstance(out, (list, tuple)) and len(out) == 2:
@@ -238,6 +287,8 @@ class TeacherFeed:
                 raise RuntimeError("TeacherFeed: pipelined step before the buffers were primed")
             if self.mode == "pipe":
                 self.prefetch(teacher)
+            if self.track is not None:
+                return TeacherOutput(_track_struct(self.X, self.track))
             return TeacherOutput(self.X)
         return run_teacher_async(teacher, image)
 
@@ -280,6 +331,9 @@ class TeacherFeed:
         t_list, x_list = _tensors(T, []), _tensors(self.X, [])
         if len(t_list) != len(x_list) or any(a.shape != b.shape for a, b in zip(t_list, x_list)):
             raise RuntimeError("TeacherFeed: pipelined teacher outputs do not match the primed buffers")
+        if self.track:
+            keep = [k for k, x in enumerate(x_list) if id(x) in self.track]
+            t_list, x_list = [t_list[k] for k in keep], [x_list[k] for k in keep]
         return t_list, x_list
 
     def commit(self) -> None:

@@ -100,19 +100,24 @@ def test_dgrad_wgrad_kernels_exact_inputs(shape):
         assert rel_x < 1e-2, rel_x
 
 
-@pytest.mark.parametrize("name", ["resnet8x4", "wrn_16_2", "vgg8", "MobileNetV2", "ShuffleV1", "ShuffleV2"])
+@pytest.mark.parametrize("name", ["resnet8x4", "wrn_16_2", "vgg8", "MobileNetV2", "ShuffleV1", "ShuffleV2",
+                                  "tiny_MobileNetV2", "tiny_ShuffleV2"])
 def test_student_train_step_uses_native_path(name):
     """A full student training forward/backward through the native path vs an
     fp32 PyTorch reference: its gradient error must be in the same band as the
-    stock bf16 (MIOpen) path's."""
-    from mdistiller_ddp_amd.models import cifar_model_dict
+    stock bf16 (MIOpen) path's, and so must every BN's running statistics
+    (Tiny-ImageNet MobileNetV2: depthwise convs with biases, folded into the
+    following training BN)."""
+    from mdistiller_ddp_amd.models import cifar_model_dict, tiny_imagenet_model_dict
     from mdistiller_ddp_amd.ops.backend import use_backend
     torch.manual_seed(0)
-    m1 = cifar_model_dict[name][0](num_classes=100).cuda().to(memory_format=torch.channels_last)
+    tiny = name.startswith("tiny_")
+    table, hw, ncls = (tiny_imagenet_model_dict, 64, 200) if tiny else (cifar_model_dict, 32, 100)
+    m1 = table[name[5:] if tiny else name][0](num_classes=ncls).cuda().to(memory_format=torch.channels_last)
     m2 = copy.deepcopy(m1)
     m3 = copy.deepcopy(m1)
-    x = torch.randn(32, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
-    y = torch.randint(0, 100, (32,), device="cuda")
+    x = torch.randn(32, 3, hw, hw, device="cuda").contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, ncls, (32,), device="cuda")
     grads = []
     for m, be, amp in ((m1, "hip", True), (m2, "torch", True), (m3, "torch", False)):
         with use_backend(be), torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
@@ -124,6 +129,11 @@ def test_student_train_step_uses_native_path(name):
     e_native = ((grads[0] - ref).norm() / ref.norm()).item()
     e_miopen = ((grads[1] - ref).norm() / ref.norm()).item()
     assert e_native < max(2.0 * e_miopen, 0.05), (e_native, e_miopen)
+    rm = [torch.cat([b.float().reshape(-1) for n, b in m.named_buffers() if "running" in n])
+          for m in (m1, m2, m3)]
+    r_native = ((rm[0] - rm[2]).norm() / rm[2].norm()).item()
+    r_miopen = ((rm[1] - rm[2]).norm() / rm[2].norm()).item()
+    assert r_native < max(2.0 * r_miopen, 1e-2), (r_native, r_miopen)
 
 
 @pytest.mark.parametrize("student", ["resnet8x4", "MobileNetV2"])

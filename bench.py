@@ -33,6 +33,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")  # see mdistiller_ddp_amd/__init__.py
 import socket
 import subprocess
 import sys

@@ -12,6 +12,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")  # see mdistiller_ddp_amd/__init__.py
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -141,6 +141,30 @@ def _autocast(device, dtype):
     return contextlib.nullcontext()
 
 
+def _multi_copy(dst, src):
+    """``dst[i].copy_(src[i])`` for same-shape, same-dtype, same-layout device
+    tensors in ONE launch (ops/csrc/optim.hip mda_multi_copy); otherwise (or
+    beyond 16 pairs) torch._foreach_copy_ (one blit per tensor)."""
+    ok = (0 < len(dst) <= 16 and all(
+        d.is_cuda and s.is_cuda and d.dtype == s.dtype and d.shape == s.shape
+        and d.stride() == s.stride() and d.is_contiguous(memory_format=_fmt(d))
+        for d, s in zip(dst, src)))
+    if ok:
+        from ..ops import _ext
+        if _ext.available():
+            tab = torch.tensor([[s.data_ptr(), d.data_ptr(), d.numel() * d.element_size()]
+                                for d, s in zip(dst, src)], dtype=torch.int64)
+            _ext.call("mda_multi_copy", tab, len(dst))
+            return
+    torch._foreach_copy_(dst, src)
+
+
+def _fmt(t):
+    if t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last):
+        return torch.channels_last
+    return torch.contiguous_format
+
+
 def _to_channels_last(module):
     for m in module.modules():
         for name, p in list(m.named_parameters(recurse=False)):
@@ -928,9 +952,9 @@ class TrainStep:
         dst = [static[k] for k in b]
         src = [b[k] for k in b]
         if prefetched:
-            torch._foreach_copy_(dst + x_list, src + t_list)
+            _multi_copy(dst + x_list, src + t_list)
         else:
-            torch._foreach_copy_(dst, src)
+            _multi_copy(dst, src)
             nxt.copy_(static["image"], non_blocking=True)  # this batch was not prefetched
             g_teach.replay()                                # its teacher straight into X
         nimg = None

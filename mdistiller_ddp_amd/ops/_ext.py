@@ -137,6 +137,7 @@ SIGNATURES = {
     "mda_adam_step": "ppppppffffifpfis",
     "mda_sq_norm": "pipppfs",
     "mda_scale_inplace": "ppis",
+    "mda_multi_copy": "pis",
 }
 
 HOST_SIGNATURES = {

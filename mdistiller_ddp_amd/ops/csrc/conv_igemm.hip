@@ -103,7 +103,23 @@ struct ConvParams {
   // tiles per group).  Dense: ldx = Cin, cout_g = Cout.
   int ldx, cout_g;
   int xcd;  // glds kernel: XCD-aware tile order (MDA_CONV_XCD, default on)
+  // halo kernels: multiply-shift divisions by W, H, W + 2, (rows + 2)(W + 2)
+  // and rows (set by halo_geometry).  The prologue's ~20 integer divisions
+  // by runtime values cost ~1.2 us per block (in-kernel stamps,
+  // scripts/conv_stamps.py) -- as much as a third of a 16x16 conv's MFMA loop.
+  uint32_t dv_W[2], dv_H[2], dv_PW[2], dv_PHPW[2], dv_RH[2];
 };
+
+// n / d for 0 <= n < 2^31 with the host-made (mul, shr) of d
+__device__ __forceinline__ int hdiv(int n, const uint32_t (&dv)[2]) {
+  return (int)((__umulhi((uint32_t)n, dv[0]) + (uint32_t)n) >> dv[1]);
+}
+inline void make_hdiv(uint32_t d, uint32_t (&dv)[2]) {
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  dv[1] = l;
+  dv[0] = (uint32_t)((((1ull << 32) * ((1ull << l) - d)) / d) + 1);
+}
 
 // first output channel past the group of the tile starting at n0
 __device__ __forceinline__ int group_nlim(const ConvParams& p, int n0) {
@@ -1098,11 +1114,12 @@ conv_halo_kernel(const ConvParams p) {
   const int RH = p.hrows;
   const int PW = W + 2;                       // patch row length (pixels)
   const int PH = RH + 2;                      // patch rows per image
-  const int grow0 = m0 / W;                   // first global output row (n*H + oh)
-  const int img0 = grow0 / H;
+  const int grow0 = hdiv(m0, p.dv_W);                   // first global output row (n*H + oh)
+  const int img0 = hdiv(grow0, p.dv_H);
   const int oh0 = grow0 - img0 * H;
   EpiPre<BM, BN, 256> pre;
   epi_prefetch(p, pre, m0, n0, PB, false);
+  stamp(p, 5);
 
   // patch DMA: piece j covers patch rows 32j..32j+31; this thread's row/chunk
   const int trow = tid >> 3;
@@ -1115,9 +1132,9 @@ conv_halo_kernel(const ConvParams p) {
       const int pr = 32 * j + trow;
       int off = -1;
       if (pr < P) {
-        const int img = pr / (PH * PW);
+        const int img = hdiv(pr, p.dv_PHPW);
         const int rem = pr - img * PH * PW;
-        const int ir = rem / PW, ic = rem - (rem / PW) * PW;
+        const int ir = hdiv(rem, p.dv_PW), ic = rem - ir * PW;
         const int n = img0 + img;
         const int ih = oh0 + ir - 1, iw = ic - 1;
         if (n < p.N && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
@@ -1136,6 +1153,7 @@ conv_halo_kernel(const ConvParams p) {
     b_row[j] = p.w + (int64_t)(b_ok[j] ? co : 0) * p.Kp + chunk * 8;
   }
 
+  stamp(p, 6);
   const int nchunks = p.Cin / BK;
   const int c_begin = blockIdx.z * p.steps_per_split;
   const int c_end = min(nchunks, c_begin + p.steps_per_split);
@@ -1174,8 +1192,8 @@ conv_halo_kernel(const ConvParams p) {
   for (int i = 0; i < MI; ++i) {
     int ml = wm * (BM / 2) + i * 16 + frow;         // local output pixel
     if (ml >= PB) ml = 0;                           // idle MFMA row (masked at the store)
-    const int lr = ml / W, c = ml - (ml / W) * W;   // local output row, column
-    const int img = lr / RH, r = lr - img * RH;
+    const int lr = hdiv(ml, p.dv_W), c = ml - lr * W;   // local output row, column
+    const int img = hdiv(lr, p.dv_RH), r = lr - img * RH;
     a_prow[i] = (img * PH + r) * PW + c;
   }
   const int bswz = (frow >> 1) & 7;
@@ -1294,8 +1312,8 @@ conv_halo1_kernel(const ConvParams p) {
   const int RH = p.hrows;
   const int PW = W + 2;                       // patch row length (pixels)
   const int PH = RH + 2;                      // patch rows per image
-  const int grow0 = m0 / W;                   // first global output row (n*H + oh)
-  const int img0 = grow0 / H;
+  const int grow0 = hdiv(m0, p.dv_W);                   // first global output row (n*H + oh)
+  const int img0 = hdiv(grow0, p.dv_H);
   const int oh0 = grow0 - img0 * H;
   EpiPre<BM, BN, 256> pre;
   epi_prefetch(p, pre, m0, n0, PB, false);
@@ -1311,9 +1329,9 @@ conv_halo1_kernel(const ConvParams p) {
       const int pr = 32 * j + trow;
       int off = -1;
       if (pr < P) {
-        const int img = pr / (PH * PW);
+        const int img = hdiv(pr, p.dv_PHPW);
         const int rem = pr - img * PH * PW;
-        const int ir = rem / PW, ic = rem - (rem / PW) * PW;
+        const int ir = hdiv(rem, p.dv_PW), ic = rem - ir * PW;
         const int n = img0 + img;
         const int ih = oh0 + ir - 1, iw = ic - 1;
         if (n < p.N && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
@@ -1368,8 +1386,8 @@ conv_halo1_kernel(const ConvParams p) {
   for (int i = 0; i < MI; ++i) {
     int ml = wm * (BM / 2) + i * 16 + frow;         // local output pixel
     if (ml >= PB) ml = 0;                           // idle MFMA row (masked at the store)
-    const int lr = ml / W, c = ml - (ml / W) * W;   // local output row, column
-    const int img = lr / RH, r = lr - img * RH;
+    const int lr = hdiv(ml, p.dv_W), c = ml - lr * W;   // local output row, column
+    const int img = hdiv(lr, p.dv_RH), r = lr - img * RH;
     a_prow[i] = (img * PH + r) * PW + c;
   }
   const int bswz = (frow >> 1) & 7;
@@ -1464,8 +1482,8 @@ conv_halo2_kernel(const ConvParams p) {
   const int W = p.W, H = p.H;
   const int IMGS = p.himgs, RH = p.hrows;
   const int PW = W + 2, PH = RH + 2;
-  const int grow0 = m0 / W;
-  const int img0 = grow0 / H;
+  const int grow0 = hdiv(m0, p.dv_W);
+  const int img0 = hdiv(grow0, p.dv_H);
   const int oh0 = grow0 - img0 * H;
   EpiPre<HALO2_CAP, BN, 512> pre;
   epi_prefetch(p, pre, m0, n0, PB, false);
@@ -1481,9 +1499,9 @@ conv_halo2_kernel(const ConvParams p) {
       const int pr = 64 * j + trow;
       int off = -1;
       if (pr < P) {
-        const int img = pr / (PH * PW);
+        const int img = hdiv(pr, p.dv_PHPW);
         const int rem = pr - img * PH * PW;
-        const int ir = rem / PW, ic = rem - (rem / PW) * PW;
+        const int ir = hdiv(rem, p.dv_PW), ic = rem - ir * PW;
         const int n = img0 + img;
         const int ih = oh0 + ir - 1, iw = ic - 1;
         if (n < p.N && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
@@ -1522,8 +1540,8 @@ conv_halo2_kernel(const ConvParams p) {
   for (int i = 0; i < MI; ++i) {
     int ml = grp * BMG + wm * (BMG / 2) + i * 16 + frow;
     if (ml >= PB) ml = 0;                       // idle MFMA row (masked at the store)
-    const int lr = ml / W, c = ml - (ml / W) * W;
-    const int img = lr / RH, r = lr - img * RH;
+    const int lr = hdiv(ml, p.dv_W), c = ml - lr * W;
+    const int img = hdiv(lr, p.dv_RH), r = lr - img * RH;
     a_prow[i] = (img * PH + r) * PW + c;
   }
   const int bswz = (frow >> 1) & 7;
@@ -1647,6 +1665,11 @@ bool halo_geometry(ConvParams& p, int max_rows, int cap = HALO_BM) {
   p.hrows = rows;
   p.himgs = imgs;
   p.hpb = pb;
+  make_hdiv((uint32_t)p.W, p.dv_W);
+  make_hdiv((uint32_t)p.H, p.dv_H);
+  make_hdiv((uint32_t)(p.W + 2), p.dv_PW);
+  make_hdiv((uint32_t)((rows + 2) * (p.W + 2)), p.dv_PHPW);
+  make_hdiv((uint32_t)rows, p.dv_RH);
   return true;
 }
 

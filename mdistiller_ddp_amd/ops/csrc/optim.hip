@@ -203,3 +203,58 @@ MDA_API int mda_scale_inplace(float* x, const float* s, int64_t n, hipStream_t s
   hipLaunchKernelGGL(scale_kernel, dim3(grid_for(n4)), dim3(256), 0, st, (float4*)x, s, n4);
   MDA_CHECK_LAUNCH();
 }
+
+// ---------------------------------------------------------------------------
+// Multi-tensor device copy: up to 16 (src, dst, bytes) pairs in ONE launch --
+// the replayed step's input + teacher-output copies (engine/step.py
+// _step_split), which torch._foreach_copy_ issues as one blit per tensor.
+// 16-byte vectors where both ends are aligned, bytes otherwise.
+namespace {
+constexpr int MCOPY_MAX = 16;
+struct MultiCopy {
+  const char* src[MCOPY_MAX];
+  char* dst[MCOPY_MAX];
+  int64_t bytes[MCOPY_MAX];
+  int64_t blk0[MCOPY_MAX + 1];  // first block of each pair (prefix sums)
+  int n;
+};
+constexpr int MCOPY_CHUNK = 256 * 16 * 4;  // bytes per block
+
+__global__ void __launch_bounds__(256) multi_copy_kernel(MultiCopy a) {
+  int t = 0;
+  while (t + 1 < a.n && (int64_t)blockIdx.x >= a.blk0[t + 1]) ++t;
+  const int64_t base = ((int64_t)blockIdx.x - a.blk0[t]) * MCOPY_CHUNK;
+  const int64_t end = min(base + (int64_t)MCOPY_CHUNK, a.bytes[t]);
+  const char* s = a.src[t];
+  char* d = a.dst[t];
+  const bool vec = (((uintptr_t)s | (uintptr_t)d) & 15) == 0;
+  if (vec) {
+    const int64_t vend = base + ((end - base) / 16) * 16;
+    for (int64_t o = base + threadIdx.x * 16; o < vend; o += 256 * 16)
+      *(uint4*)(d + o) = *(const uint4*)(s + o);
+    for (int64_t o = vend + threadIdx.x; o < end; o += 256) d[o] = s[o];
+  } else {
+    for (int64_t o = base + threadIdx.x; o < end; o += 256) d[o] = s[o];
+  }
+}
+}  // namespace
+
+// table: n x 3 int64 {src, dst, bytes} in host memory.
+MDA_API int mda_multi_copy(const int64_t* table, int64_t n, hipStream_t st) {
+  if (n < 1 || n > MCOPY_MAX) return (int)hipErrorInvalidValue;
+  MultiCopy a{};
+  a.n = (int)n;
+  int64_t blk = 0;
+  for (int i = 0; i < n; ++i) {
+    a.src[i] = (const char*)table[3 * i];
+    a.dst[i] = (char*)table[3 * i + 1];
+    a.bytes[i] = table[3 * i + 2];
+    a.blk0[i] = blk;
+    blk += (a.bytes[i] + MCOPY_CHUNK - 1) / MCOPY_CHUNK;
+  }
+  a.blk0[n] = blk;
+  if (blk <= 0) return 0;
+  if (blk > (1 << 30)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(multi_copy_kernel, dim3((unsigned)blk), dim3(256), 0, st, a);
+  MDA_CHECK_LAUNCH();
+}

@@ -824,6 +824,7 @@ class _ConvBNActTrain(torch.autograd.Function):
         if len(meta) > 3 and meta[3] == "dw":
             ctx.forks = (None, None)
             ctx.cbias = cbias is not None
+            ctx.cbias_t = cbias
             res = _dw_forward(ctx, x, weight, gamma, beta, residual, stride, pad, act, bn,
                               want_preact)
             if cbias is not None:
@@ -953,6 +954,7 @@ class _ConvBNActTrain(torch.autograd.Function):
         _LAST_LINK[0] = ctx.bnlink
         _LAST_VBN[0] = ctx.vbn
         ctx.cbias = cbias is not None
+        ctx.cbias_t = cbias
         if cbias is not None:
             # BN(y + b) == BN(y) in training; the running mean tracks mean(y) + b
             bn.running_mean.add_(cbias.detach(), alpha=float(bn.momentum))
@@ -1031,9 +1033,7 @@ class _ConvBNActTrain(torch.autograd.Function):
             notify_grad(gamma, beta)
         dgamma = None if direct_gb else sums[1].clone()
         dbeta = None if direct_gb else sums[0].clone()
-        dcb = torch.zeros(Cout, dtype=torch.float32, device=dev) if (
-            ctx.cbias and ctx.needs_input_grad[9]) else None
-        return dx, dw, dgamma, dbeta, dres, None, None, None, None, dcb, None
+        return dx, dw, dgamma, dbeta, dres, None, None, None, None, _cbias_grad(ctx), None
 
 
 def _bn_bwd_dual(dout, dpre, y, res, stats, gamma, beta, M, C, act, need_res, link, res_link, vres):
@@ -1238,7 +1238,21 @@ def _dw_backward(ctx, dout, dpre):
         dw = None if direct_w else target
         if direct_w:
             notify_grad(weight)
-    return dx, dw, dgamma, dbeta, dres, None, None, None, None, None, None
+    return dx, dw, dgamma, dbeta, dres, None, None, None, None, _cbias_grad(ctx), None
+
+
+def _cbias_grad(ctx):
+    """The gradient of a conv bias in front of a training BN is exactly zero
+    (BN subtracts the batch mean).  A bias with a bound flat-gradient view
+    (the training step) keeps its zeroed slot -- no kernel; otherwise a zero
+    tensor, so ``.grad`` exists as with PyTorch's layers."""
+    b = getattr(ctx, "cbias_t", None)
+    if b is None or not ctx.needs_input_grad[9]:
+        return None
+    if b.grad is not None:
+        notify_grad(b)
+        return None
+    return torch.zeros_like(b)
 
 
 def pack_weights(weight, dgrad=True):

@@ -47,6 +47,11 @@ def main():
             q = lambda v: f"{v.median().item():6.2f} [{v.min().item():6.2f},{v.max().item():6.2f}]"
             print(f"run {r}: blocks {len(st)}  span {rel[:, 4].max().item():.2f} us")
             print("   start      ", q(rel[:, 0]))
+            full = st - t0
+            if (st[:, 5] > 0).all():  # multi-chunk halo kernel: prologue detail
+                print("   epi prefetch", q(full[:, 5] - full[:, 0]))
+                print("   addresses   ", q(full[:, 6] - full[:, 5]))
+                print("   DMA issue   ", q(full[:, 1] - full[:, 6]))
             print("   issue done ", q(rel[:, 1] - rel[:, 0]))
             print("   tap0 landed", q(rel[:, 2] - rel[:, 1]))
             print("   9-tap loop ", q(rel[:, 3] - rel[:, 2]))

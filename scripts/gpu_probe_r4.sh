@@ -1,15 +1,12 @@
 set -o pipefail
 mkdir -p gpurun_out; export PYTHONPATH=$PWD TMPDIR=/tmp
-timeout -k 10 500 python -u -m pytest tests/test_gpu_conv.py tests/test_gpu_train_layers.py -q --timeout 200 --timeout-method thread > gpurun_out/t_c.log 2>&1; rc=$?; echo "tests rc=$rc"
-grep -E "FAILED|passed|failed" gpurun_out/t_c.log | head -12
-[ $rc -ge 124 ] && exit $rc
-out=gpurun_out/stamps2.log; : > $out
-for sh in 64,128,16,128 64,256,8,256 64,64,32,64; do
-  echo "== $sh" >> $out
-  timeout -k 10 60 python -u scripts/conv_stamps.py --shape $sh --runs 1 >> $out 2>&1 || { echo "rc=$?"; tail $out; exit 1; }
+out=gpurun_out/envsweep.log; : > $out
+for e in "X=0" "DEBUG_CLR_GRAPH_PACKET_CAPTURE=1" "DEBUG_CLR_GRAPH_PACKET_CAPTURE=0" "HSA_ENABLE_SDMA=0"; do
+  echo "== $e" >> $out
+  env $e timeout -k 10 200 python -u bench.py --steps 300 --warmup 30 >> $out 2>&1 || { echo "rc=$? $e"; tail -5 $out; exit 1; }
 done
-grep -v "amdgpu.ids" $out
-timeout -k 10 200 python -u bench.py --steps 300 --warmup 30 > gpurun_out/b1.log 2>&1 || exit 1
-timeout -k 10 200 python -u bench.py --steps 300 --warmup 30 --cfg configs/cifar100/dot/res32x4_res8x4.yaml > gpurun_out/b2.log 2>&1 || exit 1
-grep -h "{" gpurun_out/b1.log gpurun_out/b2.log | cut -c1-220
-PROF="configs/cifar100/fitnet.yaml:r4_fitnet;configs/cifar100/vid.yaml:r4_vid;configs/cifar100/dkd/res32x4_res8x4.yaml:r4_flagship" bash scripts/gpu_run.sh
+grep -E "^==|ms_per_step" $out | sed 's/.*"ms_per_step": \([0-9.]*\).*/  \1 ms/'
+MDA_EVENTS_SYNC=1 timeout -k 10 400 python -u -m pytest tests/test_gpu_multirank.py -q --timeout 380 --timeout-method thread -k events > gpurun_out/t_ev.log 2>&1; echo "events(sync) rc=$?"
+grep -E "passed|failed|assert|rel" gpurun_out/t_ev.log | head -5
+timeout -k 10 900 python -u benchmarks/throughput.py --steps 60 --warmup 15 --out gpurun_out/r4_tp_all.jsonl > gpurun_out/tp_all.log 2>&1; echo "tp rc=$?"
+grep "{" gpurun_out/tp_all.log | cut -c1-150

@@ -68,9 +68,29 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--out", default=None, help="append JSON rows to this file")
+    ap.add_argument("--in-process", action="store_true",
+                    help="run every config in THIS process (default: one child process each)")
     args = ap.parse_args()
-    from mdistiller_ddp_amd import benchmark
     names = list(CONFIGS) if args.configs == "all" else args.configs.split(",")
+    if len(names) > 1 and not args.in_process and "WORLD_SIZE" not in os.environ:
+        # one fresh process per config: a step's streams get hardware queues by
+        # the process's history of stream creation, and a config measured after
+        # others in the same process can run up to 40 % slower
+        # (profiles/r3_dot_history.md) -- rows then depend on the run order
+        import subprocess
+        for name in names:
+            cmd = [sys.executable, os.path.abspath(__file__), "--configs", name, "--steps",
+                   str(args.steps), "--warmup", str(args.warmup), "--in-process"]
+            if args.no_graph:
+                cmd.append("--no-graph")
+            if args.out:
+                cmd += ["--out", args.out]
+            r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
+            rows = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+            print(rows[-1] if rows else json.dumps({"config": name, "error": f"exit {r.returncode}"}),
+                  flush=True)
+        return
+    from mdistiller_ddp_amd import benchmark
     for name in names:
         yaml, bs, opts, ds = CONFIGS[name]
         try:

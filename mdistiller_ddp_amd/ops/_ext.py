@@ -57,6 +57,7 @@ SIGNATURES = {
     "mda_pack_conv_weights_gc": "ppp" + "i" * 7 + "s",
     "mda_channel_gather": "ppp" + "iii" + "s",
     "mda_gather2": "pppp" + "i" + "ppi" + "iii" + "s",
+    "mda_act_bwd": "pppp" + "ii" + "s",
     "mda_vid_loss": "ppp" + "ii" + "f" + "pp" + "s",
     "mda_vid_bwd": "pppp" + "p" + "ii" + "f" + "pp" + "s",
     "mda_nst_fwd": "p" + "ii" + "p" + "s",

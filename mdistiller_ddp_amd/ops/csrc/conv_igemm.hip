@@ -1123,7 +1123,11 @@ conv_halo_kernel(const ConvParams p) {
 
   // patch DMA: piece j covers patch rows 32j..32j+31; this thread's row/chunk
   const int trow = tid >> 3;
-  const int chunk = (tid & 7) ^ ((trow >> 1) & 7);  // (32j + trow) >> 1 & 7 == trow >> 1 & 7
+  // patch swizzle s(r) = r & 6 (rows mod 32j): any 16 consecutive patch rows
+  // -- a fragment read at ANY tap offset -- hit 16 distinct 16-B slots of the
+  // ds_read_b128 lane groups; the GEMM swizzle (r >> 1) & 7 assumed aligned
+  // rows and cost ~1.75-way conflicts on the shifted tap views
+  const int chunk = (tid & 7) ^ (trow & 6);
   int p_src[HALO_PIECES];                     // element offset of the patch pixel, or -1
   {
     const int P = IMGS * PH * PW;
@@ -1196,7 +1200,7 @@ conv_halo_kernel(const ConvParams p) {
     const int img = hdiv(lr, p.dv_RH), r = lr - img * RH;
     a_prow[i] = (img * PH + r) * PW + c;
   }
-  const int bswz = (frow >> 1) & 7;
+  const int bswz = frow & 6;
 
   auto compute = [&](int pbuf, int bbuf, int tap) {
     const char* Ps = smem + pbuf * PATCH;
@@ -1210,7 +1214,7 @@ conv_halo_kernel(const ConvParams p) {
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         const int pr = a_prow[i] + toff;
-        af[i] = *(const bf16x8*)(Ps + pr * 128 + ((q ^ ((pr >> 1) & 7)) * 16));
+        af[i] = *(const bf16x8*)(Ps + pr * 128 + ((q ^ (pr & 6)) * 16));
       }
 #pragma unroll
       for (int j = 0; j < NI; ++j)
@@ -1320,7 +1324,11 @@ conv_halo1_kernel(const ConvParams p) {
 
   // patch DMA: piece j covers patch rows 32j..32j+31; this thread's row/chunk
   const int trow = tid >> 3;
-  const int chunk = (tid & 7) ^ ((trow >> 1) & 7);  // (32j + trow) >> 1 & 7 == trow >> 1 & 7
+  // patch swizzle s(r) = r & 6 (rows mod 32j): any 16 consecutive patch rows
+  // -- a fragment read at ANY tap offset -- hit 16 distinct 16-B slots of the
+  // ds_read_b128 lane groups; the GEMM swizzle (r >> 1) & 7 assumed aligned
+  // rows and cost ~1.75-way conflicts on the shifted tap views
+  const int chunk = (tid & 7) ^ (trow & 6);
   int p_src[HALO1_PIECES];                    // element offset of the patch pixel, or -1
   {
     const int P = IMGS * PH * PW;
@@ -1390,7 +1398,7 @@ conv_halo1_kernel(const ConvParams p) {
     const int img = hdiv(lr, p.dv_RH), r = lr - img * RH;
     a_prow[i] = (img * PH + r) * PW + c;
   }
-  const int bswz = (frow >> 1) & 7;
+  const int bswz = frow & 6;
 
   auto compute = [&](int pbuf, int bbuf, int tap) {
     const char* Ps = smem + pbuf * PATCH;
@@ -1404,7 +1412,7 @@ conv_halo1_kernel(const ConvParams p) {
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         const int pr = a_prow[i] + toff;
-        af[i] = *(const bf16x8*)(Ps + pr * 128 + ((q ^ ((pr >> 1) & 7)) * 16));
+        af[i] = *(const bf16x8*)(Ps + pr * 128 + ((q ^ (pr & 6)) * 16));
       }
 #pragma unroll
       for (int j = 0; j < NI; ++j)
@@ -1490,7 +1498,7 @@ conv_halo2_kernel(const ConvParams p) {
 
   // DMA lanes: 64 rows (8 per wave) x 8 sixteen-byte chunks, XOR-swizzled
   const int trow = gtid >> 3;
-  const int chunk = (gtid & 7) ^ ((trow >> 1) & 7);
+  const int chunk = (gtid & 7) ^ (trow & 6);
   int p_src[HALO2_PIECES];
   {
     const int P = IMGS * PH * PW;
@@ -1544,7 +1552,7 @@ conv_halo2_kernel(const ConvParams p) {
     const int img = hdiv(lr, p.dv_RH), r = lr - img * RH;
     a_prow[i] = (img * PH + r) * PW + c;
   }
-  const int bswz = (frow >> 1) & 7;
+  const int bswz = frow & 6;
 
   // A fragments (patch rows) of tap t+1 are read during tap t: the patch is
   // resident from tap 0 on, only the weight tile of a tap needs its own wait
@@ -1558,7 +1566,7 @@ conv_halo2_kernel(const ConvParams p) {
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         const int pr = a_prow[i] + toff;
-        af[buf][kk][i] = *(const bf16x8*)(smem + pr * 128 + ((q ^ ((pr >> 1) & 7)) * 16));
+        af[buf][kk][i] = *(const bf16x8*)(smem + pr * 128 + ((q ^ (pr & 6)) * 16));
       }
     }
   };

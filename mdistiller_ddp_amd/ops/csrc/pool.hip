@@ -407,3 +407,37 @@ MDA_API int mda_shuffle_tail_bwd(const void* dout, const void* dpre, const void*
                      (bf16_t*)dx, (int)N, (int)H, (int)W, (int)Ho, (int)Wo, (int)C3, (int)Cx);
   MDA_CHECK_LAUNCH();
 }
+
+// ---------------------------------------------------------------------------
+// Activation backward of a BN-less native conv (ops/hip_train.py _ConvTrain,
+// e.g. VID's 1x1 -> ReLU regressors): dz = act'(pre) * dout (+ dpre), bf16,
+// 8 elements per thread -- one launch instead of compare + where + fill.
+namespace {
+__global__ void __launch_bounds__(256)
+act_bwd_kernel(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ pre,
+               const bf16_t* __restrict__ dpre, bf16_t* __restrict__ dz, int64_t n8, int act) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float g[8], p[8], q[8];
+    unpack8(((const uint4*)dout)[i], g);
+    unpack8(((const uint4*)pre)[i], p);
+    if (dpre) unpack8(((const uint4*)dpre)[i], q);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const bool on = act == 2 ? (p[e] > 0.f && p[e] < 6.f) : (act == 1 ? p[e] > 0.f : true);
+      g[e] = (on ? g[e] : 0.f) + (dpre ? q[e] : 0.f);
+    }
+    ((uint4*)dz)[i] = pack8(g);
+  }
+}
+}  // namespace
+
+MDA_API int mda_act_bwd(const void* dout, const void* pre, const void* dpre, void* dz, int64_t n,
+                        int64_t act, hipStream_t st) {
+  if (n % 8 || n <= 0) return (int)hipErrorInvalidValue;
+  int64_t blocks = (n / 8 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(act_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const bf16_t*)dout,
+                     (const bf16_t*)pre, (const bf16_t*)dpre, (bf16_t*)dz, n / 8, (int)act);
+  MDA_CHECK_LAUNCH();
+}

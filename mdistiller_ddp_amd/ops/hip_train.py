@@ -1392,10 +1392,17 @@ class _ConvTrain(torch.autograd.Function):
         M = N * Ho * Wo
         dev = x.device
         dz = None
-        if dout is not None:
-            dz = _act_mask(_cl_bf16(dout), pre, act)
-        if dpre is not None:
-            dz = _cl_bf16(dpre) if dz is None else dz + _cl_bf16(dpre)
+        if dout is not None and pre is not None and pre.numel() % 8 == 0 \
+                and pre.is_contiguous(memory_format=torch.channels_last):
+            # act' * dout (+ dpre) in one native launch
+            dz = torch.empty_like(pre)
+            _ext.call("mda_act_bwd", _cl_bf16(dout), pre, _cl_bf16(dpre) if dpre is not None else None,
+                      dz, pre.numel(), act)
+        else:
+            if dout is not None:
+                dz = _act_mask(_cl_bf16(dout), pre, act)
+            if dpre is not None:
+                dz = _cl_bf16(dpre) if dz is None else dz + _cl_bf16(dpre)
         dz = _cl_bf16(dz)
         dres = dz if (ctx.has_res and ctx.needs_input_grad[2]) else None
         dx = None

@@ -112,7 +112,10 @@ SIGNATURES = {
     "mda_pool_fc_bwd": "ippppppp" + "iiiii" + "s",
     "mda_sym_eig": "piiipp" + "s",
     # KDSVD alignment + RBF + L2 after the eigensolver (csrc/kdsvd.hip)
-    "mda_kdsvd_post": "ppppp" + "iii" + "pp" + "s",
+    "mda_kdsvd_post": "ppppp" + "iii" + "pp" + "pp" + "s",
+    "mda_kdsvd_gram": "pii" + "s",
+    "mda_kdsvd_gram_apply": "pi" + "s",
+    "mda_sym_eig_multi": "pii" + "s",
     "mda_pool_fc_bwd_bn": "ippppppp" + "iiiii" + "pppip" + "p" + "s",
     "mda_meters_update": "ippii" + "pppp" + "ips",
     # ReviewKD HCL + ABF (csrc/reviewkd.hip)

@@ -20,6 +20,7 @@
 //
 // Output: vals [B][n] (descending), vecs [B][n][n] row-major with the
 // eigenvectors as COLUMNS (V[:, j] pairs with vals[j]), fp32.
+#include <algorithm>
 #include <cstdlib>
 
 #include "common.h"
@@ -27,10 +28,21 @@
 namespace {
 
 constexpr int EIG_NMAX = 64;
+constexpr int EIG_MAXE = 8;
 
-__global__ void __launch_bounds__(256) sym_eig_kernel(const float* __restrict__ g, int n0,
-                                                      int sweeps, float* __restrict__ vals,
-                                                      float* __restrict__ vecs) {
+// One batch of matrices per table entry (blockIdx.y): B matrices of size n0,
+// the input summed over `parts` partial Grams (part stride pstride floats --
+// csrc/kdsvd.hip's split-K Gram), results at vals / vecs.  Entries of
+// different sizes run side by side in ONE launch (KDSVD's stages: the small
+// matrices finish under the largest one's sweeps instead of after them).
+struct EigEntry {
+  const float* g; float* vals; float* vecs;
+  int64_t pstride;
+  int B, n0, parts;
+};
+struct EigTable { EigEntry e[EIG_MAXE]; };
+
+__global__ void __launch_bounds__(256) sym_eig_kernel(EigTable tab, int sweeps) {
   __shared__ double A[EIG_NMAX][EIG_NMAX + 1];
   __shared__ float V[EIG_NMAX][EIG_NMAX + 1];  // rotations accumulated in fp32
   __shared__ double cs[EIG_NMAX / 2][2];
@@ -38,13 +50,22 @@ __global__ void __launch_bounds__(256) sym_eig_kernel(const float* __restrict__ 
   __shared__ double lam[EIG_NMAX];
   __shared__ int order[EIG_NMAX];
   __shared__ double red[2][8];
+  const EigEntry& en = tab.e[blockIdx.y];
   const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
-  const float* gb = g + (int64_t)b * n0 * n0;
+  if (b >= en.B) return;  // uniform per block: before any barrier
+  const int n0 = en.n0;
+  float* __restrict__ vals = en.vals;
+  float* __restrict__ vecs = en.vecs;
+  const float* gb = en.g + (int64_t)b * n0 * n0;
   const int n = n0 + (n0 & 1);
   for (int e = tid; e < n * n; e += nt) {
     const int i = e / n, j = e % n;
-    // symmetrise (G is symmetric up to the GEMM's rounding)
-    A[i][j] = (i < n0 && j < n0) ? 0.5 * ((double)gb[i * n0 + j] + (double)gb[j * n0 + i]) : 0.0;
+    // symmetrise (G is symmetric up to the GEMM's rounding), summing the parts
+    double a = 0.0;
+    if (i < n0 && j < n0)
+      for (int q = 0; q < en.parts; ++q)
+        a += (double)gb[q * en.pstride + i * n0 + j] + (double)gb[q * en.pstride + j * n0 + i];
+    A[i][j] = 0.5 * a;
     V[i][j] = i == j ? 1.f : 0.f;
   }
   const int m = n - 1, half = n / 2;
@@ -139,11 +160,7 @@ __global__ void __launch_bounds__(256) sym_eig_kernel(const float* __restrict__ 
 
 }  // namespace
 
-// g: [B][n][n] fp32 symmetric (n <= 63); vals [B][n], vecs [B][n][n] fp32 (see above).
-MDA_API int mda_sym_eig(const float* g, int64_t B, int64_t n, int64_t sweeps, float* vals,
-                        float* vecs, hipStream_t st) {
-  if (B <= 0 || B > 65535 || n < 2 || n >= EIG_NMAX || sweeps < 1 || sweeps > 64)
-    return (int)hipErrorInvalidValue;
+static int eig_threads() {
   // block size (64 / 128 / 256; MDA_EIG_THREADS): the Jacobi steps are
   // latency bound, fewer waves make each step's barriers cheaper
   static const int threads = [] {
@@ -151,7 +168,35 @@ MDA_API int mda_sym_eig(const float* g, int64_t B, int64_t n, int64_t sweeps, fl
     const int t = e ? atoi(e) : 256;
     return (t == 64 || t == 128) ? t : 256;
   }();
-  hipLaunchKernelGGL(sym_eig_kernel, dim3((unsigned)B), dim3(threads), 0, st, g, (int)n, (int)sweeps,
-                     vals, vecs);
+  return threads;
+}
+
+// g: [B][n][n] fp32 symmetric (n <= 63); vals [B][n], vecs [B][n][n] fp32 (see above).
+MDA_API int mda_sym_eig(const float* g, int64_t B, int64_t n, int64_t sweeps, float* vals,
+                        float* vecs, hipStream_t st) {
+  if (B <= 0 || B > 65535 || n < 2 || n >= EIG_NMAX || sweeps < 1 || sweeps > 64)
+    return (int)hipErrorInvalidValue;
+  EigTable tab{};
+  tab.e[0] = EigEntry{g, vals, vecs, 0, (int)B, (int)n, 1};
+  hipLaunchKernelGGL(sym_eig_kernel, dim3((unsigned)B), dim3(eig_threads()), 0, st, tab, (int)sweeps);
+  return (int)hipGetLastError();
+}
+
+// Several batches in one launch.  table: int64 [E][7] rows
+// (g, vals, vecs, pstride, B, n, parts); E <= 8.
+MDA_API int mda_sym_eig_multi(const int64_t* table, int64_t E, int64_t sweeps, hipStream_t st) {
+  if (E < 1 || E > EIG_MAXE || sweeps < 1 || sweeps > 64) return (int)hipErrorInvalidValue;
+  EigTable tab{};
+  int bmax = 0;
+  for (int e = 0; e < E; ++e) {
+    const int64_t* r = table + 7 * e;
+    if (r[4] <= 0 || r[4] > 65535 || r[5] < 2 || r[5] >= EIG_NMAX || r[6] < 1 || r[6] > 64)
+      return (int)hipErrorInvalidValue;
+    tab.e[e] = EigEntry{(const float*)r[0], (float*)r[1], (float*)r[2], r[3], (int)r[4], (int)r[5],
+                        (int)r[6]};
+    bmax = std::max(bmax, (int)r[4]);
+  }
+  hipLaunchKernelGGL(sym_eig_kernel, dim3((unsigned)bmax, (unsigned)E), dim3(eig_threads()), 0, st,
+                     tab, (int)sweeps);
   return (int)hipGetLastError();
 }

@@ -321,32 +321,53 @@ __device__ __forceinline__ float nst_r(const float* g, int C2, int i) {
   return fmaxf(sqrtf(fmaxf(g[(int64_t)i * C2 + i], 0.f)), 1e-12f);
 }
 
+// grid (N, ceil(2C / NST_FROWS)): one wave per row (NST_FROWS / 4 rows per
+// wave), 16-byte column loads when C % 4 == 0; rows c < C weigh the S columns
+// +1 and the X columns -2, rows C + c only their T columns (+1).  One partial
+// per block (part [N][gridDim.y], summed by the caller) -- spread over
+// N * 2C / 32 blocks instead of one block per sample reading its whole
+// 3C^2-entry Gram (141 us for C = 256 at N = 64, profiles/r4_prof_nst.md).
+constexpr int NST_FROWS = 32;
+
+template <bool VEC>
 __global__ void __launch_bounds__(256)
 nst_fwd_kernel(const float* __restrict__ g, int C, float* __restrict__ part) {
   __shared__ float rr[2 * NST_CMAX];
-  __shared__ float red[256];
+  __shared__ float red[4];
   const int C2 = 2 * C;
   const float* gn = g + (int64_t)blockIdx.x * C2 * C2;
   for (int i = threadIdx.x; i < C2; i += blockDim.x) rr[i] = 1.f / nst_r(gn, C2, i);
   __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float acc = 0.f;
-  // ss (+1), tt (+1), st (-2) blocks
-  for (int64_t e = threadIdx.x; e < (int64_t)3 * C * C; e += blockDim.x) {
-    const int blk = (int)(e / ((int64_t)C * C));
-    const int rem = (int)(e - (int64_t)blk * C * C);
-    const int i = rem / C, j = rem - (rem / C) * C;
-    const int gi = blk == 1 ? C + i : i;
-    const int gj = blk == 0 ? j : C + j;
-    const float v = gn[(int64_t)gi * C2 + gj] * rr[gi] * rr[gj];
-    acc += (blk == 2 ? -2.f : 1.f) * v * v;
+  for (int q = 0; q < NST_FROWS / 4; ++q) {
+    const int row = blockIdx.y * NST_FROWS + wave * (NST_FROWS / 4) + q;
+    if (row >= C2) break;
+    const float* gr = gn + (int64_t)row * C2;
+    const float rrow = rr[row];
+    const int c0 = row < C ? 0 : C;
+    float a = 0.f;
+    if (VEC) {
+      for (int j = c0 + lane * 4; j < C2; j += 256) {
+        const float4 v = *(const float4*)(gr + j);
+        const float w = (row < C && j >= C) ? -2.f : 1.f;
+        const float e0 = v.x * rr[j], e1 = v.y * rr[j + 1], e2 = v.z * rr[j + 2], e3 = v.w * rr[j + 3];
+        a += w * ((e0 * e0 + e1 * e1) + (e2 * e2 + e3 * e3));
+      }
+    } else {
+      for (int j = c0 + lane; j < C2; j += 64) {
+        const float e = gr[j] * rr[j];
+        a += ((row < C && j >= C) ? -2.f : 1.f) * e * e;
+      }
+    }
+    acc += a * rrow * rrow;
   }
-  red[threadIdx.x] = acc;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (lane == 0) red[wave] = acc;
   __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+  if (threadIdx.x == 0)
+    part[(int64_t)blockIdx.x * gridDim.y + blockIdx.y] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 // grid (N, 2C / 8): 8 rows of PQ per block, one wave per row pair
@@ -396,9 +417,14 @@ nst_bwd_kernel(const float* __restrict__ g, int N, int C, const float* __restric
 }
 }  // namespace
 
+// part: [N][ceil(2C / 32)] fp32 partial sums (the loss numerator is their sum).
 MDA_API int mda_nst_fwd(const float* g, int64_t N, int64_t C, float* part, hipStream_t st) {
   if (C <= 0 || C > NST_CMAX || N <= 0) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(nst_fwd_kernel, dim3((unsigned)N), dim3(256), 0, st, g, (int)C, part);
+  const dim3 grid((unsigned)N, (unsigned)((2 * C + NST_FROWS - 1) / NST_FROWS));
+  if (C % 4 == 0)
+    hipLaunchKernelGGL(nst_fwd_kernel<true>, grid, dim3(256), 0, st, g, (int)C, part);
+  else
+    hipLaunchKernelGGL(nst_fwd_kernel<false>, grid, dim3(256), 0, st, g, (int)C, part);
   MDA_CHECK_LAUNCH();
 }
 

@@ -130,7 +130,7 @@ class _NSTGram(torch.autograd.Function):
         g = torch.bmm(w.transpose(1, 2), w)
         native = g.is_cuda and hip_enabled_for(g) and C <= 1024
         if native:
-            part = torch.empty(N, dtype=torch.float32, device=g.device)
+            part = torch.empty(N, (C2 + 31) // 32, dtype=torch.float32, device=g.device)
             _ext.call("mda_nst_fwd", g, N, C, part)
             loss = part.sum() / (N * C * C)
         else:
@@ -404,6 +404,9 @@ def _sym_eig(g):
     return lam.to(g.dtype), vec.to(g.dtype)
 
 
+_EIG_DEGEN = 1e-6
+
+
 class _GramEig(torch.autograd.Function):
     """Eigenvalues (descending) and eigenvectors (columns; largest-magnitude
     component positive) of G = X^T X for a batch X [B, R, W], W <= 63: the
@@ -442,7 +445,12 @@ class _GramEig(torch.autograd.Function):
         k = torch.zeros_like(v)
         if dvec is not None:
             diff = lam.unsqueeze(1) - lam.unsqueeze(2)  # [i, j] = lam_j - lam_i
-            f = torch.where(diff != 0, 1.0 / diff, torch.zeros_like(diff))
+            # gaps below 1e-6 of the largest eigenvalue (the fp32 solver's
+            # resolution) are one degenerate subspace: no 1/gap term (the SVD
+            # backward's 1/(s_j^2 - s_i^2) otherwise amplifies rounding noise
+            # by orders of magnitude; csrc/kdsvd.hip KS_DEGEN)
+            thr = _EIG_DEGEN * lam.abs().amax(dim=1, keepdim=True).unsqueeze(2)
+            f = torch.where(diff.abs() > thr, 1.0 / diff, torch.zeros_like(diff))
             f.diagonal(dim1=1, dim2=2).zero_()
             k = f * torch.bmm(v.transpose(1, 2), dvec)
         if dlam is not None:
@@ -507,7 +515,7 @@ class _KdsvdPost(torch.autograd.Function):
         W = [v.shape[-1] for v in vs]
         part = torch.empty(N, dtype=torch.float32, device=vs[0].device)
         tab = _kdsvd_table(vs, vt, lt, None, W)
-        _ext.call("mda_kdsvd_post", *tab, S, N, k, part, None)
+        _ext.call("mda_kdsvd_post", *tab, S, N, k, part, None, None, None)
         ctx.save_for_backward(*vs, *vt, *lt)
         ctx.meta = (k, S, N, W)
         return part.sum()
@@ -519,8 +527,85 @@ class _KdsvdPost(torch.autograd.Function):
         vs, vt, lt = list(t[:S]), list(t[S:2 * S]), list(t[2 * S:])
         dvs = [torch.empty_like(v) for v in vs]
         tab = _kdsvd_table(vs, vt, lt, dvs, W)
-        _ext.call("mda_kdsvd_post", *tab, S, N, k, None, go.float().reshape(1).contiguous())
+        _ext.call("mda_kdsvd_post", *tab, S, N, k, None, go.float().reshape(1).contiguous(), None, None)
         return (None, None, None) + tuple(dvs)
+
+
+_KDSVD_KSPLIT = 4  # row ranges per sample in the Gram launch (partials summed by the eigensolver)
+
+
+def _nhwc(f):
+    return f.contiguous(memory_format=torch.channels_last)
+
+
+class _KdsvdNative(torch.autograd.Function):
+    """The whole KDSVD loss on the native kernels, from the NHWC feature maps:
+    forward = ONE Gram launch for every stage's student and teacher
+    (csrc/kdsvd.hip mda_kdsvd_gram, bf16/fp32 in, fp32 split-K partials) +
+    ONE eigensolver launch for all stages (csrc/eig.hip mda_sym_eig_multi) +
+    the post-processing launch; backward = the post-processing launch in D
+    mode (through the eigendecomposition's backward: D = dG + dG^T) + ONE
+    dX = X D launch for every stage.  Same algebra as the composition
+    _GramEig + _KdsvdPost (which the tests pin it against); ~6 launches per
+    step instead of ~100 (profiles/r4_prof_kdsvd.md)."""
+
+    @staticmethod
+    def forward(ctx, k, S, *feats):
+        fs = [_nhwc(f.detach()) for f in feats[:S]]
+        ft = [_nhwc(f.detach()) for f in feats[S:]]
+        N, dev, ks = fs[0].shape[0], fs[0].device, _KDSVD_KSPLIT
+        grams, rows = [], []
+        for a, b in zip(fs, ft):
+            W = a.shape[3]
+            gp = torch.empty(ks, 2 * N, W, W, dtype=torch.float32, device=dev)
+            grams.append(gp)
+            for side, x in ((0, a), (1, b)):
+                _, C, H, _ = x.shape
+                rows.append([x.data_ptr(), gp.data_ptr() + side * N * W * W * 4, 2 * N * W * W,
+                             N, H, W, C, int(x.dtype == torch.bfloat16)])
+        _ext.call("mda_kdsvd_gram", torch.tensor(rows, dtype=torch.int64), len(rows), ks)
+        lams, vecs, erows = [], [], []
+        for gp in grams:
+            W = gp.shape[-1]
+            lam = torch.empty(2 * N, W, dtype=torch.float32, device=dev)
+            vec = torch.empty(2 * N, W, W, dtype=torch.float32, device=dev)
+            lams.append(lam)
+            vecs.append(vec)
+            erows.append([gp.data_ptr(), lam.data_ptr(), vec.data_ptr(), 2 * N * W * W, 2 * N, W, ks])
+        _ext.call("mda_sym_eig_multi", torch.tensor(erows, dtype=torch.int64), len(erows), 8)
+        Ws = [v.shape[-1] for v in vecs]
+        part = torch.empty(N, dtype=torch.float32, device=dev)
+        tab = _kdsvd_table([v[:N] for v in vecs], [v[N:] for v in vecs], [l[N:] for l in lams], None, Ws)
+        _ext.call("mda_kdsvd_post", *tab, S, N, k, part, None, None, None)
+        ctx.save_for_backward(*fs, *lams, *vecs)
+        ctx.meta = (k, S, N, Ws)
+        return part.sum()
+
+    @staticmethod
+    def backward(ctx, go):
+        k, S, N, Ws = ctx.meta
+        t = ctx.saved_tensors
+        fs, lams, vecs = t[:S], t[S:2 * S], t[2 * S:]
+        dev = fs[0].device
+        ds = [torch.empty(N, W, W, dtype=torch.float32, device=dev) for W in Ws]
+        tab = _kdsvd_table([v[:N] for v in vecs], [v[N:] for v in vecs], [l[N:] for l in lams], None, Ws)
+        ls = torch.tensor([l.data_ptr() for l in lams], dtype=torch.int64)  # student rows first
+        dptr = torch.tensor([d.data_ptr() for d in ds], dtype=torch.int64)
+        _ext.call("mda_kdsvd_post", *tab, S, N, k, None, go.detach().float().reshape(1).contiguous(),
+                  ls, dptr)
+        dx = [torch.empty_like(f) for f in fs]
+        rows = [[f.data_ptr(), d.data_ptr(), g.data_ptr(), N, f.shape[2], f.shape[3], f.shape[1],
+                 int(f.dtype == torch.bfloat16)] for f, d, g in zip(fs, ds, dx)]
+        _ext.call("mda_kdsvd_gram_apply", torch.tensor(rows, dtype=torch.int64), S)
+        return (None, None) + tuple(dx) + (None,) * S
+
+
+def kdsvd_native_full_ok(g_s, g_t, k) -> bool:
+    """:class:`_KdsvdNative` serves (on top of :func:`kdsvd_fused_ok`): bf16 /
+    fp32 feature maps, one batch size."""
+    return (kdsvd_fused_ok(g_s, g_t, k)
+            and all(f.dtype in (torch.bfloat16, torch.float32) and f.dim() == 4
+                    and f.shape[0] == g_s[0].shape[0] for f in list(g_s) + list(g_t)))
 
 
 def _kdsvd_table(vs, vt, lt, dvs, W):
@@ -544,17 +629,24 @@ def kdsvd_native_ok(g_s, g_t) -> bool:
     return all(_svd_native_ok(f) for f in list(g_s) + list(g_t))
 
 
-def kdsvd_loss(g_s, g_t, k, native: bool | None = None, fused: bool | None = None):
+def kdsvd_loss(g_s, g_t, k, native: bool | None = None, fused: bool | str | None = None):
     """`distillers/KDSVD.py:8-35`.  ``native`` (default: whenever the shapes
     allow): the SVDs through the Gram eigendecomposition (:class:`_GramEig`);
     else torch.linalg.svd (rocSOLVER, host-synchronising).  Singular vectors
     are defined up to sign; the native path's convention (largest component
     positive) differs from LAPACK's arbitrary one, so the teacher-side signs
     -- and with them the inter-stage RBF terms -- can differ from the
-    reference (parity is pinned on sign-invariant quantities)."""
+    reference (parity is pinned on sign-invariant quantities).
+
+    ``fused`` (GPU): None/True -- :class:`_KdsvdNative` (everything native);
+    "post" -- _GramEig + the fused post-processing; False -- PyTorch ops
+    around the eigensolver."""
     if native is None:
         native = kdsvd_native_ok(g_s, g_t)
+    if native and fused in (None, True) and kdsvd_native_full_ok(g_s, g_t, k):
+        return _KdsvdNative.apply(int(k), len(g_s), *g_s, *g_t)
     if native and fused is not False and kdsvd_fused_ok(g_s, g_t, k):
+        # fused="post": eigendecompositions through _GramEig, post-processing fused
         lts, vts, vss = [], [], []
         for f_s, f_t in zip(g_s, g_t):
             N, C, H, W = f_t.shape

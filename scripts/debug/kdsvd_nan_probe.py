@@ -1,5 +1,7 @@
-"""Where does KDSVD training go non-finite with the fused post-processing?
-Eager fp32 steps, fused vs PyTorch composition, loss + grad norms per step."""
+"""Where does KDSVD training go non-finite?  Two graph runs and two eager
+runs of the same fp32 steps (same init, same data): per-step loss_kd, grad
+norm, finiteness, and the smallest relative eigenvalue gap among the k+3
+leading student eigenvalues (the SVD backward divides by it)."""
 import copy
 import os
 import sys
@@ -19,21 +21,39 @@ cfg.DISTILLER.TYPE = "KDSVD"
 cfg.DISTILLER.TEACHER = "resnet32x4"
 cfg.DISTILLER.STUDENT = "resnet8x4"
 cfg.DISTILLER.RANDOM_TEACHER = True
-d1 = build_distiller(cfg, 100, "cuda")
-d2 = copy.deepcopy(d1)
-orig = FL.kdsvd_loss
-d3 = copy.deepcopy(d1)
-for d, fused, g in ((d1, True, True), (d2, False, True), (d3, True, False)):
-    FL.kdsvd_loss = (lambda *a, _f=fused, **k: orig(*a, fused=_f, **k))
+base = build_distiller(cfg, 100, "cuda")
+gaps = []
+orig_eig = FL._sym_eig
+
+
+def _eig_spy(g):
+    lam, v = orig_eig(g)
+    if not torch.cuda.is_current_stream_capturing():
+        top = lam[:, :8]
+        d = (top[:, :-1] - top[:, 1:]).abs() / top[:, :1].abs().clamp_min(1e-30)
+        gaps.append(float(d.min()))
+    return lam, v
+
+
+FL._sym_eig = _eig_spy
+finals = []
+for run, g in enumerate((True, True, False, False)):
+    d = copy.deepcopy(base)
     d.train()
     st = TrainStep(d, cfg, "cuda", use_graph=g, dtype=torch.float32)
     st.set_epoch(1.0)
     ld = SyntheticLoader("cifar100", 16, "cuda", steps_per_epoch=6, channels_last=True)
     for i, b in enumerate(ld):
+        gaps.clear()
         preds, losses = st.step(b)
         torch.cuda.synchronize()
-        g = st.flat.grads
-        print(f"fused={fused} graph={g} step {i}: loss_kd {float(losses['loss_kd']):.5g} ce {float(losses['loss_ce']):.4g} "
-              f"grad finite {bool(torch.isfinite(g).all())} |g| {float(torch.nan_to_num(g).norm()):.4g} "
-              f"params finite {bool(torch.isfinite(st.flat.data).all())}", flush=True)
-FL.kdsvd_loss = orig
+        gr = st.flat.grads
+        print(f"run {run} graph={g} step {i}: loss_kd {float(losses['loss_kd']):.7g} "
+              f"ce {float(losses['loss_ce']):.7g} |g| {float(torch.nan_to_num(gr).norm()):.6g} "
+              f"grad finite {bool(torch.isfinite(gr).all())} params finite "
+              f"{bool(torch.isfinite(st.flat.data).all())} |p| {float(st.flat.data.double().norm()):.6g} "
+              f"min rel gap {min(gaps) if gaps else float('nan'):.3g}", flush=True)
+    finals.append(st.flat.data.clone())
+for i in range(1, 4):
+    rel = (finals[i].double() - finals[0].double()).norm() / finals[0].double().norm()
+    print(f"final params run {i} vs run 0: rel {float(rel):.3g}", flush=True)

@@ -33,7 +33,7 @@ if [ -n "$PROF" ]; then
     name=${name:-${TAG:-$(basename $cfg .yaml)}}
     extra=${extra:-$EXTRA}
     timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/prof_$name -o run -- python bench.py --cfg $cfg --steps 20 --warmup 10 $extra > gpurun_out/prof_$name.log 2>&1 || { tail -20 gpurun_out/prof_$name.log; exit 1; }
-    python scripts/prof_summary.py gpurun_out/prof_$name/run_results.db --skip 12 --top ${TOP:-40} --md gpurun_out/prof_${name}_summary.md | head -3
+    python scripts/prof_summary.py gpurun_out/prof_$name/run_results.db --skip 12 --top ${TOP:-40} ${BYDISP:+--by-dispatch} --md gpurun_out/prof_${name}_summary.md > /dev/null; head -3 gpurun_out/prof_${name}_summary.md
     python scripts/step_timeline.py gpurun_out/prof_$name/run_results.db > gpurun_out/prof_${name}_timeline.txt
     tail -1 gpurun_out/prof_${name}_timeline.txt
     rm -f gpurun_out/prof_$name/run_results.db

@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--step-kernel", default=r"sgd_kernel|dot_kernel|adam_kernel")
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--md", default=None)
+    ap.add_argument("--by-dispatch", action="store_true",
+                    help="also list one step's dispatches in order with their grid sizes")
     args = ap.parse_args()
     dbs = glob.glob(args.db) if "*" in args.db else [args.db]
     c = sqlite3.connect(dbs[0])
@@ -46,6 +48,19 @@ def main():
     for name, (n, tot) in sorted(agg.items(), key=lambda kv: -kv[1][1])[: args.top]:
         short = name if len(name) < 110 else name[:107] + "..."
         lines.append(f"| {tot / nsteps:.1f} | {100 * tot / nsteps / busy:.1f} | {n / nsteps:.1f} | `{short}` |")
+    if args.by_dispatch:
+        cols = [r[1] for r in c.execute("PRAGMA table_info(kernels)").fetchall()]
+        gcols = [x for x in cols if "grid" in x.lower() or "workgroup" in x.lower()]
+        sel = ", ".join(["name", "start", "end", "duration"] + gcols)
+        last = [m for m in marks][-2:]
+        step = c.execute(f"select {sel} from kernels where start >= ? and end <= ? order by start",
+                         (last[0][2], last[1][2])).fetchall()
+        lines += ["", f"one step in dispatch order ({', '.join(gcols)}):", "",
+                  "| start us | us | kernel | grid |", "|---:|---:|---|---|"]
+        for r in step:
+            short = r[0] if len(r[0]) < 70 else r[0][:67] + "..."
+            lines.append(f"| {(r[1] - last[0][2]) / 1000:.1f} | {r[3] / 1000:.1f} | `{short}` | "
+                         f"{' '.join(str(v) for v in r[4:])} |")
     text = "\n".join(lines)
     print(text)
     if args.md:

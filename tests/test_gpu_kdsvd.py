@@ -82,13 +82,16 @@ def test_kdsvd_training_graph_matches_eager():
     assert rel < 5e-3, rel
 
 
+@pytest.mark.parametrize("fused", [True, "post"])
 @pytest.mark.parametrize("k", [1, 2, 5])
-def test_kdsvd_fused_post_matches_torch_composition(k):
+def test_kdsvd_fused_post_matches_torch_composition(k, fused):
     """csrc/kdsvd.hip (alignment + scaling + RBF + L2, forward and backward in
-    one launch each) == the PyTorch composition on the same eigensolver output."""
+    one launch each; with fused=True also the Grams, the eigensolver's backward
+    and dX = X D natively) == the PyTorch composition on the same eigensolver
+    output."""
     gs, gt = _feats(1, "cuda")
     assert FL.kdsvd_fused_ok(gs, gt, k)
-    lf = FL.kdsvd_loss(gs, gt, k)  # fused (default)
+    lf = FL.kdsvd_loss(gs, gt, k, fused=fused)
     lf.backward()
     gf = [t.grad.clone() for t in gs]
     for t in gs:
@@ -99,3 +102,25 @@ def test_kdsvd_fused_post_matches_torch_composition(k):
     for a, t in zip(gf, gs):
         rel = (a - t.grad).norm() / t.grad.norm().clamp_min(1e-30)
         assert rel < 1e-3, rel
+
+
+@pytest.mark.parametrize("k", [1, 4])
+def test_kdsvd_native_bf16_channels_last(k):
+    """The all-native path on bf16 NHWC feature maps (the training layout)
+    against the composition on the same values in fp32 NCHW."""
+    gs, gt = _feats(2, "cuda")
+    gs_b = [t.detach().to(torch.bfloat16).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+            for t in gs]
+    gt_b = [t.to(torch.bfloat16).contiguous(memory_format=torch.channels_last) for t in gt]
+    gs_f = [t.detach().float().contiguous().requires_grad_(True) for t in gs_b]
+    gt_f = [t.float().contiguous() for t in gt_b]
+    assert FL.kdsvd_native_full_ok(gs_b, gt_b, k)
+    lb = FL.kdsvd_loss(gs_b, gt_b, k)
+    lb.backward()
+    lf = FL.kdsvd_loss(gs_f, gt_f, k, fused=False)
+    lf.backward()
+    torch.testing.assert_close(lb, lf, rtol=1e-4, atol=1e-6)
+    for a, b in zip(gs_b, gs_f):
+        assert a.grad.dtype == torch.bfloat16
+        rel = (a.grad.float() - b.grad).norm() / b.grad.norm().clamp_min(1e-30)
+        assert rel < 1e-2, rel

@@ -82,8 +82,10 @@ SIGNATURES = {
     "mda_dw_pack": "pppiis",
     "mda_dw_fwd": "ppppppp" + "i" * 11 + "s",
     "mda_dw_dgrad": "ppp" + "i" * 10 + "s",
+    "mda_dw_dgrad_bnsum": "ppp" + "i" * 10 + "ppp" + "i" + "pp" + "s",
     "mda_dw_wgrad_blocks": "iiiip",
-    "mda_dw_wgrad": "pppp" + "i" * 12 + "s",
+    "mda_dw_wgrad": "pppp" + "i" * 12 + "pi" + "s",
+    "mda_dw_fwd_bnacc_vin": "pppp" + "i" * 10 + "pppppp" + "ff" + "pi" + "s",
     # training-mode BatchNorm (csrc/bn.hip)
     "mda_bn_stats": "pii" + "pp" + "pppp" + "pppp" + "ffps",
     "mda_bn_apply": "pppppp" + "iii" + "s",

@@ -259,7 +259,7 @@ int launch_kk(const S1Params& p, hipStream_t st) {
 }  // namespace
 
 // Eligibility + launch (host side of conv_igemm.hip's dispatch): 1x1, pad 0,
-// dense, K in {64, 128, 192, 256} (K = Kp), Cout % 64 == 0, stride 1 (or 2
+// dense, K a multiple of 32 up to 256 (weight rows Kp >= K), Cout % 64 == 0, stride 1 (or 2
 // for a forward), large M.  Returns -1 when the shape is not served.
 extern "C" int mda_conv1x1_stream_try(const void* x, const void* w, const float* scale,
                                       const float* bias, const void* res, void* y, void* preact,
@@ -275,7 +275,7 @@ extern "C" int mda_conv1x1_stream_try(const void* x, const void* w, const float*
     return e ? (int64_t)atoll(e) : (int64_t)16384;
   }();
   const int64_t M = N * Ho * Wo;
-  if (!on || K != Kp || K % 64 || K > 256 || Cout % 64 || M < min_m || (stride != 1 && stride != 2))
+  if (!on || Kp < K || K % 32 || K > 256 || Cout % 64 || M < min_m || (stride != 1 && stride != 2))
     return -1;
   if (N * H * W * K >= ((int64_t)1 << 31) || M * Cout >= ((int64_t)1 << 31)) return -1;
   if (((uintptr_t)x | (uintptr_t)y | (uintptr_t)(res ? res : y) | (uintptr_t)(preact ? preact : y)) & 15)
@@ -287,9 +287,13 @@ extern "C" int mda_conv1x1_stream_try(const void* x, const void* w, const float*
   p.Kp = (int)Kp; p.Cout = (int)Cout; p.stride = (int)stride; p.M = (int)M; p.act = (int)act;
   p.ntiles = (int)((M + S_BM - 1) / S_BM);
   switch (K) {
+    case 32: return launch_kk<1>(p, st);   // MobileNetV1's 32 -> 64 at 112^2 (output-bound)
     case 64: return launch_kk<2>(p, st);
+    case 96: return launch_kk<3>(p, st);
     case 128: return launch_kk<4>(p, st);
+    case 160: return launch_kk<5>(p, st);
     case 192: return launch_kk<6>(p, st);
+    case 224: return launch_kk<7>(p, st);
     default: return launch_kk<8>(p, st);
   }
 }

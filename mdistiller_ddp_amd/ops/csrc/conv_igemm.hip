@@ -1866,10 +1866,13 @@ int dispatch(ConvParams& p, int mode, int64_t tile, int64_t splits, hipStream_t 
   // the accumulators; -1 = shape not served, fall through
   if (p.KH == 1 && p.KW == 1 && p.pad == 0 && p.cout_g >= p.Cout && p.ldx == p.Cin &&
       p.bnb_slot == nullptr && p.stats_part == nullptr && p.stamps == nullptr &&
-      (mode == LOAD_FAST || (mode == LOAD_DGRAD_FAST && p.stride == 1))) {
+      (mode == LOAD_FAST || mode == LOAD_VEC8 ||
+       ((mode == LOAD_DGRAD_FAST || mode == LOAD_DGRAD_VEC8) && p.stride == 1))) {
+    // (K = Cin a multiple of 32 is enough there: LOAD_VEC8 covers K = 32 / 96 / ...)
+    const bool fwd = mode == LOAD_FAST || mode == LOAD_VEC8;
     const int rc = mda_conv1x1_stream_try(p.x, p.w, p.scale, p.bias, p.res, p.y, p.preact,
                                           p.stats_slot, p.N, p.H, p.W, p.Cin, p.Kp, p.Ho, p.Wo,
-                                          p.Cout, mode == LOAD_FAST ? p.stride : 1, p.act, st);
+                                          p.Cout, fwd ? p.stride : 1, p.act, st);
     if (rc != -1) return rc;
   }
   p.xcd = use_xcd_remap() ? 1 : 0;

@@ -19,6 +19,8 @@
 // Weights arrive as fp32 packed tap-major [KH*KW, C] (coalesced per-channel
 // loads); folded teacher weights are packed once on the host.  3x3 kernels,
 // stride 1 or 2 (every depthwise layer of the model zoo); others use PyTorch.
+#include <cstdlib>
+
 #include "common.h"
 #include "bnslot.h"
 
@@ -102,10 +104,92 @@ struct DwParams {
   // separate statistics pass; needs a grid stride that is a multiple of C / V
   // (every thread keeps one channel group), see launch_fwd
   BnRegion* stats_slot;
+  // dgrad only (BnLink, csrc/conv_igemm.hip conv_epilogue_bnb): dx is the
+  // whole output gradient of the training BN that produced this conv's input;
+  // the kernel also adds that BN's backward sums (sum dz, sum dz*xhat of the
+  // stored dx through the activation) into bnb_slot
+  const bf16_t* bnb_y;      // that BN's input [N, H, W, C]
+  const bf16_t* bnb_res;    // its residual (activation after the add) or null
+  const float* bnb_stats;   // its [4][C] mean, rstd, scale, shift
+  const float* bnb_vres;    // virtual residual stats [4][C] or null
+  int bnb_act;
+  BnRegion* bnb_slot;
+  // forward only (virtual input, VirtualBN of ops/hip_train.py): x is the RAW
+  // output of a training conv whose BN + activation were never applied; its
+  // batch sums are in in_reg.  Every thread finalizes its channel group's
+  // scale / shift in the prologue (block 0 also writes the [4][C] stats and
+  // the running statistics) and loads act(x * scale + shift) (zero padding
+  // stays zero) -- the producer's apply pass never runs.
+  BnRegion* in_reg;
+  const float* in_gamma; const float* in_beta;
+  float* in_rmean; float* in_rvar; float* in_stats;
+  float in_mom, in_eps;
+  int64_t* in_nbt;
+  int in_act;
 };
 
-template <int V, int S>
-__global__ void __launch_bounds__(256) dw_fwd_kernel(const DwParams p) {
+// BN finalize of channel c from a region (sums of a producer's output over
+// M rows): scale / shift; with `wr` (block 0) also the [4][C] stats and the
+// running statistics (csrc/bn.hip fin_channel, same arithmetic).
+__device__ __forceinline__ void dw_fin_channel(const DwParams& p, int c, int64_t M, bool wr,
+                                               float& sc, float& sh) {
+  const int C = p.C, SH = slot_shards(C);
+  double t0 = 0.0, t1 = 0.0;
+  for (int k = 0; k < SH; ++k) {
+    t0 += region_acc(p.in_reg, C, k, 0)[c];
+    t1 += region_acc(p.in_reg, C, k, 1)[c];
+  }
+  const double mean = t0 / (double)M;
+  double var = t1 / (double)M - mean * mean;
+  if (var < 0) var = 0;
+  const float rstd = (float)(1.0 / sqrt(var + (double)p.in_eps));
+  sc = (p.in_gamma ? p.in_gamma[c] : 1.f) * rstd;
+  sh = (p.in_beta ? p.in_beta[c] : 0.f) - (float)mean * sc;
+  if (wr) {
+    p.in_stats[c] = (float)mean;
+    p.in_stats[C + c] = rstd;
+    p.in_stats[2 * C + c] = sc;
+    p.in_stats[3 * C + c] = sh;
+    if (p.in_rmean) {
+      const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
+      p.in_rmean[c] = (1.f - p.in_mom) * p.in_rmean[c] + p.in_mom * (float)mean;
+      p.in_rvar[c] = (1.f - p.in_mom) * p.in_rvar[c] + p.in_mom * (float)unbiased;
+    }
+  }
+}
+
+// Block channel sums of the per-thread (channel group) partials st1/st2 into
+// a region shard; deterministic: thread t always held channel group
+// (blockIdx.x * 256 + t) % CG (grid stride a multiple of CG, launch_dw), and
+// channel c sums the threads of its group in order.
+template <int V>
+__device__ __forceinline__ void dw_block_sums(BnRegion* slot, int C, const float (&st1)[V],
+                                              const float (&st2)[V]) {
+  const int CG = C / V;
+  __shared__ float red[256][2 * V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    red[threadIdx.x][v] = st1[v];
+    red[threadIdx.x][V + v] = st2[v];
+  }
+  __syncthreads();
+  const int base = (int)(((int64_t)blockIdx.x * blockDim.x) % CG);
+  const int shard = (int)blockIdx.x % slot_shards(C);
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const int g = c / V, e = c - g * V;
+    float a = 0.f, b = 0.f;
+    for (int t = ((g - base) % CG + CG) % CG; t < (int)blockDim.x; t += CG) {
+      a += red[t][e];
+      b += red[t][V + e];
+    }
+    acc_add(region_acc(slot, C, shard, 0) + c, (double)a);
+    acc_add(region_acc(slot, C, shard, 1) + c, (double)b);
+  }
+}
+
+template <int V, int S, bool VIN>
+__global__ void __launch_bounds__(256)
+dw_fwd_kernel(const DwParams p) {
   constexpr int NCOLS = (OWT - 1) * S + KS;
   const int CG = p.C / V;
   const int WT = (p.Wo + OWT - 1) / OWT;
@@ -113,6 +197,26 @@ __global__ void __launch_bounds__(256) dw_fwd_kernel(const DwParams p) {
   float st1[V], st2[V];
 #pragma unroll
   for (int v = 0; v < V; ++v) st1[v] = st2[v] = 0.f;
+  // virtual input: this thread's channel group never changes (grid stride a
+  // multiple of CG, region_grid), so its input scale / shift are finalized once
+  // (a separate instantiation: the plain kernel keeps its register budget)
+  constexpr bool vin = VIN;
+  float isc[V], ish[V];
+  if constexpr (VIN) {
+    // the block finalizes every channel once (LDS), each thread takes its group's
+    __shared__ float s_in[2][SLOT_CMAX];
+    const int64_t Min = (int64_t)p.N * p.H * p.W;
+    for (int c = threadIdx.x; c < p.C; c += blockDim.x)
+      dw_fin_channel(p, c, Min, blockIdx.x == 0, s_in[0][c], s_in[1][c]);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && p.in_nbt) p.in_nbt[0] += 1;
+    __syncthreads();
+    const int c0 = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) % CG) * V;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      isc[v] = s_in[0][c0 + v];
+      ish[v] = s_in[1][c0 + v];
+    }
+  }
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int cg = (int)(i % CG);
@@ -129,6 +233,7 @@ __global__ void __launch_bounds__(256) dw_fwd_kernel(const DwParams p) {
 #pragma unroll
     for (int t = 0; t < KS * KS; ++t) ld_w<V>(p.w + t * p.C + c0, wv[t]);
     typename vec<V>::t raw[KS][NCOLS];
+    uint32_t okm = 0;  // in-bounds taps (zero padding is zero after the input's apply too)
 #pragma unroll
     for (int kh = 0; kh < KS; ++kh) {
       const int ih = ho * S - p.pad + kh;
@@ -137,7 +242,9 @@ __global__ void __launch_bounds__(256) dw_fwd_kernel(const DwParams p) {
 #pragma unroll
       for (int q = 0; q < NCOLS; ++q) {
         const int iw = iw0 + q;
-        raw[kh][q] = ld_raw<V>(row + (int64_t)iw * p.C, okr && (unsigned)iw < (unsigned)p.W);
+        const bool ok = okr && (unsigned)iw < (unsigned)p.W;
+        raw[kh][q] = ld_raw<V>(row + (int64_t)iw * p.C, ok);
+        okm |= (ok ? 1u : 0u) << (kh * NCOLS + q);
       }
     }
     float acc[OWT][V];
@@ -149,7 +256,18 @@ __global__ void __launch_bounds__(256) dw_fwd_kernel(const DwParams p) {
     for (int kh = 0; kh < KS; ++kh) {
       float xin[NCOLS][V];
 #pragma unroll
-      for (int q = 0; q < NCOLS; ++q) unpack<V>(raw[kh][q], xin[q]);
+      for (int q = 0; q < NCOLS; ++q) {
+        unpack<V>(raw[kh][q], xin[q]);
+        if (vin) {
+          const bool ok = (okm >> (kh * NCOLS + q)) & 1u;
+#pragma unroll
+          for (int v = 0; v < V; ++v) {
+            // the producer's apply rounds to bf16: same value here
+            const float z = bf2f(f2bf(act_fn(xin[q][v] * isc[v] + ish[v], p.in_act)));
+            xin[q][v] = ok ? z : 0.f;
+          }
+        }
+      }
 #pragma unroll
       for (int kw = 0; kw < KS; ++kw)
 #pragma unroll
@@ -192,38 +310,30 @@ __global__ void __launch_bounds__(256) dw_fwd_kernel(const DwParams p) {
     }
   }
   if (p.stats_slot == nullptr) return;
-  // block sums per channel, deterministic: thread t always held channel group
-  // (blockIdx.x * 256 + t) % CG; channel c sums the threads of its group in order
-  __shared__ float red[256][2 * V];
-#pragma unroll
-  for (int v = 0; v < V; ++v) {
-    red[threadIdx.x][v] = st1[v];
-    red[threadIdx.x][V + v] = st2[v];
-  }
-  __syncthreads();
-  const int base = (int)(((int64_t)blockIdx.x * blockDim.x) % CG);
-  const int shard = (int)blockIdx.x % slot_shards(p.C);
-  for (int c = threadIdx.x; c < p.C; c += blockDim.x) {
-    const int g = c / V, e = c - g * V;
-    float a = 0.f, b = 0.f;
-    for (int t = ((g - base) % CG + CG) % CG; t < (int)blockDim.x; t += CG) {
-      a += red[t][e];
-      b += red[t][V + e];
-    }
-    acc_add(region_acc(p.stats_slot, p.C, shard, 0) + c, (double)a);
-    acc_add(region_acc(p.stats_slot, p.C, shard, 1) + c, (double)b);
-  }
+  dw_block_sums<V>(p.stats_slot, p.C, st1, st2);
 }
 
 // dx[n, h, w, c] = sum_{kh, kw} dy[n, (h + p - kh)/s, (w + p - kw)/s, c] * w[kh, kw, c]
 // over taps landing on the stride grid.  p.x = dy, p.y = dx; H/W = input dims.
 // S = 1: dx[h, w0 + j] = sum dy[h + p - kh, w0 + j + p - kw] * w[kh, kw], the
 // OWT + 2 dy columns of each of the three rows loaded once, all up front.
-template <int V, int S>
-__global__ void __launch_bounds__(256) dw_dgrad_kernel(const DwParams p) {
+__device__ __forceinline__ float dw_act_grad(float z, int act) {
+  if (act == 1) return z > 0.f ? 1.f : 0.f;
+  if (act == 2) return (z > 0.f && z < 6.f) ? 1.f : 0.f;
+  return 1.f;
+}
+
+template <int V, int S, bool BNB>
+__global__ void __launch_bounds__(256)
+dw_dgrad_kernel(const DwParams p) {
   const int CG = p.C / V;
   const int WT = (p.W + OWT - 1) / OWT;
   const int64_t total = (int64_t)p.N * p.H * WT * CG;
+  constexpr bool bnb = BNB;  // (a separate instantiation, see dw_fwd_kernel)
+  const bool zres = bnb && p.bnb_res != nullptr && p.bnb_act != 0;
+  float st1[V], st2[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) st1[v] = st2[v] = 0.f;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int cg = (int)(i % CG);
@@ -297,13 +407,57 @@ __global__ void __launch_bounds__(256) dw_dgrad_kernel(const DwParams p) {
       }
     }
     }
+    if constexpr (!BNB) {
+#pragma unroll
+      for (int j = 0; j < OWT; ++j) {
+        const int w = w0 + j;
+        if (w >= p.W) break;
+        st_vec<V>(p.y + (((int64_t)n * p.H + h) * p.W + w) * p.C + c0, acc[j]);
+      }
+      continue;
+    } else {
+    // BnLink epilogue: every load first, then the stores and the sums of the
+    // STORED (bf16) values
+    typename vec<V>::t yr[OWT], rr[OWT];
+    const int64_t o0 = (((int64_t)n * p.H + h) * p.W + w0) * p.C + c0;
 #pragma unroll
     for (int j = 0; j < OWT; ++j) {
-      const int w = w0 + j;
-      if (w >= p.W) break;
-      st_vec<V>(p.y + (((int64_t)n * p.H + h) * p.W + w) * p.C + c0, acc[j]);
+      const bool ok = w0 + j < p.W;
+      yr[j] = ld_raw<V>(p.bnb_y + o0 + (int64_t)j * p.C, ok);
+      rr[j] = ld_raw<V>(zres ? p.bnb_res + o0 + (int64_t)j * p.C : p.bnb_y, ok && zres);
+    }
+    float mu[V], rs[V], sc[V], sh[V], vsc[V], vsh[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      mu[v] = p.bnb_stats[c0 + v];
+      rs[v] = p.bnb_stats[p.C + c0 + v];
+      sc[v] = p.bnb_stats[2 * p.C + c0 + v];
+      sh[v] = p.bnb_stats[3 * p.C + c0 + v];
+      vsc[v] = p.bnb_vres ? p.bnb_vres[2 * p.C + c0 + v] : 1.f;
+      vsh[v] = p.bnb_vres ? p.bnb_vres[3 * p.C + c0 + v] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < OWT; ++j) {
+      if (w0 + j >= p.W) break;
+      st_vec<V>(p.y + o0 + (int64_t)j * p.C, acc[j]);
+      float yf[V], rf[V];
+      unpack<V>(yr[j], yf);
+      unpack<V>(rr[j], rf);
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        float d = bf2f(f2bf(acc[j][v]));
+        if (p.bnb_act != 0) {
+          float z = yf[v] * sc[v] + sh[v];
+          if (zres) z += rf[v] * vsc[v] + vsh[v];
+          d *= dw_act_grad(z, p.bnb_act);
+        }
+        st1[v] += d;
+        st2[v] += d * ((yf[v] - mu[v]) * rs[v]);
+      }
+    }
     }
   }
+  if constexpr (BNB) dw_block_sums<V>(p.bnb_slot, p.C, st1, st2);
 }
 
 // Per-block partials of dW[tap, c] = sum_m dy[m, c] * x[src(m, tap), c].
@@ -311,11 +465,11 @@ __global__ void __launch_bounds__(256) dw_dgrad_kernel(const DwParams p) {
 // output pixels of one output row: it loads the 3 x ((OWT-1)*S + 3) input
 // columns and OWT dy vectors once (~5.5 loads per pixel instead of 10, all
 // independent), accumulating acc[9][V].  partial[blk][9][C].
-template <int V, int S>
+template <int V, int S, bool VIN>
 __global__ void __launch_bounds__(256)
 dw_wgrad_partial_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
                         float* __restrict__ partial, int N, int H, int W, int C, int Ho, int Wo,
-                        int pad) {
+                        int pad, const float* __restrict__ in_stats, int in_act) {
   constexpr int NCOLS = (OWT - 1) * S + KS;
   constexpr int KK = KS * KS;
   constexpr int TG = 3;  // taps per reduction round
@@ -329,6 +483,15 @@ dw_wgrad_partial_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__
   const int c0 = cg * V;
   const int WT = (Wo + OWT - 1) / OWT;
   const int64_t items = (int64_t)N * Ho * WT;
+  // virtual input (see DwParams::in_reg): x is the raw producer output, the
+  // input is act(x * scale + shift) from the producer's [4][C] stats
+  constexpr bool vin = VIN;  // (a separate instantiation, see dw_fwd_kernel)
+  float isc[V], ish[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    isc[v] = vin && active ? in_stats[2 * C + c0 + v] : 1.f;
+    ish[v] = vin && active ? in_stats[3 * C + c0 + v] : 0.f;
+  }
   float acc[KK][V];
 #pragma unroll
   for (int t = 0; t < KK; ++t)
@@ -343,6 +506,7 @@ dw_wgrad_partial_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__
       const int wo0 = wt * OWT;
       const int iw0 = wo0 * S - pad;
       typename vec<V>::t draw[OWT], raw[KS][NCOLS];
+      uint32_t okm = 0;
       const bf16_t* drow = dy + (((int64_t)n * Ho + ho) * Wo + wo0) * C + c0;
 #pragma unroll
       for (int j = 0; j < OWT; ++j) draw[j] = ld_raw<V>(drow + (int64_t)j * C, wo0 + j < Wo);
@@ -354,7 +518,9 @@ dw_wgrad_partial_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__
 #pragma unroll
         for (int q = 0; q < NCOLS; ++q) {
           const int iw = iw0 + q;
-          raw[kh][q] = ld_raw<V>(row + (int64_t)iw * C, okr && (unsigned)iw < (unsigned)W);
+          const bool ok = okr && (unsigned)iw < (unsigned)W;
+          raw[kh][q] = ld_raw<V>(row + (int64_t)iw * C, ok);
+          okm |= (ok ? 1u : 0u) << (kh * NCOLS + q);
         }
       }
       float d[OWT][V];
@@ -364,7 +530,17 @@ dw_wgrad_partial_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__
       for (int kh = 0; kh < KS; ++kh) {
         float xin[NCOLS][V];
 #pragma unroll
-        for (int q = 0; q < NCOLS; ++q) unpack<V>(raw[kh][q], xin[q]);
+        for (int q = 0; q < NCOLS; ++q) {
+          unpack<V>(raw[kh][q], xin[q]);
+          if (vin) {
+            const bool ok = (okm >> (kh * NCOLS + q)) & 1u;
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+              const float z = bf2f(f2bf(act_fn(xin[q][v] * isc[v] + ish[v], in_act)));
+              xin[q][v] = ok ? z : 0.f;
+            }
+          }
+        }
 #pragma unroll
         for (int kw = 0; kw < KS; ++kw)
 #pragma unroll
@@ -454,13 +630,37 @@ __global__ void dw_pack_kernel(const float* __restrict__ w, const float* __restr
   }
 }
 
-inline int vwidth(int C) { return (C % 8 == 0) ? 8 : (C % 4 == 0) ? 4 : (C % 2 == 0) ? 2 : 1; }
+// channels per thread, capped at MDA_DW_VMAX (default 4): the V = 8 kernels
+// (16-byte vectors) need 234-256 VGPRs -- 1-2 waves per SIMD -- the V = 4 ones
+// ~150 (3 waves); R50->MV1 6.55 -> 6.40 ms, VGG13->MV2 2.77 -> 2.68
+// (profiles/r4_dw_fusion_ab.md)
+inline int vwidth(int C) {
+  static const int vmax = [] {
+    const char* e = getenv("MDA_DW_VMAX");
+    const int v = e ? atoi(e) : 4;
+    return (v == 1 || v == 2 || v == 8) ? v : 4;
+  }();
+  const int v = (C % 8 == 0) ? 8 : (C % 4 == 0) ? 4 : (C % 2 == 0) ? 2 : 1;
+  return v < vmax ? v : vmax;
+}
 
 inline int grid_for(int64_t work) {
   int64_t b = (work + 255) / 256;
   if (b > 8192) b = 8192;
   if (b < 1) b = 1;
   return (int)b;
+}
+
+// grid of a launch whose threads keep one channel group (region sums): a
+// multiple of the stride period, at most 256 blocks per region shard
+int region_grid(int nb, int C, int V) {
+  const int CG = C / V;
+  int a = CG, b = 256;
+  while (b) { const int t = a % b; a = b; b = t; }
+  const int unit = CG / a;  // blocks per stride period
+  const int cap = 256 * slot_shards(C);
+  nb = nb < cap ? nb : cap;
+  return (nb + unit - 1) / unit * unit;
 }
 
 int launch_fwd(const DwParams& p, hipStream_t st) {
@@ -479,7 +679,11 @@ int launch_fwd(const DwParams& p, hipStream_t st) {
     nb = (nb + unit - 1) / unit * unit;
   }
   const dim3 g(nb);
-#define DW_FWD(VV, SS) hipLaunchKernelGGL((dw_fwd_kernel<VV, SS>), g, dim3(256), 0, st, p)
+#define DW_FWD(VV, SS)                                                                   \
+  do {                                                                                   \
+    if (p.in_reg) hipLaunchKernelGGL((dw_fwd_kernel<VV, SS, true>), g, dim3(256), 0, st, p); \
+    else hipLaunchKernelGGL((dw_fwd_kernel<VV, SS, false>), g, dim3(256), 0, st, p);         \
+  } while (0)
   if (p.stride == 1) {
     if (V == 8) DW_FWD(8, 1); else if (V == 4) DW_FWD(4, 1); else if (V == 2) DW_FWD(2, 1); else DW_FWD(1, 1);
   } else {
@@ -510,17 +714,20 @@ MDA_API int mda_dw_fwd(const void* x, const float* w, const float* scale, const 
   return launch_fwd(p, st);
 }
 
-// dy [N,Ho,Wo,C] bf16 -> dx [N,H,W,C] bf16.
-MDA_API int mda_dw_dgrad(const void* dy, const float* w, void* dx, int64_t N, int64_t H, int64_t W,
-                         int64_t C, int64_t Ho, int64_t Wo, int64_t KH, int64_t KW, int64_t stride,
-                         int64_t pad, hipStream_t st) {
-  if (KH != KS || KW != KS || stride < 1 || stride > 2) return (int)hipErrorInvalidValue;
-  DwParams p{(const bf16_t*)dy, w, nullptr, nullptr, nullptr, (bf16_t*)dx, nullptr, (int)N,
-             (int)H, (int)W, (int)C, (int)Ho, (int)Wo, (int)KH, (int)KW, (int)stride, (int)pad, 0};
+namespace {
+int launch_dgrad(const DwParams& p, hipStream_t st) {
+  const int64_t N = p.N, H = p.H, W = p.W, C = p.C;
+  const int stride = p.stride;
   const int V = vwidth((int)C);
   const int64_t work = N * H * ((W + OWT - 1) / OWT) * (C / V);
-  const dim3 g(grid_for(work));
-#define DW_DG(VV, SS) hipLaunchKernelGGL((dw_dgrad_kernel<VV, SS>), g, dim3(256), 0, st, p)
+  int nb = grid_for(work);
+  if (p.bnb_slot) nb = region_grid(nb, (int)C, V);
+  const dim3 g(nb);
+#define DW_DG(VV, SS)                                                                        \
+  do {                                                                                       \
+    if (p.bnb_slot) hipLaunchKernelGGL((dw_dgrad_kernel<VV, SS, true>), g, dim3(256), 0, st, p); \
+    else hipLaunchKernelGGL((dw_dgrad_kernel<VV, SS, false>), g, dim3(256), 0, st, p);           \
+  } while (0)
   if (stride == 1) {
     if (V == 8) DW_DG(8, 1); else if (V == 4) DW_DG(4, 1); else if (V == 2) DW_DG(2, 1); else DW_DG(1, 1);
   } else {
@@ -528,6 +735,35 @@ MDA_API int mda_dw_dgrad(const void* dy, const float* w, void* dx, int64_t N, in
   }
 #undef DW_DG
   MDA_CHECK_LAUNCH();
+}
+}  // namespace
+
+// dy [N,Ho,Wo,C] bf16 -> dx [N,H,W,C] bf16.
+MDA_API int mda_dw_dgrad(const void* dy, const float* w, void* dx, int64_t N, int64_t H, int64_t W,
+                         int64_t C, int64_t Ho, int64_t Wo, int64_t KH, int64_t KW, int64_t stride,
+                         int64_t pad, hipStream_t st) {
+  if (KH != KS || KW != KS || stride < 1 || stride > 2) return (int)hipErrorInvalidValue;
+  DwParams p{(const bf16_t*)dy, w, nullptr, nullptr, nullptr, (bf16_t*)dx, nullptr, (int)N,
+             (int)H, (int)W, (int)C, (int)Ho, (int)Wo, (int)KH, (int)KW, (int)stride, (int)pad, 0};
+  return launch_dgrad(p, st);
+}
+
+// mda_dw_dgrad + the BnLink epilogue: dx is the whole output gradient of the
+// training BN (input y, residual res, stats, act, virtual-residual stats
+// vres) that produced this conv's input; its backward sums go into region.
+MDA_API int mda_dw_dgrad_bnsum(const void* dy, const float* w, void* dx, int64_t N, int64_t H,
+                               int64_t W, int64_t C, int64_t Ho, int64_t Wo, int64_t KH, int64_t KW,
+                               int64_t stride, int64_t pad, const void* y, const void* res,
+                               const float* stats, int64_t act, void* region, const float* vres,
+                               hipStream_t st) {
+  if (KH != KS || KW != KS || stride < 1 || stride > 2 || region == nullptr || y == nullptr ||
+      stats == nullptr || C > SLOT_CMAX || C % 8)
+    return (int)hipErrorInvalidValue;
+  DwParams p{(const bf16_t*)dy, w, nullptr, nullptr, nullptr, (bf16_t*)dx, nullptr, (int)N,
+             (int)H, (int)W, (int)C, (int)Ho, (int)Wo, (int)KH, (int)KW, (int)stride, (int)pad, 0,
+             nullptr, (const bf16_t*)y, (const bf16_t*)res, stats, vres, (int)act,
+             (BnRegion*)region};
+  return launch_dgrad(p, st);
 }
 
 MDA_API int mda_dw_wgrad_blocks(int64_t N, int64_t Ho, int64_t Wo, int64_t C, int64_t* nblk) {
@@ -553,17 +789,26 @@ MDA_API int mda_dw_wgrad_blocks(int64_t N, int64_t Ho, int64_t Wo, int64_t C, in
 
 // x [N,H,W,C], dy [N,Ho,Wo,C] bf16; partial >= nblk*KH*KW*C floats;
 // grad fp32 [C, KH, KW] (accumulated when accumulate != 0).
+// in_stats (or null): x is a virtual input (raw producer output; the input is
+// act(x * in_stats[2] + in_stats[3]), see DwParams::in_reg).
 MDA_API int mda_dw_wgrad(const void* x, const void* dy, float* partial, float* grad, int64_t N,
                          int64_t H, int64_t W, int64_t C, int64_t Ho, int64_t Wo, int64_t KH,
                          int64_t KW, int64_t stride, int64_t pad, int64_t nblk,
-                         int64_t accumulate, hipStream_t st) {
+                         int64_t accumulate, const float* in_stats, int64_t in_act, hipStream_t st) {
   if (KH != KS || KW != KS || stride < 1 || stride > 2 || nblk < 1) return (int)hipErrorInvalidValue;
   const int V = vwidth((int)C);
   if (C / V > 256) return (int)hipErrorInvalidValue;
 #define DW_WG(VV, SS)                                                                         \
-  hipLaunchKernelGGL((dw_wgrad_partial_kernel<VV, SS>), dim3(nblk), dim3(256), 0, st,        \
-                     (const bf16_t*)x, (const bf16_t*)dy, partial, (int)N, (int)H, (int)W,    \
-                     (int)C, (int)Ho, (int)Wo, (int)pad)
+  do {                                                                                        \
+    if (in_stats)                                                                             \
+      hipLaunchKernelGGL((dw_wgrad_partial_kernel<VV, SS, true>), dim3(nblk), dim3(256), 0, st, \
+                         (const bf16_t*)x, (const bf16_t*)dy, partial, (int)N, (int)H, (int)W,  \
+                         (int)C, (int)Ho, (int)Wo, (int)pad, in_stats, (int)in_act);            \
+    else                                                                                      \
+      hipLaunchKernelGGL((dw_wgrad_partial_kernel<VV, SS, false>), dim3(nblk), dim3(256), 0, st, \
+                         (const bf16_t*)x, (const bf16_t*)dy, partial, (int)N, (int)H, (int)W,  \
+                         (int)C, (int)Ho, (int)Wo, (int)pad, in_stats, (int)in_act);            \
+  } while (0)
   if (stride == 1) {
     if (V == 8) DW_WG(8, 1); else if (V == 4) DW_WG(4, 1); else if (V == 2) DW_WG(2, 1); else DW_WG(1, 1);
   } else {
@@ -589,3 +834,25 @@ MDA_API int mda_dw_fwd_bnacc(const void* x, const float* w, void* y, void* regio
   return launch_fwd(p, st);
 }
 
+// mda_dw_fwd_bnacc with a virtual input (DwParams::in_reg): x is the raw
+// output of a training conv whose BN (region in_reg, affine in_gamma /
+// in_beta, running stats, [4][C] stats out in_stats) + activation in_act this
+// launch applies on load.
+MDA_API int mda_dw_fwd_bnacc_vin(const void* x, const float* w, void* y, void* region, int64_t N,
+                                 int64_t H, int64_t W, int64_t C, int64_t Ho, int64_t Wo,
+                                 int64_t KH, int64_t KW, int64_t stride, int64_t pad, void* in_reg,
+                                 const float* in_gamma, const float* in_beta, float* in_rmean,
+                                 float* in_rvar, float* in_stats, float in_mom, float in_eps,
+                                 int64_t* in_nbt, int64_t in_act, hipStream_t st) {
+  if (KH != KS || KW != KS || stride < 1 || stride > 2 || C > SLOT_CMAX || region == nullptr ||
+      in_reg == nullptr || in_stats == nullptr || C % 8)
+    return (int)hipErrorInvalidValue;
+  DwParams p{(const bf16_t*)x, w, nullptr, nullptr, nullptr, (bf16_t*)y, nullptr, (int)N, (int)H,
+             (int)W, (int)C, (int)Ho, (int)Wo, (int)KH, (int)KW, (int)stride, (int)pad, 0,
+             (BnRegion*)region};
+  p.in_reg = (BnRegion*)in_reg;
+  p.in_gamma = in_gamma; p.in_beta = in_beta;
+  p.in_rmean = in_rmean; p.in_rvar = in_rvar; p.in_stats = in_stats;
+  p.in_mom = in_mom; p.in_eps = in_eps; p.in_nbt = in_nbt; p.in_act = (int)in_act;
+  return launch_fwd(p, st);
+}

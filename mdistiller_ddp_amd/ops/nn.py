@@ -57,7 +57,7 @@ def _bn(x: torch.Tensor, bn: nn.BatchNorm2d) -> torch.Tensor:
 
 def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d | None = None,
                 act: str = "relu", residual: torch.Tensor | None = None,
-                want_preact: bool = False, fork=None, res_fork=None, defer_apply: bool = False):
+                want_preact: bool = False, fork=None, res_fork=None, defer_apply: bool | str = False):
     """``act(bn(conv(x)) + residual)``; returns ``(out, preact_or_None)``.
 
     ``fork`` / ``res_fork`` (:class:`ops.hip_train.GradFork`, optional): x /
@@ -66,7 +66,9 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d | None = No
     ``defer_apply`` (a projection shortcut, ``act="none"``): on the native
     training path the BN apply is left to the one consumer, which must be a
     native conv + BN taking the result as ``residual``
-    (:class:`ops.hip_train.VirtualBN`; see :func:`ops.hip_train.can_defer_residual`)."""
+    (:class:`ops.hip_train.VirtualBN`; see :func:`ops.hip_train.can_defer_residual`);
+    ``defer_apply="dw"``: the one consumer is a native depthwise conv that
+    applies this BN + act on load (:func:`ops.hip_train.can_defer_to_depthwise`)."""
     if hip_enabled_for(x):
         from . import hip_layers
         if hip_layers.conv_supported(x, conv, bn):
@@ -78,6 +80,9 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d | None = No
     if residual is not None and getattr(residual, "_mda_vbn", None) is not None:
         raise RuntimeError("a VirtualBN residual reached a non-native consumer "
                            "(check ops.hip_train.can_defer_residual at the call site)")
+    if getattr(x, "_mda_vbn", None) is not None:
+        raise RuntimeError("a virtual depthwise input reached a non-native consumer "
+                           "(check ops.hip_train.can_defer_to_depthwise at the call site)")
     if hip_enabled_for(x):
         from . import hip_train
         if _TRAIN_KERNELS["on"] and bn is None and hip_train.conv_train_supported(x, conv):

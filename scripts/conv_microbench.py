@@ -50,6 +50,17 @@ IMAGENET = [  # ResNet-50 teacher at batch 64, ResNet-18 student at batch 32
     (32, 256, 14, 256, 3, 1, 1),
     (32, 512, 7, 512, 3, 1, 1),
 ]
+MV1 = [  # MobileNetV1 student pointwise convs at batch 64
+    (64, 32, 112, 64, 1, 1, 0),
+    (64, 64, 56, 128, 1, 1, 0),
+    (64, 128, 56, 128, 1, 1, 0),
+    (64, 128, 28, 256, 1, 1, 0),
+    (64, 256, 28, 256, 1, 1, 0),
+    (64, 256, 14, 512, 1, 1, 0),
+    (64, 512, 14, 512, 1, 1, 0),
+    (64, 512, 7, 1024, 1, 1, 0),
+    (64, 1024, 7, 1024, 1, 1, 0),
+]
 
 
 def timeit(fn, iters):
@@ -108,7 +119,7 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--shape", type=int, default=-1, help="index into SHAPES (-1 = all)")
     ap.add_argument("--ops", default="fwd,mio,wgrad,dgrad")
-    ap.add_argument("--set", default="cifar", choices=["cifar", "imagenet"])
+    ap.add_argument("--set", default="cifar", choices=["cifar", "imagenet", "mv1"])
     ap.add_argument("--graph", action="store_true", help="time hipGraph replays (no CPU overhead)")
     args = ap.parse_args()
     global timeit
@@ -118,7 +129,7 @@ def main():
     from mdistiller_ddp_amd.ops import hip_layers, hip_train
     torch.backends.cudnn.benchmark = True
     rows = []
-    table = SHAPES if args.set == "cifar" else IMAGENET
+    table = {"cifar": SHAPES, "imagenet": IMAGENET, "mv1": MV1}[args.set]
     shapes = table if args.shape < 0 else [table[args.shape]]
     nan = float("nan")
     for (N, Cin, H, Cout, k, s, p) in shapes:

@@ -1,7 +1,7 @@
 """Streaming 1x1 conv (csrc/conv1x1.hip: transposed MFMA, resident weights,
 stores straight from the accumulators) vs PyTorch fp32: inference epilogue
 (folded BN, residual, activation, pre-activation), the training forward with
-BN batch statistics, and the stride-1 dgrad.  Shapes cover K = 64 / 128 / 192 /
+BN batch statistics, and the stride-1 dgrad.  Shapes cover K = 32 / 64 / 96 / 128 / 192 /
 256, 64 / 128 / 256-channel slices, stride 2 and an M tail."""
 import pytest
 import torch
@@ -19,6 +19,9 @@ SHAPES = [  # N, Cin, H, Cout, stride
     (8, 192, 48, 128, 1),   # K = 192
     (3, 64, 99, 128, 1),    # M = 29403: tail tile
     (16, 128, 56, 256, 2),  # stride-2 projection shortcut
+    (8, 32, 112, 64, 1),    # K = 32 on 64-padded weight rows (MobileNetV1's first pointwise)
+    (8, 96, 40, 128, 1),    # K = 96 (Kp = 128)
+    (8, 64, 40, 96, 1),     # dgrad K = 96 (LOAD_DGRAD_VEC8 mode reaches the stream kernel)
 ]
 
 
@@ -78,7 +81,8 @@ def test_stream_train_forward_stats_and_dgrad(shape):
     assert _rel(conv.weight.grad, ref_conv.weight.grad) < 5e-2
 
 
-@pytest.mark.parametrize("shape", [(16, 256, 56, 64), (8, 128, 28, 256), (3, 64, 99, 128)])
+@pytest.mark.parametrize("shape", [(16, 256, 56, 64), (8, 128, 28, 256), (3, 64, 99, 128),
+                                   (8, 64, 40, 96), (8, 64, 112, 32)])
 def test_stream_dgrad(shape):
     """dx = dgrad(dy) of a stride-1 1x1 conv (the stream kernel with W^T)."""
     N, Cin, H, Cout = shape

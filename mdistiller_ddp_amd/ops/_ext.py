@@ -85,6 +85,7 @@ SIGNATURES = {
     "mda_dw_dgrad_bnsum": "ppp" + "i" * 10 + "ppp" + "i" + "pp" + "s",
     "mda_dw_wgrad_blocks": "iiiip",
     "mda_dw_wgrad": "pppp" + "i" * 12 + "pi" + "s",
+    "mda_dw_wgrad_blocks2": "i" * 8 + "p",
     "mda_dw_fwd_bnacc_vin": "pppp" + "i" * 10 + "pppppp" + "ff" + "pi" + "s",
     # training-mode BatchNorm (csrc/bn.hip)
     "mda_bn_stats": "pii" + "pp" + "pppp" + "pppp" + "ffps",

@@ -587,6 +587,249 @@ dw_wgrad_partial_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__
   }
 }
 
+// ---------------------------------------------------------------------------
+// LDS-tiled depthwise forward / weight gradient (pad 1, stride 1 or 2).
+// The register-tiled kernels above load every input vector ~4.5x through the
+// cache hierarchy and need 150-256 VGPRs (1-3 waves per SIMD): latency bound
+// at 15-25 % of HBM rate on the MobileNet layers.  Here a block stages the
+// input rows of `tr` output rows (+ halo, zero padded) for `cc` channels ONCE
+// in LDS (the weight gradient also the tile's dy), and each thread owns one
+// channel of a pixel slice: 9 LDS reads + 9 FMAs per output (forward) or per
+// dy pixel (weight gradient, 9 per-thread accumulators); slices reduce through
+// LDS.  Block = (sample, row tile) x channel chunk; the weight-gradient
+// partial rows keep the [blk][tap][C] layout of dw_wgrad_partial_kernel
+// (same finalize / multi-layer reduce).
+// LDS bytes per block (MDA_DW_TILE_KB, default 24: 6 blocks per CU; A/B 24 / 40 /
+// 64 KB: R50->MV1 6.34 / 6.44 / 6.63 ms, VGG13->MV2 2.62 / 2.61 / 2.61,
+// register kernels 6.41 / 2.70 -- profiles/r4_dw_fusion_ab.md)
+inline int64_t dwt_budget() {
+  static const int64_t b = [] {
+    const char* e = getenv("MDA_DW_TILE_KB");
+    const int64_t k = e ? atoll(e) : 24;
+    return (k >= 8 && k <= 150 ? k : 24) * 1024;
+  }();
+  return b;
+}
+
+__device__ __forceinline__ uint4 dw_vin8(uint4 v, const float* sc, const float* sh, int act) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t o[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float a = act_fn(__uint_as_float(w[k] << 16) * sc[2 * k] + sh[2 * k], act);
+    const float b = act_fn(__uint_as_float(w[k] & 0xffff0000u) * sc[2 * k + 1] + sh[2 * k + 1], act);
+    o[k] = pack_bf16x2(a, b);
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+// x rows [ih0, ih0 + rin) x cols [-1, W] of channels [c0, c0 + cc) -> xs
+// (zero outside the image); VIN: act(x * sc + sh) with sc/sh indexed by the
+// chunk-local channel.
+template <bool VIN>
+__device__ __forceinline__ void dw_fill_x(const bf16_t* __restrict__ x, bf16_t* xs, int n, int H, int W,
+                                          int C, int c0, int cc, int ih0, int rin, const float* vsc,
+                                          const float* vsh, int act) {
+  const int Wp = W + 2, cv = cc / 8;
+  for (int i = threadIdx.x; i < rin * Wp * cv; i += blockDim.x) {
+    const int pos = i / cv, q = i - pos * cv;
+    const int r = pos / Wp, col = pos - r * Wp;
+    const int ih = ih0 + r, iw = col - 1;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) {
+      v = *(const uint4*)(x + (((int64_t)n * H + ih) * W + iw) * C + c0 + 8 * q);
+      if constexpr (VIN) v = dw_vin8(v, vsc + 8 * q, vsh + 8 * q, act);
+    }
+    *(uint4*)(xs + (size_t)pos * cc + 8 * q) = v;
+  }
+}
+
+template <int S, bool VIN>
+__global__ void __launch_bounds__(256) dw_wgrad_tile_kernel(const bf16_t* __restrict__ x,
+                                                            const bf16_t* __restrict__ dy,
+                                                            float* __restrict__ partial, int N, int H,
+                                                            int W, int C, int Ho, int Wo, int tr, int cc,
+                                                            const float* __restrict__ in_stats,
+                                                            int in_act) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t dwt_sm[];
+  __shared__ float s_v[2][64];
+  const int tid = threadIdx.x;
+  const int nrt = (Ho + tr - 1) / tr;
+  const int blk = blockIdx.x, n = blk / nrt, rt = blk - n * nrt;
+  const int c0 = blockIdx.y * cc;
+  const int ho0 = rt * tr, hon = min(tr, Ho - ho0);
+  const int rin = (tr - 1) * S + 3, Wp = W + 2, cv = cc / 8;
+  bf16_t* xs = dwt_sm;
+  bf16_t* ds = dwt_sm + (size_t)rin * Wp * cc;
+  if constexpr (VIN) {
+    if (tid < cc) {
+      s_v[0][tid] = in_stats[2 * C + c0 + tid];
+      s_v[1][tid] = in_stats[3 * C + c0 + tid];
+    }
+    __syncthreads();
+  }
+  dw_fill_x<VIN>(x, xs, n, H, W, C, c0, cc, ho0 * S - 1, rin, s_v[0], s_v[1], in_act);
+  for (int i = tid; i < tr * Wo * cv; i += 256) {
+    const int pos = i / cv, q = i - pos * cv;
+    const int r = pos / Wo, col = pos - r * Wo;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (r < hon) v = *(const uint4*)(dy + (((int64_t)n * Ho + ho0 + r) * Wo + col) * C + c0 + 8 * q);
+    *(uint4*)(ds + (size_t)pos * cc + 8 * q) = v;
+  }
+  __syncthreads();
+  const int c = tid % cc, sl = tid / cc, nsl = 256 / cc;
+  float acc[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) acc[t] = 0.f;
+  for (int r = 0; r < hon; ++r)
+    for (int col = sl; col < Wo; col += nsl) {
+      const float d = bf2f(ds[((size_t)r * Wo + col) * cc + c]);
+      const bf16_t* xb = xs + ((size_t)(r * S) * Wp + col * S) * cc + c;
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) acc[kh * 3 + kw] += d * bf2f(xb[((size_t)kh * Wp + kw) * cc]);
+    }
+  __syncthreads();  // the tiles are dead: the slice reduction reuses the LDS
+  float* red = (float*)dwt_sm;  // [nsl][9][cc]
+#pragma unroll
+  for (int t = 0; t < 9; ++t) red[((size_t)sl * 9 + t) * cc + c] = acc[t];
+  __syncthreads();
+  for (int o = tid; o < 9 * cc; o += 256) {
+    const int t = o / cc, ch = o - t * cc;
+    float a = 0.f;
+    for (int s2 = 0; s2 < nsl; ++s2) a += red[((size_t)s2 * 9 + t) * cc + ch];
+    partial[((int64_t)blk * 9 + t) * C + c0 + ch] = a;
+  }
+}
+
+// Training forward: raw bf16 output + the BN batch sums of the stored values
+// into p.stats_slot (or no statistics).  VIN: p.in_reg finalized per chunk.
+template <int S, bool VIN>
+__global__ void __launch_bounds__(256) dw_fwd_tile_kernel(const DwParams p, int tr, int cc) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t dwt_sm[];
+  __shared__ float s_v[2][64];
+  const int tid = threadIdx.x;
+  const int nrt = (p.Ho + tr - 1) / tr;
+  const int blk = blockIdx.x, n = blk / nrt, rt = blk - n * nrt;
+  const int c0 = blockIdx.y * cc;
+  const int ho0 = rt * tr, hon = min(tr, p.Ho - ho0);
+  const int rin = (tr - 1) * S + 3, Wp = p.W + 2;
+  if constexpr (VIN) {
+    const int64_t Min = (int64_t)p.N * p.H * p.W;
+    if (tid < cc) dw_fin_channel(p, c0 + tid, Min, blk == 0, s_v[0][tid], s_v[1][tid]);
+    if (blk == 0 && blockIdx.y == 0 && tid == 0 && p.in_nbt) p.in_nbt[0] += 1;
+    __syncthreads();
+  }
+  bf16_t* xs = dwt_sm;
+  dw_fill_x<VIN>(p.x, xs, n, p.H, p.W, p.C, c0, cc, ho0 * S - 1, rin, s_v[0], s_v[1], p.in_act);
+  __syncthreads();
+  const int c = tid % cc, sl = tid / cc, nsl = 256 / cc;
+  float wv[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) wv[t] = p.w[t * p.C + c0 + c];
+  float st1 = 0.f, st2 = 0.f;
+  for (int r = 0; r < hon; ++r) {
+    bf16_t* yrow = p.y + (((int64_t)n * p.Ho + ho0 + r) * p.Wo) * p.C + c0 + c;
+    for (int col = sl; col < p.Wo; col += nsl) {
+      const bf16_t* xb = xs + ((size_t)(r * S) * Wp + col * S) * cc + c;
+      float a = 0.f;
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) a += wv[kh * 3 + kw] * bf2f(xb[((size_t)kh * Wp + kw) * cc]);
+      const bf16_t o = f2bf(a);
+      yrow[(int64_t)col * p.C] = o;
+      const float q = bf2f(o);
+      st1 += q;
+      st2 += q * q;
+    }
+  }
+  if (p.stats_slot == nullptr) return;
+  __syncthreads();
+  float* red = (float*)dwt_sm;  // [2][nsl][cc]
+  red[(size_t)sl * cc + c] = st1;
+  red[(size_t)(nsl + sl) * cc + c] = st2;
+  __syncthreads();
+  if (tid < 2 * cc) {
+    const int qq = tid / cc, ch = tid - qq * cc;
+    float a = 0.f;
+    for (int s2 = 0; s2 < nsl; ++s2) a += red[(size_t)(qq * nsl + s2) * cc + ch];
+    const int shard = (int)(blk + gridDim.x * blockIdx.y) % slot_shards(p.C);
+    acc_add(region_acc(p.stats_slot, p.C, shard, qq) + c0 + ch, (double)a);
+  }
+}
+
+// dgrad: dx[h, w] = sum_{kh,kw} w[2-kh, 2-kw] * dyd[h - 1 + kh, w - 1 + kw]
+// with dyd the stride-dilated dy (dy[i/S, j/S] at multiples of S, else 0):
+// the stride-1 forward's tile loop on a (dilated) dy tile with the flipped
+// filter.  p.x = dy [N, Ho, Wo, C], p.y = dx [N, H, W, C].
+template <int S>
+__global__ void __launch_bounds__(256) dw_dgrad_tile_kernel(const DwParams p, int tr, int cc) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t dwt_sm[];
+  const int tid = threadIdx.x;
+  const int nrt = (p.H + tr - 1) / tr;
+  const int blk = blockIdx.x, n = blk / nrt, rt = blk - n * nrt;
+  const int c0 = blockIdx.y * cc;
+  const int h0 = rt * tr, hon = min(tr, p.H - h0);
+  const int rin = tr + 2, Wp = p.W + 2, cv = cc / 8;
+  bf16_t* xs = dwt_sm;
+  for (int i = tid; i < rin * Wp * cv; i += blockDim.x) {
+    const int pos = i / cv, q = i - pos * cv;
+    const int r = pos / Wp, col = pos - r * Wp;
+    const int di = h0 - 1 + r, dj = col - 1;  // dilated dy coordinates
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (di >= 0 && dj >= 0 && di % S == 0 && dj % S == 0 && di / S < p.Ho && dj / S < p.Wo)
+      v = *(const uint4*)(p.x + (((int64_t)n * p.Ho + di / S) * p.Wo + dj / S) * p.C + c0 + 8 * q);
+    *(uint4*)(xs + (size_t)pos * cc + 8 * q) = v;
+  }
+  __syncthreads();
+  const int c = tid % cc, sl = tid / cc, nsl = 256 / cc;
+  float wv[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) wv[t] = p.w[(8 - t) * p.C + c0 + c];
+  for (int r = 0; r < hon; ++r) {
+    bf16_t* xrow = p.y + (((int64_t)n * p.H + h0 + r) * p.W) * p.C + c0 + c;
+    for (int col = sl; col < p.W; col += nsl) {
+      const bf16_t* xb = xs + ((size_t)r * Wp + col) * cc + c;
+      float a = 0.f;
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) a += wv[kh * 3 + kw] * bf2f(xb[((size_t)kh * Wp + kw) * cc]);
+      xrow[(int64_t)col * p.C] = f2bf(a);
+    }
+  }
+}
+
+// Tile plan: output rows per block (tr) and channels per block (cc) so the
+// block's LDS fits dwt_budget(); false = not served (the register kernels run).
+inline bool dw_tile_plan(int H, int W, int C, int Ho, int Wo, int S, int pad, bool with_dy, int& tr,
+                         int& cc) {
+  static const bool on = [] {
+    const char* e = getenv("MDA_DW_TILE");
+    return !(e && e[0] == '0');
+  }();
+  cc = C % 64 == 0 ? 64 : C % 32 == 0 ? 32 : C % 16 == 0 ? 16 : 8;  // channels per block
+  if (!on || pad != 1 || C % cc || (S != 1 && S != 2)) return false;
+  for (int t = Ho < 16 ? Ho : 16; t >= 1; --t) {
+    const int64_t rin = (int64_t)(t - 1) * S + 3;
+    const int64_t bytes = (rin * (W + 2) + (with_dy ? (int64_t)t * Wo : 0)) * cc * 2;
+    if (bytes <= dwt_budget()) {
+      tr = t;
+      return true;
+    }
+  }
+  return false;
+}
+
+inline size_t dw_tile_lds(int W, int Wo, int S, int tr, int cc, bool with_dy) {
+  const size_t rin = (size_t)(tr - 1) * S + 3;
+  const size_t b = (rin * (W + 2) + (with_dy ? (size_t)tr * Wo : 0)) * cc * 2;
+  const size_t red = (size_t)256 * 9 * 4;  // the slice reduction reuses the tile
+  return b > red ? b : red;
+}
+
 // grad[c, tap] (+)= sum_blk partial[blk][tap][c]   (fixed order, fp64)
 // Block = 32 elements x 8 block-slices: thread (e, s) sums the partial blocks
 // b = s (mod 8) with four loads in flight, then slice sums combine in a fixed
@@ -664,6 +907,17 @@ int region_grid(int nb, int C, int V) {
 }
 
 int launch_fwd(const DwParams& p, hipStream_t st) {
+  int tr, cc;
+  if (!p.scale && !p.bias && !p.res && !p.preact && p.act == 0 &&
+      dw_tile_plan(p.H, p.W, p.C, p.Ho, p.Wo, p.stride, p.pad, false, tr, cc)) {
+    const dim3 g((unsigned)(p.N * ((p.Ho + tr - 1) / tr)), (unsigned)(p.C / cc));
+    const size_t lds = dw_tile_lds(p.W, p.Wo, p.stride, tr, cc, false);
+#define DW_FT(SS, VV) hipLaunchKernelGGL((dw_fwd_tile_kernel<SS, VV>), g, dim3(256), lds, st, p, tr, cc)
+    if (p.stride == 1) { if (p.in_reg) DW_FT(1, true); else DW_FT(1, false); }
+    else { if (p.in_reg) DW_FT(2, true); else DW_FT(2, false); }
+#undef DW_FT
+    return (int)hipGetLastError();
+  }
   const int V = vwidth(p.C);
   const int64_t work = (int64_t)p.N * p.Ho * ((p.Wo + OWT - 1) / OWT) * (p.C / V);
   int nb = grid_for(work);
@@ -718,6 +972,14 @@ namespace {
 int launch_dgrad(const DwParams& p, hipStream_t st) {
   const int64_t N = p.N, H = p.H, W = p.W, C = p.C;
   const int stride = p.stride;
+  int tr, cc;
+  if (!p.bnb_slot && dw_tile_plan((int)H, (int)W, (int)C, (int)H, (int)W, 1, p.pad, false, tr, cc)) {
+    const dim3 g((unsigned)(N * ((H + tr - 1) / tr)), (unsigned)(C / cc));
+    const size_t lds = dw_tile_lds((int)W, (int)W, 1, tr, cc, false);
+    if (stride == 1) hipLaunchKernelGGL((dw_dgrad_tile_kernel<1>), g, dim3(256), lds, st, p, tr, cc);
+    else hipLaunchKernelGGL((dw_dgrad_tile_kernel<2>), g, dim3(256), lds, st, p, tr, cc);
+    return (int)hipGetLastError();
+  }
   const int V = vwidth((int)C);
   const int64_t work = N * H * ((W + OWT - 1) / OWT) * (C / V);
   int nb = grid_for(work);
@@ -766,6 +1028,20 @@ MDA_API int mda_dw_dgrad_bnsum(const void* dy, const float* w, void* dx, int64_t
   return launch_dgrad(p, st);
 }
 
+MDA_API int mda_dw_wgrad_blocks(int64_t N, int64_t Ho, int64_t Wo, int64_t C, int64_t* nblk);
+
+// Partial rows of mda_dw_wgrad for this shape (the tile kernel's (sample,
+// row tile) blocks when it serves the shape, else mda_dw_wgrad_blocks').
+MDA_API int mda_dw_wgrad_blocks2(int64_t N, int64_t H, int64_t W, int64_t C, int64_t Ho, int64_t Wo,
+                                 int64_t stride, int64_t pad, int64_t* nblk) {
+  int tr, cc;
+  if (dw_tile_plan((int)H, (int)W, (int)C, (int)Ho, (int)Wo, (int)stride, (int)pad, true, tr, cc)) {
+    *nblk = N * ((Ho + tr - 1) / tr);
+    return 0;
+  }
+  return mda_dw_wgrad_blocks(N, Ho, Wo, C, nblk);
+}
+
 MDA_API int mda_dw_wgrad_blocks(int64_t N, int64_t Ho, int64_t Wo, int64_t C, int64_t* nblk) {
   const int V = vwidth((int)C);
   const int64_t CG = C / V;
@@ -796,6 +1072,20 @@ MDA_API int mda_dw_wgrad(const void* x, const void* dy, float* partial, float* g
                          int64_t KW, int64_t stride, int64_t pad, int64_t nblk,
                          int64_t accumulate, const float* in_stats, int64_t in_act, hipStream_t st) {
   if (KH != KS || KW != KS || stride < 1 || stride > 2 || nblk < 1) return (int)hipErrorInvalidValue;
+  int tr, cc;
+  if (dw_tile_plan((int)H, (int)W, (int)C, (int)Ho, (int)Wo, (int)stride, (int)pad, true, tr, cc)) {
+    const int64_t nb = N * ((Ho + tr - 1) / tr);
+    if (nb != nblk) return (int)hipErrorInvalidValue;  // partial rows sized by mda_dw_wgrad_blocks2
+    const dim3 g((unsigned)nb, (unsigned)(C / cc));
+    const size_t lds = dw_tile_lds((int)W, (int)Wo, (int)stride, tr, cc, true);
+#define DW_WT(SS, VV)                                                                          \
+  hipLaunchKernelGGL((dw_wgrad_tile_kernel<SS, VV>), g, dim3(256), lds, st, (const bf16_t*)x,    \
+                     (const bf16_t*)dy, partial, (int)N, (int)H, (int)W, (int)C, (int)Ho, (int)Wo, \
+                     tr, cc, in_stats, (int)in_act)
+    if (stride == 1) { if (in_stats) DW_WT(1, true); else DW_WT(1, false); }
+    else { if (in_stats) DW_WT(2, true); else DW_WT(2, false); }
+#undef DW_WT
+  } else {
   const int V = vwidth((int)C);
   if (C / V > 256) return (int)hipErrorInvalidValue;
 #define DW_WG(VV, SS)                                                                         \
@@ -815,6 +1105,7 @@ MDA_API int mda_dw_wgrad(const void* x, const void* dy, float* partial, float* g
     if (V == 8) DW_WG(8, 2); else if (V == 4) DW_WG(4, 2); else if (V == 2) DW_WG(2, 2); else DW_WG(1, 2);
   }
 #undef DW_WG
+  }
   if (grad == nullptr) MDA_CHECK_LAUNCH();  // partials only (a deferred multi-layer reduce sums them)
   hipLaunchKernelGGL(dw_wgrad_finalize_kernel, dim3((unsigned)((KH * KW * C + 31) / 32)), dim3(256), 0, st,
                      partial, (int)nblk, (int)(KH * KW), (int)C, grad, (int)accumulate);

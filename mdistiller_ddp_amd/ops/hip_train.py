@@ -701,12 +701,12 @@ def dw_pack(weight, scale=None):
     return out
 
 
-def _dw_wgrad_blocks(N, Ho, Wo, C):
-    key = ("dw", N, Ho, Wo, C)
+def _dw_wgrad_blocks(N, H, W, C, Ho, Wo, stride, pad=1):
+    key = ("dw", N, H, W, C, Ho, Wo, stride, pad)
     v = _WG_PLANS.get(key)
     if v is None:
         b = ctypes.c_int64(0)
-        _ext.call("mda_dw_wgrad_blocks", N, Ho, Wo, C, b)
+        _ext.call("mda_dw_wgrad_blocks2", N, H, W, C, Ho, Wo, stride, pad, b)
         v = _WG_PLANS[key] = b.value
     return v
 
@@ -1276,7 +1276,7 @@ def _dw_backward(ctx, dout, dpre):
             _ext.call("mda_dw_dgrad", dy, wp, dx, N, H, W, C, Ho, Wo, 3, 3, stride, pad)
     dw = None
     if ctx.needs_input_grad[1]:
-        nblk = _dw_wgrad_blocks(N, Ho, Wo, C)
+        nblk = _dw_wgrad_blocks(N, H, W, C, Ho, Wo, stride, pad)
         vin = getattr(ctx, "vin", None)  # virtual input: the activation recomputed on load
         vst, vact = (vin.stats, vin.act) if vin is not None else (None, 0)
         direct_w = weight.grad is not None and weight.grad.is_contiguous()

@@ -22,6 +22,11 @@ SHAPES = [
     (4, 144, 8, 2),
     (2, 960, 7, 1),
     (3, 6, 9, 2),       # 2-wide vectors, odd sizes
+    (2, 32, 112, 1),    # MobileNetV1 112^2 (LDS-tiled kernels: several row tiles)
+    (2, 64, 112, 2),
+    (2, 512, 14, 1),
+    (2, 1024, 7, 1),
+    (3, 40, 20, 2),     # 8-channel chunks
 ]
 
 
@@ -114,7 +119,7 @@ def test_dw_dgrad_wgrad_exact_inputs(shape):
     wp = hip_train.dw_pack(w)
     dx = torch.empty_like(x)
     _ext.call("mda_dw_dgrad", dy, wp, dx, N, H, H, C, Ho, Ho, 3, 3, s, 1)
-    nblk = hip_train._dw_wgrad_blocks(N, Ho, Ho, C)
+    nblk = hip_train._dw_wgrad_blocks(N, H, H, C, Ho, Ho, s)
     part = torch.empty(nblk * 9 * C, device="cuda")
     dw = torch.full_like(w, 1.0)
     _ext.call("mda_dw_wgrad", x, dy, part, dw, N, H, H, C, Ho, Ho, 3, 3, s, 1, nblk, 1, None, 0)

@@ -247,7 +247,11 @@ class GradReducer:
 
     def _signal(self, b) -> None:
         if self._cap_flush is not None:
-            self._cap_flush()
+            # on the CAPTURING stream: the hook that completes a bucket may run
+            # with another current stream (a leaf's AccumulateGrad), and a flush
+            # enqueued there would run once, eagerly, instead of in every replay
+            with torch.cuda.stream(self._cap_stream):
+                self._cap_flush()
         from ..runtime.streams import HipEvent
         ev = HipEvent()  # (torch.cuda.Event(external=True) is refused on ROCm)
         ev.record(external=True, stream=self._cap_stream)

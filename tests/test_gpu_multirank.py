@@ -139,9 +139,10 @@ def _spawn(scenario, world=2):
 @pytest.mark.timeout(600)
 @pytest.mark.xfail(strict=False, reason=(
     "DIST.GRAPH_COMM=events (experimental, not the default) trains bit-identical replicas but "
-    "drifts ~2.5e-2 (relative, 20 steps) from the split path -- also with the replay drained "
-    "before the first all-reduce (MDA_EVENTS_SYNC=1), so not an event-ordering race; root cause "
-    "open (round 4)"))
+    "drifts 8.3e-3 (relative, 20 steps) from the split path.  Round 4 found one cause -- a bucket "
+    "completed inside a hook running on a non-capturing stream flushed its deferred weight-gradient "
+    "reductions there (eagerly, once) instead of into the graph (GradReducer._signal now flushes on "
+    "the capture stream: 2.5e-2 -> 8.3e-3); the rest is open"))
 def test_events_overlap_matches_split():
     """DIST.GRAPH_COMM=events (per-bucket all-reduce behind external events of
     the captured backward, launched right after the replay) trains exactly

@@ -58,6 +58,13 @@ __global__ void __launch_bounds__(256) sym_eig_kernel(EigTable tab, int sweeps) 
   float* __restrict__ vecs = en.vecs;
   const float* gb = en.g + (int64_t)b * n0 * n0;
   const int n = n0 + (n0 & 1);
+  // e -> (e / n, e % n) by shift / mask when n is a power of two (the KDSVD
+  // sizes 8 / 16 / 32): the row / column phases run it every Jacobi step
+  const int lgn = (n & (n - 1)) == 0 ? __builtin_ctz(n) : -1;
+  auto divn = [&](int e, int& a, int& b) {
+    if (lgn >= 0) { a = e >> lgn; b = e & (n - 1); }
+    else { a = e / n; b = e - (e / n) * n; }
+  };
   for (int e = tid; e < n * n; e += nt) {
     const int i = e / n, j = e % n;
     // symmetrise (G is symmetric up to the GEMM's rounding), summing the parts
@@ -76,7 +83,8 @@ __global__ void __launch_bounds__(256) sym_eig_kernel(EigTable tab, int sweeps) 
     {
       double off = 0.0, tot = 0.0;
       for (int e = tid; e < n * n; e += nt) {
-        const int i = e / n, j = e % n;
+        int i, j;
+        divn(e, i, j);
         const double a2 = A[i][j] * A[i][j];
         tot += a2;
         off += i == j ? 0.0 : a2;
@@ -116,7 +124,9 @@ __global__ void __launch_bounds__(256) sym_eig_kernel(EigTable tab, int sweeps) 
       __syncthreads();
       // rows, in place per pair: A <- J^T A
       for (int e = tid; e < half * n; e += nt) {
-        const int k = e / n, j = e % n, p = pp[k], q = qq[k];
+        int k, j;
+        divn(e, k, j);
+        const int p = pp[k], q = qq[k];
         const double c = cs[k][0], s = cs[k][1], ap = A[p][j], aq = A[q][j];
         A[p][j] = c * ap - s * aq;
         A[q][j] = s * ap + c * aq;
@@ -124,7 +134,9 @@ __global__ void __launch_bounds__(256) sym_eig_kernel(EigTable tab, int sweeps) 
       __syncthreads();
       // columns, in place per pair: A <- A J, V <- V J
       for (int e = tid; e < half * n; e += nt) {
-        const int k = e / n, i = e % n, p = pp[k], q = qq[k];
+        int k, i;
+        divn(e, k, i);
+        const int p = pp[k], q = qq[k];
         const double c = cs[k][0], s = cs[k][1], ap = A[i][p], aq = A[i][q];
         A[i][p] = c * ap - s * aq;
         A[i][q] = s * ap + c * aq;

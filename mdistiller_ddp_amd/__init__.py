@@ -14,6 +14,20 @@ import os as _os
 # flagship step (scripts/conv_stamps.py, 1x MI355X).  Read by the HIP runtime
 # at initialisation, so it must be set before the first GPU call; an explicit
 # setting in the environment wins.
-_os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+# The launchers (bench.py, tools/train.py) set it before anything imports torch;
+# this import-time default only covers library use, and warns when it came too
+# late to take effect.
+if "HIP_FORCE_DEV_KERNARG" not in _os.environ:
+    _os.environ["HIP_FORCE_DEV_KERNARG"] = "1"
+    import sys as _sys
+    _t = _sys.modules.get("torch")
+    try:
+        if _t is not None and _t.cuda.is_initialized():
+            import warnings as _w
+            _w.warn("mdistiller_ddp_amd imported after the GPU was initialised: "
+                    "HIP_FORCE_DEV_KERNARG=1 has no effect in this process (set it in the "
+                    "environment, as bench.py and tools/train.py do)", RuntimeWarning)
+    except Exception:  # noqa: BLE001 -- a partially imported torch
+        pass
 
 __version__ = "0.1.0"

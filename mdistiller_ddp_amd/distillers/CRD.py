@@ -76,7 +76,9 @@ class _EmbedFn(torch.autograd.Function):
         need_b = bias is not None and ctx.needs_input_grad[2]
         direct = (need_w and weight.grad is not None and weight.grad.is_contiguous()
                   and (not need_b or bias.grad is not None))
-        dw = weight.grad if direct else (torch.zeros_like(weight) if need_w else None)
+        # the kernel computes db in the same pass as dW: a bias-only gradient
+        # still needs a (scratch) dW target, or db would silently stay zero
+        dw = weight.grad if direct else (torch.zeros_like(weight) if (need_w or need_b) else None)
         db = (bias.grad if direct else torch.zeros_like(bias)) if need_b else None
         dx = torch.empty_like(x) if need_x else None
         dy = torch.empty(N, D, dtype=torch.float32, device=x.device)
@@ -85,7 +87,7 @@ class _EmbedFn(torch.autograd.Function):
         if direct:
             notify_grad(weight, *([bias] if need_b else []))
             return dx, None, None
-        return dx, dw, db
+        return dx, dw if need_w else None, db
 
 
 class Embed(nn.Module):

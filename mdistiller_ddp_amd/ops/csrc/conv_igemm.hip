@@ -103,11 +103,21 @@ struct ConvParams {
   // tiles per group).  Dense: ldx = Cin, cout_g = Cout.
   int ldx, cout_g;
   int xcd;  // glds kernel: XCD-aware tile order (MDA_CONV_XCD, default on)
+  // K-order rotation (MDA_CONV_KROT): block (mt, nt) starts its K loop at step
+  // (mt + nt) mod steps, so the blocks of a wave of the grid do not all read
+  // the same weight tile of the same L2 channel in the same step
+  int krot;
   // halo kernels: multiply-shift divisions by W, H, W + 2, (rows + 2)(W + 2)
   // and rows (set by halo_geometry).  The prologue's ~20 integer divisions
   // by runtime values cost ~1.2 us per block (in-kernel stamps,
   // scripts/conv_stamps.py) -- as much as a third of a 16x16 conv's MFMA loop.
   uint32_t dv_W[2], dv_H[2], dv_PW[2], dv_PHPW[2], dv_RH[2];
+  // glds kernel loader: the same multiply-shift divisions by Cin, KW, Cin / 64,
+  // Ho * Wo, Wo and the stride (set by dispatch).  With generic integer
+  // divisions (and the branches hipcc wraps around them) the per-stage address
+  // math of the strided dgrad was ~1.6 us of VALU per K-step -- the whole
+  // kernel time (scripts/dgrad_stamps.py)
+  uint32_t dv_Cin[2], dv_KW[2], dv_cb[2], dv_HoWo[2], dv_Wo[2], dv_s[2];
 };
 
 // n / d for 0 <= n < 2^31 with the host-made (mul, shr) of d
@@ -691,9 +701,9 @@ conv_fwd_kernel(const ConvParams p) {
         bool ok = kok && nh >= 0 && nw >= 0;
         int ih = nh, iw = nw;
         if (p.stride != 1) {
-          ok = ok && (nh % p.stride == 0) && (nw % p.stride == 0);
-          ih = nh / p.stride;
-          iw = nw / p.stride;
+          ih = hdiv(max(nh, 0), p.dv_s);
+          iw = hdiv(max(nw, 0), p.dv_s);
+          ok = ok && ih * p.stride == nh && iw * p.stride == nw;
         }
         ok = ok && ih < p.H && iw < p.W;
         ra[j] = ld16(xr, sel_off(ok, (a_img[j] + (ih * p.W + iw) * p.Cin + c0) * 2));
@@ -900,21 +910,31 @@ conv_glds_kernel(const ConvParams p) {
     if (m0 >= pcv.Mc) return;                             // whole block past this class
   }
   const int mlim = PAR ? pcv.Mc : p.M;
+  stamp(p, 0);
   EpiPre<BM, BN, 256> pre;
   epi_prefetch(p, pre, m0, n0, BM, PAR);
 
+  // per A row: image base, and the input row / column of tap (0, 0) --
+  // for a strided-dgrad class, the dy row / column of the class's first tap
+  // (dy pixel of class tap (th, tw) = (a_ih0 - th, a_iw0 - tw): no division
+  // per stage)
   int a_img[AROWS], a_ih0[AROWS], a_iw0[AROWS];
 #pragma unroll
   for (int j = 0; j < AROWS; ++j) {
     const int m = m0 + trow + 32 * j;
     const bool ok = m < mlim;
     const int mm = ok ? (PAR ? par_row(p, pcv, m) : m) : 0;
-    const int n = mm / HoWo;
+    const int n = hdiv(mm, p.dv_HoWo);
     const int r = mm - n * HoWo;
-    const int oh = r / p.Wo;
+    const int oh = hdiv(r, p.dv_Wo);
     const int ow = r - oh * p.Wo;
     a_img[j] = n * p.H * p.W * p.ldx + xoff;
-    if (DGRAD) {
+    if (PAR) {
+      // (oh + pad - kh0) is a non-negative multiple of the stride for every
+      // pixel of the class (par_class), up to the tail rows masked below
+      a_ih0[j] = hdiv(oh + p.pad - pcv.kh0 + p.par, p.dv_s) - 1;
+      a_iw0[j] = hdiv(ow + p.pad - pcv.kw0 + p.par, p.dv_s) - 1;
+    } else if (DGRAD) {
       a_ih0[j] = oh + p.pad;
       a_iw0[j] = ow + p.pad;
     } else {
@@ -938,41 +958,54 @@ conv_glds_kernel(const ConvParams p) {
   const int s_begin = zs * p.steps_per_split;
   const int s_end = min(total_steps, s_begin + p.steps_per_split);
 
+  const int nst = s_end - s_begin;
+  const int rot = (p.krot && nst > 1) ? (mt + nt) % nst : 0;
   // issue every copy of stage s into LDS buffer buf (always NL per wave)
   auto issue = [&](int s, int buf) {
     const bool live = s < s_end;
-    s = live ? s : s_begin;
+    if (live) {  // logical step -> rotated physical step
+      s += rot;
+      if (s >= s_end) s -= nst;
+    } else {
+      s = s_begin;
+    }
     int tap, c0;
     bool kok = live;
+    int th = 0, tw = 0;
     if (PAR) {  // class tap t -> real tap; the weight column follows the real tap
-      const int t = s / cin_blocks, cb = s - t * cin_blocks;
-      const int th = t / max(pcv.nkw, 1), tw = t - th * max(pcv.nkw, 1);
+      const int t = hdiv(s, p.dv_cb), cb = s - t * cin_blocks;
+      th = pcv.nkw == 2 ? (t >> 1) : (pcv.nkw == 1 ? t : t / max(pcv.nkw, 1));
+      tw = t - th * pcv.nkw;
       tap = (pcv.kh0 + p.par * th) * p.KW + pcv.kw0 + p.par * tw;
       c0 = cb * BK + chunk * 8;
       s = tap * cin_blocks + cb;
     } else if (FASTK) {
-      tap = s / cin_blocks;
+      tap = hdiv(s, p.dv_cb);
       c0 = (s - tap * cin_blocks) * BK + chunk * 8;
     } else {
       const int k0 = s * BK + chunk * 8;
-      tap = k0 / p.Cin;
+      tap = hdiv(k0, p.dv_Cin);
       c0 = k0 - tap * p.Cin;
       kok = kok && k0 < p.K;
     }
-    const int kh = tap / p.KW, kw = tap - kh * p.KW;
+    const int kh = hdiv(tap, p.dv_KW), kw = tap - kh * p.KW;
     const uint32_t abase = lds0 + (uint32_t)(buf * STAGE) + wave_off;
 #pragma unroll
     for (int j = 0; j < AROWS; ++j) {
       int ih, iw;
       bool ok = kok;
-      if (DGRAD) {
+      if (PAR) {
+        ih = a_ih0[j] - th;
+        iw = a_iw0[j] - tw;
+        ok = ok && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+      } else if (DGRAD) {
         const int nh = a_ih0[j] - kh, nw = a_iw0[j] - kw;
         ok = ok && nh >= 0 && nw >= 0;
         ih = nh; iw = nw;
         if (p.stride != 1) {
-          ok = ok && (nh % p.stride == 0) && (nw % p.stride == 0);
-          ih = nh / p.stride;
-          iw = nw / p.stride;
+          ih = hdiv(max(nh, 0), p.dv_s);
+          iw = hdiv(max(nw, 0), p.dv_s);
+          ok = ok && ih * p.stride == nh && iw * p.stride == nw;
         }
         ok = ok && ih < p.H && iw < p.W;
       } else {
@@ -1034,9 +1067,11 @@ conv_glds_kernel(const ConvParams p) {
   } else {
     issue(s_begin, 0);
     issue(s_begin + 1, 1);
+    stamp(p, 1);
     int cbuf = 0;
     for (int t = 0; t < n; ++t) {
       vm_wait_barrier<NL>();  // stage t landed everywhere; stage t-1 reads retired everywhere
+      if (t == 0) stamp(p, 2);
       const int ibuf = cbuf == 0 ? 2 : cbuf - 1;  // (t + 2) % 3
       issue(s_begin + t + 2, ibuf);
       compute(cbuf);
@@ -1044,7 +1079,12 @@ conv_glds_kernel(const ConvParams p) {
     }
   }
   vm_wait_barrier<0>();  // drain the zero-page prefetches; all reads done before the C tile
+  stamp(p, 3);
   conv_epilogue<BM, BN>(p, acc, smem, m0, n0, BM, pcv, PAR, pre);
+  if (p.stamps != nullptr) {
+    __syncthreads();
+    stamp(p, 4);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1732,6 +1772,14 @@ bool use_xcd_remap() {
   return on;
 }
 
+bool use_krot() {
+  static const bool on = [] {
+    const char* e = getenv("MDA_CONV_KROT");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 bool use_par_dgrad() {
   static const bool on = [] {
     const char* e = getenv("MDA_DGRAD_PARITY");
@@ -1876,6 +1924,13 @@ int dispatch(ConvParams& p, int mode, int64_t tile, int64_t splits, hipStream_t 
     if (rc != -1) return rc;
   }
   p.xcd = use_xcd_remap() ? 1 : 0;
+  p.krot = use_krot() ? 1 : 0;
+  make_hdiv((uint32_t)std::max(p.Cin, 1), p.dv_Cin);
+  make_hdiv((uint32_t)std::max(p.KW, 1), p.dv_KW);
+  make_hdiv((uint32_t)std::max(p.Cin / BK, 1), p.dv_cb);
+  make_hdiv((uint32_t)std::max(p.Ho * p.Wo, 1), p.dv_HoWo);
+  make_hdiv((uint32_t)std::max(p.Wo, 1), p.dv_Wo);
+  make_hdiv((uint32_t)std::max(p.stride, 1), p.dv_s);
   if (p.cout_g < p.Cout) {  // grouped: group-aligned tiles on the glds kernel only
     if (p.Cout % p.cout_g || p.ldx != p.Cin * (p.Cout / p.cout_g) || p.cout_g % 8 || p.Cin % 8)
       return (int)hipErrorInvalidValue;

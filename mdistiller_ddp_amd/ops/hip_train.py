@@ -158,11 +158,14 @@ def _region_pair(C: int, device):
 # kernels that would touch such a gradient (a PyTorch add, a cast) breaks the
 # pairing, which :func:`dual_full` detects and refuses loudly.
 class _Dual:
-    __slots__ = ("gstride", "ptrs")
+    __slots__ = ("gstride", "halves")
 
     def __init__(self, gstride):
         self.gstride = int(gstride)   # set-1 gradient = set-0 view + gstride floats
-        self.ptrs = set()             # bases of the stacked buffers of this backward
+        # base address -> (the set-0 half handed to autograd, its _version): a
+        # gradient is accepted only if it IS that tensor, unmodified -- an
+        # in-place accumulation by autograd (InputBuffer add) bumps the version
+        self.halves = {}
 
 
 _DUAL = [None]
@@ -183,8 +186,17 @@ def dual_alloc(shape, dtype, device, channels_last=True):
     fmt = torch.channels_last if (channels_last and len(shape) == 4) else torch.contiguous_format
     full = torch.empty((2 * shape[0],) + tuple(shape[1:]), dtype=dtype, device=device,
                        memory_format=fmt)
-    _DUAL[0].ptrs.add(full.data_ptr())
-    return full, full[:shape[0]]
+    half = full[:shape[0]]
+    _DUAL[0].halves[full.data_ptr()] = (half, half._version)
+    return full, half
+
+
+def dual_seal(half) -> None:
+    """Re-record ``half``'s version after a PyTorch op wrote its stacked buffer
+    (``torch.add(..., out=full)``): the write is ours, not autograd's."""
+    D = _DUAL[0]
+    if D is not None and half.data_ptr() in D.halves:
+        D.halves[half.data_ptr()] = (half, half._version)
 
 
 def dual_full(g):
@@ -192,9 +204,8 @@ def dual_full(g):
     if g is None:
         return None
     D = _DUAL[0]
-    need = (g.storage_offset() + 2 * g.numel()) * g.element_size()
-    if (D is None or g.data_ptr() not in D.ptrs or g.storage_offset() != 0
-            or g.untyped_storage().nbytes() < need):
+    rec = D.halves.get(g.data_ptr()) if D is not None else None
+    if (rec is None or rec[0] is not g or g._version != rec[1] or g.storage_offset() != 0):
         raise RuntimeError(
             "DOT single-pass backward: a gradient reached a native layer without its stacked "
             "second set (a non-native op in the student's backward?); set "
@@ -773,6 +784,7 @@ def _fork_sum(fork, g):
         gf, of = dual_full(g), dual_full(other)
         full, half = dual_alloc(g.shape, g.dtype, g.device)
         torch.add(gf, of, out=full)
+        dual_seal(half)
         return half
     return g + other
 

@@ -63,6 +63,7 @@ class GradReducer:
         self.bytes_reduced = 0  # bytes put on the wire (tests / accounting)
         self.calls = 0
         self.early_launches = 0  # buckets launched from inside backward (overlap)
+        self.avoid_streams = []  # streams the comm stream must differ from (TrainStep sets them)
         bucket_elems = max(64, int(bucket_mb * (1 << 20) / 4))
         # buckets aligned to parameter boundaries, in flat (= backward) order
         order = sorted(range(len(flat.params)), key=lambda i: flat.offsets[i])
@@ -290,8 +291,12 @@ class GradReducer:
         bucket's all-reduce on the comm stream, each behind its event; the
         caller then runs :meth:`wait_launched` before the optimizer."""
         if self._comm is None:
-            from ..runtime.streams import _fresh_stream
-            self._comm = _fresh_stream(torch.cuda.current_device())
+            from ..runtime import streams as S
+            idx = torch.cuda.current_device()
+            # never one of the step's other live streams (teacher, branch,
+            # wgrad, capture): the bucket all-reduces would queue behind them
+            avoid = [S._streams.get(idx), S._branch_streams.get(idx)] + list(self.avoid_streams)
+            self._comm = S._fresh_stream(idx, avoid)
         # (no wait on the current stream: that would wait for the whole replay;
         # each all-reduce waits only for its bucket's event)
         self._works = {}

@@ -1,68 +1,53 @@
-"""Loss / optimizer parity against the reference implementation's own formulas.
+"""Loss / optimizer parity against the reference implementation's own numbers.
 
-Each test feeds identical fixed-seed tensors to the reference function
-(loaded read-only from /root/reference) and to ours, comparing values and
-gradients in fp32 on CPU.
+Inputs, values and gradients of the reference's functions were stored once
+by ``scripts/gen_ref_fixtures.py`` (``tests/fixtures/ref_losses.safetensors``);
+each test feeds the same tensors to ours and compares in fp32 / fp64 on CPU.
+No reference code is imported or run here.
 """
-import copy
-import math
-
 import pytest
 import torch
 import torch.nn as nn
 
-from tests import _refload as R
+from tests import _fixtures as FX
 from mdistiller_ddp_amd.ops import losses as L
 from mdistiller_ddp_amd.ops import feat_losses as FL
 from mdistiller_ddp_amd.ops.backend import use_backend
 
-pytestmark = pytest.mark.skipif(not R.available(), reason="reference tree not mounted")
+
+def _case(key):
+    return FX.case("ref_losses", key)
 
 
-def _grad_pair(fn_ref, fn_new, *tensors, atol=1e-5, rtol=1e-4, nstudent=None):
-    """Student tensors (the first ``nstudent``, default half) get gradients;
-    teacher tensors are constants, as in training."""
-    ns = len(tensors) // 2 if nstudent is None else nstudent
-    a = [t.clone().requires_grad_(i < ns) for i, t in enumerate(tensors)]
-    b = [t.clone().requires_grad_(i < ns) for i, t in enumerate(tensors)]
-    lr = fn_ref(*a)
-    ln = fn_new(*b)
-    torch.testing.assert_close(ln.reshape(()).double(), lr.reshape(()).double(), atol=atol, rtol=rtol)
-    lr.sum().backward()
-    ln.sum().backward()
-    for x, y in zip(a, b):
-        if x.grad is not None:
-            torch.testing.assert_close(y.grad, x.grad, atol=atol, rtol=rtol)
+def _check(key, fn_new, nstudent=1, atol=1e-5, rtol=1e-4):
+    """Our loss and student gradients vs the stored reference ones."""
+    c = _case(key)
+    n = sum(1 for k in c if k.startswith("in"))
+    ts = [c[f"in{i}"].clone().requires_grad_(i < nstudent) for i in range(n)]
+    loss = fn_new(*ts)
+    torch.testing.assert_close(loss.reshape(()).double(), c["loss"].double(), atol=atol, rtol=rtol)
+    loss.sum().backward()
+    for i in range(nstudent):
+        torch.testing.assert_close(ts[i].grad, c[f"grad{i}"], atol=atol, rtol=rtol)
 
 
 def test_kd_loss():
-    ref = R.load("distillers", "KD")
-    torch.manual_seed(0)
-    s, t = torch.randn(16, 100) * 3, torch.randn(16, 100) * 3
     with use_backend("torch"):
-        _grad_pair(lambda a, b: ref.kd_loss(a, b, 4.0), lambda a, b: L.kd_loss_ref(a, b, 4.0), s, t)
+        _check("kd", lambda a, b: L.kd_loss_ref(a, b, 4.0))
 
 
 def test_dkd_loss():
-    ref = R.load("distillers", "DKD")
-    torch.manual_seed(1)
-    s, t = torch.randn(16, 100) * 3, torch.randn(16, 100) * 3
-    y = torch.randint(0, 100, (16,))
-    _grad_pair(lambda a, b: ref.dkd_loss(a, b, y, 1.0, 8.0, 4.0),
-               lambda a, b: L.dkd_loss_ref(a, b, y, 1.0, 8.0, 4.0), s, t)
+    y = _case("dkd")["target"]
+    _check("dkd", lambda a, b: L.dkd_loss_ref(a, b, y, 1.0, 8.0, 4.0))
 
 
 def test_dkd_closed_form_gradient_matches_autograd():
-    """The fused kernel's analytic DKD gradient (used on GPU) vs autograd of the reference."""
-    ref = R.load("distillers", "DKD")
-    torch.manual_seed(2)
-    B, C, T = 8, 37, 4.0
-    s = (torch.randn(B, C) * 3).double().requires_grad_(True)
-    t = (torch.randn(B, C) * 3).double()
-    y = torch.randint(0, C, (B,))
-    loss = ref.dkd_loss(s, t, y, 1.0, 8.0, T)
-    g, = torch.autograd.grad(loss, s)
-    z = s.detach() / T
+    """The fused kernel's analytic DKD gradient (used on GPU) vs the reference's autograd gradient."""
+    c = _case("dkd64")
+    s, t, y, g = c["in0"], c["in1"], c["target"], c["grad0"]
+    B, C = s.shape
+    T = 4.0
+    z = s / T
     p = torch.softmax(z, 1)
     pt = torch.softmax(t / T, 1)
     gt = torch.zeros(B, C, dtype=torch.bool).scatter_(1, y[:, None], True)
@@ -76,113 +61,73 @@ def test_dkd_closed_form_gradient_matches_autograd():
 
 
 def test_at_loss():
-    ref = R.load("distillers", "AT")
-    torch.manual_seed(3)
-    fs = [torch.randn(4, 8, 16, 16), torch.randn(4, 16, 8, 8)]
-    ft = [torch.randn(4, 32, 16, 16), torch.randn(4, 64, 4, 4)]
-    _grad_pair(lambda a, b, c, d: ref.at_loss([a, b], [c, d], 2),
-               lambda a, b, c, d: FL.at_loss([a, b], [c, d], 2), *fs, *ft)
+    _check("at", lambda a, b, c, d: FL.at_loss([a, b], [c, d], 2), nstudent=2)
 
 
 def test_nst_loss():
-    ref = R.load("distillers", "NST")
-    torch.manual_seed(4)
-    fs, ft = torch.randn(4, 8, 8, 8), torch.randn(4, 16, 8, 8)
-    _grad_pair(lambda a, b: ref.nst_loss([a], [b]), lambda a, b: FL.nst_loss([a], [b]), fs, ft)
+    _check("nst", lambda a, b: FL.nst_loss([a], [b]))
 
 
 def test_nst_gram_form_matches_reference():
     """The closed-form one-Gram NST (used on the GPU) == the reference's
     broadcast polynomial kernels, value and student gradient."""
-    ref = R.load("distillers", "NST")
-    torch.manual_seed(5)
-    fs = torch.randn(4, 16, 8, 8).contiguous(memory_format=torch.channels_last)
-    ft = torch.randn(4, 16, 8, 8).contiguous(memory_format=torch.channels_last)
-    _grad_pair(lambda a, b: ref.nst_loss([a], [b]),
-               lambda a, b: FL.single_stage_nst_loss_gram(a, b), fs, ft)
+    cl = torch.channels_last
+    _check("nst_sq", lambda a, b: FL.single_stage_nst_loss_gram(a.contiguous(memory_format=cl),
+                                                                  b.contiguous(memory_format=cl)))
 
 
 def test_pkt_loss():
-    ref = R.load("distillers", "PKT")
-    torch.manual_seed(5)
-    _grad_pair(ref.pkt_loss, FL.pkt_loss, torch.randn(16, 64), torch.randn(16, 32))
+    _check("pkt", FL.pkt_loss)
 
 
 def test_sp_loss():
-    ref = R.load("distillers", "SP")
-    torch.manual_seed(6)
-    _grad_pair(lambda a, b: ref.sp_loss([a], [b]), lambda a, b: FL.sp_loss([a], [b]),
-               torch.randn(8, 16, 4, 4), torch.randn(8, 32, 4, 4))
+    _check("sp", lambda a, b: FL.sp_loss([a], [b]))
 
 
 @pytest.mark.parametrize("squared", [False, True])
 def test_rkd_loss(squared):
-    ref = R.load("distillers", "RKD")
-    torch.manual_seed(7)
-    _grad_pair(lambda a, b: ref.rkd_loss(a, b, squared, 1e-12, 25, 50),
-               lambda a, b: FL.rkd_loss(a, b, squared, 1e-12, 25, 50),
-               torch.randn(10, 32), torch.randn(10, 64))
+    _check(f"rkd_{int(squared)}", lambda a, b: FL.rkd_loss(a, b, squared, 1e-12, 25, 50))
 
 
 def test_kdsvd_loss():
-    ref = R.load("distillers", "KDSVD")
-    torch.manual_seed(8)
-    fs = [torch.randn(4, 8, 8, 8), torch.randn(4, 16, 4, 4)]
-    ft = [torch.randn(4, 8, 8, 8), torch.randn(4, 16, 4, 4)]
-    lr = ref.kdsvd_loss(fs, ft, 1)
+    c = _case("kdsvd")
+    fs, ft = [c["in0"], c["in1"]], [c["in2"], c["in3"]]
     # the rocSOLVER/LAPACK path: same SVD, same signs as the reference
-    ln = FL.kdsvd_loss(fs, ft, 1, native=False)
-    torch.testing.assert_close(ln, lr, atol=1e-4, rtol=1e-3)
+    torch.testing.assert_close(FL.kdsvd_loss(fs, ft, 1, native=False), c["loss"], atol=1e-4, rtol=1e-3)
 
 
-def test_kdsvd_loss_gram_path_with_reference_signs(monkeypatch):
-    """The Gram-eigensolver path vs the reference once the reference's SVD
-    signs follow the same convention (singular vectors are sign-ambiguous;
-    LAPACK's choice is arbitrary)."""
-    ref = R.load("distillers", "KDSVD")
-    torch.manual_seed(8)
-    fs = [torch.randn(4, 8, 8, 8), torch.randn(4, 16, 4, 4)]
-    ft = [torch.randn(4, 8, 8, 8), torch.randn(4, 16, 4, 4)]
-    ref_svd = ref.svd
-
-    def svd_fixed(feat, n=1):
-        u, s_, v = ref_svd(feat, n)
-        idx = v.abs().argmax(dim=1, keepdim=True)
-        return u, s_, v * torch.where(v.gather(1, idx) < 0, -1.0, 1.0)
-
-    monkeypatch.setattr(ref, "svd", svd_fixed)
-    lr = ref.kdsvd_loss(fs, ft, 1)
-    ln = FL.kdsvd_loss(fs, ft, 1, native=True)
-    torch.testing.assert_close(ln, lr, atol=1e-4, rtol=1e-3)
+def test_kdsvd_loss_gram_path_with_reference_signs():
+    """The Gram-eigensolver path vs the reference run with its SVD signs fixed
+    to the same convention (singular vectors are sign-ambiguous; LAPACK's
+    choice is arbitrary)."""
+    c = _case("kdsvd")
+    fs, ft = [c["in0"], c["in1"]], [c["in2"], c["in3"]]
+    torch.testing.assert_close(FL.kdsvd_loss(fs, ft, 1, native=True), c["loss_signfix"],
+                               atol=1e-4, rtol=1e-3)
 
 
 def test_vid_loss():
-    ref = R.load("distillers", "VID")
-    torch.manual_seed(9)
+    c = _case("vid")
     reg = nn.Sequential(nn.Conv2d(8, 16, 1, bias=False), nn.ReLU(), nn.Conv2d(16, 16, 1, bias=False))
-    ls = nn.Parameter(torch.randn(16))
-    fs, ft = torch.randn(4, 8, 8, 8), torch.randn(4, 16, 4, 4)
-    a = ref.vid_loss(reg, ls, fs, ft, 1e-5)
-    b = FL.vid_loss(reg, ls, fs, ft, 1e-5)
-    torch.testing.assert_close(b, a, atol=1e-5, rtol=1e-5)
+    with torch.no_grad():
+        reg[0].weight.copy_(c["w0"])
+        reg[2].weight.copy_(c["w2"])
+    ls = nn.Parameter(c["log_scale"])
+    torch.testing.assert_close(FL.vid_loss(reg, ls, c["fs"], c["ft"], 1e-5).reshape(()), c["loss"],
+                               atol=1e-5, rtol=1e-5)
 
 
 def test_hcl_loss():
-    ref = R.load("distillers", "ReviewKD")
-    torch.manual_seed(10)
-    fs = [torch.randn(2, 8, 8, 8), torch.randn(2, 16, 1, 1), torch.randn(2, 4, 16, 16)]
-    ft = [torch.randn_like(f) for f in fs]
-    torch.testing.assert_close(FL.hcl_loss(fs, ft), ref.hcl_loss(fs, ft), atol=1e-6, rtol=1e-5)
+    c = _case("hcl")
+    fs, ft = [c[f"in{i}"] for i in range(3)], [c[f"in{i}"] for i in range(3, 6)]
+    torch.testing.assert_close(FL.hcl_loss(fs, ft).reshape(()), c["loss"], atol=1e-6, rtol=1e-5)
 
 
 def test_ofd_feat_loss_and_margin():
-    ref = R.load("distillers", "OFD")
     import importlib
     ofd = importlib.import_module("mdistiller_ddp_amd.distillers.OFD")
-    torch.manual_seed(11)
-    s, t = torch.randn(4, 8, 4, 4), torch.randn(4, 8, 4, 4)
-    m = torch.randn(1, 8, 1, 1) - 1
-    torch.testing.assert_close(ofd.feat_loss(s, t, m), ref.feat_loss(s, t, m))
+    c = _case("ofd")
+    torch.testing.assert_close(ofd.feat_loss(c["s"], c["t"], c["m"]).reshape(()), c["loss"])
     # margin formula (scipy.stats.norm.cdf in the reference vs math.erf here)
     from scipy.stats import norm
     for s_, m_ in [(1.0, 0.3), (0.5, -1.2), (2.0, 4.0)]:
@@ -190,82 +135,50 @@ def test_ofd_feat_loss_and_margin():
 
 
 def test_crd_contrast_loss_and_memory():
-    ref = R.load("distillers", "CRD")
     import importlib
     crd = importlib.import_module("mdistiller_ddp_amd.distillers.CRD")
-    torch.manual_seed(12)
-    x = torch.rand(8, 33) * 1e-3
-    torch.testing.assert_close(crd.ContrastLoss(500)(x), ref.ContrastLoss(500)(x).reshape(()))
+    c = _case("crd")
+    torch.testing.assert_close(crd.ContrastLoss(500)(c["x"]).reshape(()), c["contrast_loss"])
     # memory forward (scores + Z init) and update, with fixed contrast indices
-    N, D, K = 200, 16, 31
-    torch.manual_seed(13)
+    m = _case("crdmem")
+    N, D = m["mem1"].shape
+    K = m["idx"].shape[1] - 1
     mine = crd.ContrastMemory(D, N, K, 0.07, 0.5)
-    theirs = ref.ContrastMemory.__new__(ref.ContrastMemory)
-    nn.Module.__init__(theirs)
-    theirs.n_lem, theirs.K = N, K
-    theirs.register_buffer("params", torch.tensor([K, 0.07, -1, -1, 0.5]))
-    theirs.register_buffer("memory_v1", mine.memory_v1.clone())
-    theirs.register_buffer("memory_v2", mine.memory_v2.clone())
-    v1 = nn.functional.normalize(torch.randn(8, D), dim=1)
-    v2 = nn.functional.normalize(torch.randn(8, D), dim=1)
-    y = torch.arange(8) * 3
-    idx = torch.randint(0, N, (8, K + 1))
-    idx[:, 0] = y
-    a1, a2 = theirs(v1, v2, y, idx)
-    b1, b2 = mine(v1, v2, y, idx)
+    mine.memory_v1.copy_(m["mem1"])
+    mine.memory_v2.copy_(m["mem2"])
+    b1, b2 = mine(m["v1"], m["v2"], m["y"], m["idx"])
     mine.apply_pending()
-    a1, a2 = a1.squeeze(-1), a2.squeeze(-1)  # reference keeps a trailing bmm dim
-    torch.testing.assert_close(b1, a1, rtol=1e-5, atol=1e-7)
-    torch.testing.assert_close(b2, a2, rtol=1e-5, atol=1e-7)
-    torch.testing.assert_close(mine.memory_v1, theirs.memory_v1, rtol=1e-6, atol=1e-7)
-    torch.testing.assert_close(mine.memory_v2, theirs.memory_v2, rtol=1e-6, atol=1e-7)
-    torch.testing.assert_close(mine.params.float(), theirs.params.float())
+    torch.testing.assert_close(b1, m["out1"], rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(b2, m["out2"], rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(mine.memory_v1, m["mem1_after"], rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(mine.memory_v2, m["mem2_after"], rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(mine.params.float(), m["params"])
 
 
 @pytest.mark.parametrize("reach", ["all", "mixed"])
 def test_dot_optimizer_matches_reference(reach):
-    """Flat fused DOT == reference DistillationOrientedTrainer over several steps,
-    including params that receive only a task or only a KD gradient."""
-    ref = R.load("engine", "dot")
+    """Flat fused DOT == the reference DistillationOrientedTrainer's stored
+    5-step trajectory, including params that receive only a task or only a
+    KD gradient."""
     from mdistiller_ddp_amd.engine.optim import FlatParams, FlatDOT
-    torch.manual_seed(14)
-    shapes = [(5, 3), (7,), (4, 4), (3,)]
-    p_ref = [nn.Parameter(torch.randn(s)) for s in shapes]
-    p_new = [nn.Parameter(p.detach().clone()) for p in p_ref]
+    c = _case(f"dot_{reach}")
+    p_new = [nn.Parameter(c[f"p{i}_init"].clone()) for i in range(4)]
     mu, delta, lr, wd = 0.9, 0.075, 0.05, 5e-4
-    opt_ref = ref.DistillationOrientedTrainer(p_ref, lr=lr, momentum=mu - delta,
-                                              momentum_kd=mu + delta, weight_decay=wd)
     flat = FlatParams(p_new, num_grad_sets=2)
     opt = FlatDOT(flat, lr, mu - delta, mu + delta, wd)
-    if reach == "all":
-        has_t = [True] * 4
-        has_k = [True] * 4
-    else:
-        has_t = [True, True, False, True]
-        has_k = [True, False, True, True]
+    has_t = [True] * 4 if reach == "all" else [True, True, False, True]
+    has_k = [True] * 4 if reach == "all" else [True, False, True, True]
     opt.set_reachability(has_t, has_k)
     order = [next(j for j, q in enumerate(flat.params) if q is p) for p in p_new]
     for step in range(5):
-        gt = [torch.randn(s) for s in shapes]
-        gk = [torch.randn(s) for s in shapes]
-        # reference: kd backward -> step_kd -> task backward -> step
-        opt_ref.zero_grad(set_to_none=True)
-        for p, g, k in zip(p_ref, gk, has_k):
-            p.grad = g.clone() if k else None
-        opt_ref.step_kd()
-        opt_ref.zero_grad(set_to_none=True)
-        for p, g, t in zip(p_ref, gt, has_t):
-            p.grad = g.clone() if t else None
-        opt_ref.step()
-        # ours: both grad sets in the flat buffer
         flat.zero_grad()
         for i, p in enumerate(p_new):
             o, n = flat.offsets[order[i]], p.numel()
             if has_t[i]:
-                flat.grads[0, o:o + n] = gt[i].reshape(-1)
+                flat.grads[0, o:o + n] = c[f"s{step}_gt{i}"].reshape(-1)
             if has_k[i]:
-                flat.grads[1, o:o + n] = gk[i].reshape(-1)
+                flat.grads[1, o:o + n] = c[f"s{step}_gk{i}"].reshape(-1)
         with use_backend("torch"):
             opt.step()
-        for a, b in zip(p_ref, p_new):
-            torch.testing.assert_close(b.detach(), a.detach(), atol=1e-6, rtol=1e-5)
+        for i, p in enumerate(p_new):
+            torch.testing.assert_close(p.detach(), c[f"s{step}_p{i}"], atol=1e-6, rtol=1e-5)

@@ -1,75 +1,79 @@
 """ShuffleNetV1 with physically padded groups (models/cifar/shufflenet.py
-BottleneckV1) is the reference network: the reference's own model
-(`mdistiller/models/cifar/ShuffleNetv1.py`, loaded read-only) and ours share a
-state_dict and give the same logits, features and parameter gradients on the
-CPU path; the pad channels stay exactly zero through SGD steps."""
+BottleneckV1) is the reference network: loaded with the reference model's
+state_dict it gives the reference's logits, features and parameter gradients
+(stored once from `mdistiller/models/cifar/ShuffleNetv1.py` by
+``scripts/gen_ref_fixtures.py``, fp64, a narrow groups-3 net with padded
+18/20/30-channel groups) on the CPU path; the pad channels stay exactly zero
+through SGD steps."""
 import pytest
 import torch
 
-from mdistiller_ddp_amd.models.cifar.shufflenet import BottleneckV1, ShuffleV1
-from tests import _refload as R
+from mdistiller_ddp_amd.models.cifar.shufflenet import BottleneckV1, ShuffleNet, ShuffleV1
+from tests import _fixtures as FX
 
-pytestmark = pytest.mark.skipif(not R.available(), reason="reference tree not mounted")
+CFG = {"out_planes": [120, 240, 480], "num_blocks": [2, 2, 2], "groups": 3}  # gen_ref_fixtures.SHUV1_CFG
 
 
-def _pair():
-    ref_mod = R.load_model_module("cifar", "ShuffleNetv1")
-    torch.manual_seed(0)
+def _ref_state():
+    d = FX.load("ref_shufflenetv1")
+    return {k[3:]: v.clone() for k, v in d.items() if k.startswith("sd/")}
 
-    # the reference's ShuffleNet leaves ModelBase.get_arch abstract, so its own
-    # ShuffleV1() cannot be instantiated; supply it to build the same network
-    class Ref(ref_mod.ShuffleNet):
-        def get_arch(self):
-            return "cnn"
-    ref = Ref({"out_planes": [240, 480, 960], "num_blocks": [4, 8, 4], "groups": 3}, num_classes=100)
-    ours = ShuffleV1(num_classes=100)
-    missing = ours.load_state_dict(ref.state_dict(), strict=True)
+
+def _ours():
+    ours = ShuffleNet(CFG, num_classes=100)
+    missing = ours.load_state_dict(_ref_state(), strict=True)
     assert not missing.missing_keys and not missing.unexpected_keys
-    return ref, ours
+    return ours
+
+
+def test_full_size_state_dict_is_the_reference_layout():
+    """The full ShuffleV1 (240/480/960) has the reference checkpoint's keys and shapes."""
+    import json
+    import os
+    with open(os.path.join(FX.DIR, "ref_shufflev1_shapes.json")) as f:
+        ref = json.load(f)
+    ours = {k: list(v.shape) for k, v in ShuffleV1(num_classes=100).state_dict().items()}
+    assert ours == ref
 
 
 def test_state_dict_shapes_are_the_reference():
-    ref, ours = _pair()
-    a, b = ref.state_dict(), ours.state_dict()
-    assert a.keys() == b.keys()
-    for k in a:
-        assert a[k].shape == b[k].shape, k
-        torch.testing.assert_close(a[k], b[k], atol=0, rtol=0)
+    ref = _ref_state()
+    ours = _ours().state_dict()
+    assert ref.keys() == ours.keys()
+    for k in ref:
+        assert ref[k].shape == ours[k].shape, k
+        torch.testing.assert_close(ours[k], ref[k], atol=0, rtol=0)
 
 
 @pytest.mark.parametrize("train", [False, True])
 def test_forward_backward_match_reference(train):
     # float64: the padded network is the same function to round-off (fp32 BN
-    # at 4x4 maps x batch 4 amplifies summation-order noise to ~1e-3)
-    ref, ours = _pair()
-    ref.double().train(train)
-    ours.double().train(train)
-    x = torch.randn(4, 3, 32, 32, dtype=torch.float64)
-    lr, fr = ref(x)
-    lo, fo = ours(x)
-    torch.testing.assert_close(lo, lr, atol=1e-10, rtol=1e-10)
+    # at small maps x batch 2 amplifies summation-order noise)
+    d = FX.load("ref_shufflenetv1")
+    t = f"t{int(train)}"
+    ours = _ours().double().train(train)
+    lo, fo = ours(d["x"].clone())
+    torch.testing.assert_close(lo, d[f"{t}/logits"], atol=1e-10, rtol=1e-10)
     # ours also returns the stem output as f0 (like the other CIFAR models)
-    assert len(fo["feats"]) == len(fr["feats"]) + 1
-    for a, b in zip(fr["feats"], fo["feats"][1:]):
-        torch.testing.assert_close(b, a, atol=1e-10, rtol=1e-10)
+    nref = sum(1 for k in d if k.startswith(f"{t}/feat"))
+    assert len(fo["feats"]) == nref + 1
+    for i in range(nref):
+        torch.testing.assert_close(fo["feats"][i + 1], d[f"{t}/feat{i}"], atol=1e-10, rtol=1e-10)
     if not train:
         return
-    g = torch.randn_like(lr)
-    lr.backward(g)
-    lo.backward(g)
+    lo.backward(d["t1/dlogits"].clone())
     # compare gradients in the reference's (unpadded) layout
-    rg = {n: p.grad for n, p in ref.named_parameters()}
     specs = ours._pad_entries()
     for n, p in ours.named_parameters():
         gr = p.grad
         if n in specs:
             dim, idx = specs[n]
             gr = gr.index_select(dim, torch.tensor(idx))
-        torch.testing.assert_close(gr, rg[n], atol=1e-10, rtol=1e-8, msg=n)
+        torch.testing.assert_close(gr, d[f"grad/{n}"], atol=1e-10, rtol=1e-8, msg=n)
 
 
 def test_pad_channels_stay_zero_under_sgd():
-    _, ours = _pair()
+    ours = _ours()
     ours.train()
     opt = torch.optim.SGD(ours.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-4)
     for _ in range(3):

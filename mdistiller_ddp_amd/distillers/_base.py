@@ -123,6 +123,10 @@ class Vanilla(nn.Module):
     def __init__(self, student: nn.Module):
         super().__init__()
         self.student = student
+        # CE on the logits only: no pre-activation features are stored, so every
+        # native BN backward takes its sums from the consumer's dgrad (BnLink)
+        if hasattr(student, "request_features"):
+            student.request_features(False)
 
     @property
     def module(self):

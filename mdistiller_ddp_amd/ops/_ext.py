@@ -74,7 +74,7 @@ SIGNATURES = {
     "mda_shuffle_tail_fwd": "pppp" + "i" * 7 + "s",
     "mda_shuffle_tail_bwd": "ppppp" + "i" * 7 + "s",
     "mda_pack_conv_weights_pad": "pp" + "i" * 6 + "s",
-    "mda_wgrad_plan": "iiiiiip",
+    "mda_wgrad_plan": "iiiiiiiiiip",
     "mda_pack_conv_weights": "ppp" + "i" * 6 + "s",
     "mda_pack_conv_weights_multi": "piiis",
     "mda_pack_tiles": "iiiip",

@@ -19,6 +19,8 @@
 //         operand), in one launch per conv per step.
 #include "common.h"
 
+extern uint64_t* g_stamps;  // csrc/conv_igemm.hip (mda_conv_set_stamps)
+
 namespace {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
@@ -62,7 +64,17 @@ struct WgParams {
   // backward: two stacked cotangents) reads dy k*M*Cout elements in and owns
   // partial sets [k*zsp, (k+1)*zsp); x is shared.
   int zsp;
+  // halo kernel: a 64-pixel stage is h_img whole images of h_rh rows (W = Wo)
+  int h_rh, h_img;
+  uint64_t* stamps;  // diagnostics: per-block phase stamps (mda_conv_set_stamps), else null
 };
+
+__device__ __forceinline__ void wg_stamp(const WgParams& p, int k) {
+  if (p.stamps != nullptr && threadIdx.x == 0) {
+    const int b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    p.stamps[(int64_t)b * 8 + k] = __builtin_amdgcn_s_memrealtime();
+  }
+}
 
 constexpr uint32_t OOB = 0x80000000u;
 
@@ -432,6 +444,235 @@ conv_wgrad_glds_kernel(const WgParams p) {
       }
 }
 
+// ---------------------------------------------------------------------------
+// Patch-reuse ("halo") weight gradient of a 3x3 / stride-1 / pad-1 conv
+// (Cin, Cout multiples of 64, W in {8, 16, 32}: the CIFAR ResNet bodies).
+// The im2col kernels above give each block one tap's 64-wide k tile, so every
+// input pixel crosses L2 -> LDS nine times and the dy tile once per tap.
+// Here a block owns 64 output channels x 64 input channels x ALL NINE taps:
+// per 64-pixel stage (whole image rows) it stages the dy tile [64 px][64 co]
+// and the input patch [(rows + 2) x (W + 2) px][64 ci] once, and forms the
+// tap operands as shifted views of the patch (the transposing LDS read takes
+// a per-lane row address, so a tap is only a row offset).
+//
+// 12 waves: three groups of four, group g owning the filter row kh = g (three
+// taps, 48 accumulator VGPRs per wave) over the same 2 x 2 (co, ci) wave
+// grid.  Three waves per SIMD keep the MFMA pipe busy while one waits on its
+// LDS reads -- the 4-wave version (nine taps per wave, 144 accumulators, one
+// wave per SIMD) ran its loop at ~38 % MFMA occupancy (rocprofv3
+// SQ_VALU_MFMA_BUSY_CYCLES, scripts/wgrad_stamps.py).  Every wave issues 2-3
+// of a stage's 28 DMA instructions.  Split partials as [splits][Cout][Kp] (the common reduce),
+// staged through LDS so each thread stores 16-byte runs along k.
+constexpr int WGH_PROWS = 160;                  // patch rows per stage (5 DMA rounds of 32)
+constexpr int WGH_XB = WGH_PROWS * 128;         // dy tile offset within a stage
+constexpr int WGH_STAGE = (64 + WGH_PROWS) * 128;  // patch + dy tile: 28 KB
+constexpr int WGH_RING = 5;                     // 140 KB: four stages in flight
+constexpr int WGH_CS = 68;                      // C staging row stride (floats)
+constexpr int WGH_NT = 768;                     // threads per block
+static_assert(3 * 64 * WGH_CS * 4 <= WGH_RING * WGH_STAGE, "C staging fits the ring");
+
+// patch swizzle (even: keeps a lane's 32-B chunk pair): column bits 1 and 3,
+// the latter XOR the image row's parity
+__device__ __forceinline__ int wgh_swz(int ir, int ic) {
+  return (((ic >> 1) & 1) | ((((ic >> 3) ^ ir) & 1) << 1)) << 1;
+}
+
+__global__ void __launch_bounds__(WGH_NT)
+conv_wgrad_halo_kernel(const WgParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[WGH_RING * WGH_STAGE];
+  typedef __attribute__((address_space(3))) char lds_char;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_char*)smem;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int kh = __builtin_amdgcn_readfirstlane(wid >> 2);  // this wave's filter row
+  const int wq = wid & 3, wm = wq >> 1, wn = wq & 1;
+  // XCD-aware block order: hardware block b runs on XCD b % 8; each XCD gets a
+  // contiguous run of (co tile, ci tile, split) in that order, so the blocks
+  // that read the same x chunk / dy chunk of a split share an L2
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int nwg = gx * gy * gridDim.z;
+  const int bid = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  int wg = bid;
+  {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int bx = wg % gx, by = (wg / gx) % gy, bz = wg / (gx * gy);
+  const int co0 = bx * 64;
+  const int ci0 = by * 64;
+  const int zset = bz / p.zsp;
+  const int m_begin = (bz - zset * p.zsp) * p.m_per_split;
+  const int m_end = min(p.M, m_begin + p.m_per_split);
+  const bf16_t* const dyp = p.dy + (int64_t)zset * p.M * p.Cout;
+  const bf16_t* const zero = (const bf16_t*)g_wg_zero16;
+  const int W = p.W, H = p.H, HW = H * W;
+  const int RH = p.h_rh, PW = W + 2, PHPW = (RH + 2) * PW, P = p.h_img * PHPW;
+  wg_stamp(p, 0);
+
+  // Stage layout: patch rows [0, 160) (byte 0), dy rows after (byte WGH_XB).
+  // A DMA instruction writes 8 rows of 128 B (lane-linear);
+  // LDS slot tid & 7 of a row holds global 16-B chunk slot ^ swizzle.  dy rows
+  // (read at aligned row groups) use wg_swz(row); patch rows use
+  // wgh_swz(image row, column): the tap views read rows at any shift, and
+  // keying the XOR on the pixel's column bits 1 / 3 and its image row's
+  // parity keeps every 32-lane transposing read conflict-free for W = 8, 16
+  // and 32 (a row-index key conflicts 2-way at W = 8).
+  // Waves 0-3 issue the stage DMAs (7 per wave): round j of 32 rows covers
+  // patch rows 32 j .. (j < 5), then dy rows (j = 5, 6).  (Spreading the 28
+  // DMA instructions over all 12 waves measured slower: loop 10.0 vs 9.0 us.)
+  const int trow = (tid & 255) >> 3, slot = tid & 7;
+  const bool loader = wid < 4;
+  const uint32_t wave_off = (uint32_t)__builtin_amdgcn_readfirstlane(wq) * 1024u;
+  int d_off[2];
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {
+    const int r = trow + 32 * d;
+    d_off[d] = r * p.Cout + co0 + ((slot ^ wg_swz(r)) << 3);
+  }
+  int x_rel[5], x_ir[5];
+  bool x_ok[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const int pr = trow + 32 * j;
+    const int img = pr / PHPW, rem = pr - img * PHPW;
+    const int ir = rem / PW, ic = rem - ir * PW;
+    x_ok[j] = pr < P && (unsigned)(ic - 1) < (unsigned)W;
+    x_ir[j] = pr < P ? ir - 1 : -(1 << 20);
+    x_rel[j] = ((img * H + ir - 1) * W + ic - 1) * p.Cin + ci0 + ((slot ^ wgh_swz(ir, ic)) << 3);
+  }
+
+  auto issue = [&](int mb, int buf) {  // stage of 64 pixels from mb (7 DMAs per loader wave)
+    if (!loader) return;
+    const uint32_t base = lds0 + (uint32_t)(buf * WGH_STAGE) + wave_off;
+    const bool live = mb < m_end;
+    const int mm = live ? mb : 0;
+    const int n0 = mm / HW, oh0 = (mm - n0 * HW) / W;
+    const bf16_t* xb = p.x + ((int64_t)n0 * HW + oh0 * W) * p.Cin;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const bool ok = live && x_ok[j] && (unsigned)(oh0 + x_ir[j]) < (unsigned)H;
+      wg_glds16(ok ? xb + x_rel[j] : zero, base + (uint32_t)(j * 4096));
+    }
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+      wg_glds16(live ? dyp + ((int64_t)mm * p.Cout + d_off[d]) : zero,
+                base + (uint32_t)(WGH_XB + d * 4096));
+  };
+
+  f32x4 acc[3][2][2];  // [kw][co 16-block][ci 16-block]
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[t][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // Transposing reads: lane 16 g + 4 q + pp supplies the address of pixel
+  // 8 g + q (lo) / 8 g + q + 4 (hi) of a 32-pixel half, 8 bytes at column
+  // c0 + 4 pp, and receives column c0 + (lane & 15) of pixels 8 g .. 8 g + 7.
+  // Every address within a stage is fixed per lane, so they are made here.
+  // The second 16-column fragment of a wave (chunk + 2) is the first one's
+  // address XOR 32: the lane's chunk c has bit 1 clear and every swizzle is
+  // even, so (c + 2) ^ s = (c ^ s) ^ 2.
+  const int fg = lane >> 4, fq = (lane >> 2) & 3, fp = lane & 3;
+  int xa[2][3][2];  // [kk][kw][lo/hi]: patch byte offsets of fragment 0
+  int da[2][2];     // [kk][lo/hi]: dy byte offsets of fragment 0
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int m = kk * 32 + 8 * fg;  // 8 consecutive pixels in one image row (W % 8 == 0)
+    const int img = m / (RH * W), rr = m - img * RH * W;
+    const int r = rr / W, c = rr - r * W + fq;
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int ir = r + kh, ic = c + kw + 4 * h;
+        const int row = img * PHPW + ir * PW + ic;
+        xa[kk][kw][h] = row * 128 + (((wn * 4 + (fp >> 1)) ^ wgh_swz(ir, ic)) << 4) + (fp & 1) * 8;
+      }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int row = kk * 32 + 8 * fg + fq + 4 * h;
+      da[kk][h] = WGH_XB + row * 128 + (((wm * 4 + (fp >> 1)) ^ wg_swz(row)) << 4) + (fp & 1) * 8;
+    }
+  }
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  auto rd2 = [&](const char* base, int lo, int hi) {
+    s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + lo));
+    s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + hi));
+    bf16x8 out;
+    short* o = (short*)&out;
+    o[0] = a[0]; o[1] = a[1]; o[2] = a[2]; o[3] = a[3];
+    o[4] = b[0]; o[5] = b[1]; o[6] = b[2]; o[7] = b[3];
+    return out;
+  };
+  auto compute = [&](const char* S) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[2];
+      af[0] = rd2(S, da[kk][0], da[kk][1]);
+      af[1] = rd2(S, da[kk][0] ^ 32, da[kk][1] ^ 32);
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        bf16x8 bfr[2];
+        bfr[0] = rd2(S, xa[kk][kw][0], xa[kk][kw][1]);
+        bfr[1] = rd2(S, xa[kk][kw][0] ^ 32, xa[kk][kw][1] ^ 32);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[kw][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[kw][i][j], 0, 0, 0);
+      }
+    }
+  };
+
+  const int n = (m_end - m_begin + 63) / 64;
+#pragma unroll
+  for (int s0 = 0; s0 < WGH_RING - 1; ++s0) issue(m_begin + s0 * 64, s0);
+  wg_stamp(p, 1);
+  int cbuf = 0;
+  for (int t = 0; t < n; ++t) {
+    // loaders: stage t landed (the 7 DMAs of each of the RING - 2 younger
+    // stages still in flight); the barrier publishes it and retires every
+    // wave's reads of the slot stage t + RING - 1 overwrites (stage t - 1's)
+    wg_wait_barrier<7 * (WGH_RING - 2)>();
+    if (t == 0) wg_stamp(p, 2);
+    const int ibuf = cbuf == 0 ? WGH_RING - 1 : cbuf - 1;  // (t + RING - 1) % RING
+    issue(m_begin + (t + WGH_RING - 1) * 64, ibuf);
+    compute(smem + cbuf * WGH_STAGE);
+    cbuf = cbuf == WGH_RING - 1 ? 0 : cbuf + 1;
+  }
+  wg_wait_barrier<0>();  // zero-page prefetches drained, every fragment read retired
+  wg_stamp(p, 3);
+
+  // partials: round kw stages the three taps (kh, kw) of all groups, then
+  // 16-byte stores along k (partial[z][co][tap * Cin + ci])
+  float* Cs = (float*)smem;
+  const int ecol = lane & 15, erow = (lane >> 4) * 4;
+  float* const dst0 = p.partial + ((int64_t)bz * p.Cout + co0) * p.Kp + ci0;
+#pragma unroll
+  for (int kw = 0; kw < 3; ++kw) {
+    if (kw) __syncthreads();  // the previous round's stores have read the staging area
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          Cs[(kh * 64 + wm * 32 + i * 16 + erow + r) * WGH_CS + wn * 32 + j * 16 + ecol] = acc[kw][i][j][r];
+    __syncthreads();
+    for (int f = tid; f < 3 * 1024; f += WGH_NT) {
+      const int g = f >> 10, rem = f & 1023, row = rem >> 4, c4 = rem & 15;
+      const float4 v = *(const float4*)&Cs[(g * 64 + row) * WGH_CS + 4 * c4];
+      *(float4*)(dst0 + (int64_t)row * p.Kp + (3 * g + kw) * p.Cin + 4 * c4) = v;
+    }
+  }
+  if (p.stamps != nullptr) {
+    __syncthreads();
+    wg_stamp(p, 4);
+  }
+}
+
 // grad[co][ci][kh][kw] (+)= scale * sum_s partial[s][co][(kh*KW+kw)*Cin+ci]
 // Block = 16 float4 columns (64 packed (co, k) elements) x 16 set-slices:
 // thread (c, sl) sums the partial sets s = sl (mod 16), two loads in flight,
@@ -793,8 +1034,51 @@ static int wg_tile(int64_t M, int64_t Cout, int64_t Cin, int64_t KH, int64_t KW,
   return M >= 20000 ? 64128 : 0;
 }
 
+// The halo kernel's stage geometry: 64 output pixels = img whole images of
+// rh rows (false: not served).
+static bool wg_halo_geom(int64_t H, int64_t W, int64_t* rh, int64_t* img) {
+  if (W % 8 || W > 32 || H <= 0) return false;
+  if (H * W >= 64) {
+    if (64 % W || H % (64 / W)) return false;
+    *rh = 64 / W;
+    *img = 1;
+  } else {
+    if (64 % (H * W)) return false;
+    *rh = H;
+    *img = 64 / (H * W);
+  }
+  return *img * (*rh + 2) * (W + 2) <= WGH_PROWS;
+}
+
+static bool wg_halo_ok(int64_t M, int64_t Cout, int64_t Cin, int64_t KH, int64_t KW, int64_t H,
+                       int64_t W, int64_t stride, int64_t pad) {
+  static const bool on = [] {
+    const char* e = getenv("MDA_WG_HALO");
+    return !(e && e[0] == '0');
+  }();
+  int64_t rh, img;
+  return on && KH == 3 && KW == 3 && stride == 1 && pad == 1 && Cin % 64 == 0 && Cout % 64 == 0 &&
+         M % 64 == 0 && wg_halo_geom(H, W, &rh, &img);
+}
+
+// halo kernel splits: MDA_WGH_BLOCKS (default 128) blocks, >= 2 stages each
+static int64_t wg_halo_splits(int64_t M, int64_t Cout, int64_t Cin) {
+  static const int64_t target = [] {
+    const char* e = getenv("MDA_WGH_BLOCKS");
+    return e ? (int64_t)atoi(e) : (int64_t)128;
+  }();
+  const int64_t tiles = (Cout / 64) * (Cin / 64), stages = M / 64;
+  int64_t sp = (target + tiles - 1) / tiles;
+  sp = std::min<int64_t>(sp, std::max<int64_t>(1, stages / 2));
+  return std::max<int64_t>(1, std::min<int64_t>(sp, 128));
+}
+
 MDA_API int mda_wgrad_plan(int64_t M, int64_t Cout, int64_t Cin, int64_t KH, int64_t KW, int64_t Kp,
-                           int64_t* splits) {
+                           int64_t H, int64_t W, int64_t stride, int64_t pad, int64_t* splits) {
+  if (wg_halo_ok(M, Cout, Cin, KH, KW, H, W, stride, pad)) {
+    *splits = wg_halo_splits(M, Cout, Cin);
+    return 0;
+  }
   const int tile = wg_tile(M, Cout, Cin, KH, KW, Kp);
   int64_t sp = 1;
   if (tile == 0) {
@@ -837,15 +1121,23 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* partial, float*
   if (xb >= ((int64_t)1 << 31) || db >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
   p.x_bytes = (int)xb;
   p.dy_bytes = (int)db;
+  p.stamps = g_stamps;
   p.div_howo = make_fastdiv((uint32_t)(Ho * Wo));
   p.div_wo = make_fastdiv((uint32_t)Wo);
-  if (splits <= 0) mda_wgrad_plan(p.M, Cout, Cin, KH, KW, Kp, &splits);
+  if (splits <= 0) mda_wgrad_plan(p.M, Cout, Cin, KH, KW, Kp, H, W, stride, pad, &splits);
   p.m_per_split = (int)(((p.M + splits - 1) / splits + TM - 1) / TM * TM);
   p.zsp = (int)splits;
   const int mode = (Cin % TK == 0) ? WG_FAST : (Cin % 8 == 0 ? WG_VEC8 : WG_SCALAR);
   dim3 grid((int)((Cout + TC - 1) / TC), (int)(Kp / TK), (int)(splits * nsets));
   const int tile = mode == WG_SCALAR ? 0 : wg_tile(p.M, Cout, Cin, KH, KW, Kp);
-  if (tile != 0) {
+  int64_t hrh = 0, himg = 0;
+  if (groups <= 1 && cin_keep == Cin && Kp == 9 * Cin &&
+      wg_halo_ok(p.M, Cout, Cin, KH, KW, H, W, stride, pad) && wg_halo_geom(H, W, &hrh, &himg)) {
+    p.h_rh = (int)hrh;
+    p.h_img = (int)himg;
+    dim3 gh((int)(Cout / 64), (int)(Cin / 64), (int)(splits * nsets));
+    hipLaunchKernelGGL(conv_wgrad_halo_kernel, gh, dim3(WGH_NT), 0, st, p);
+  } else if (tile != 0) {
     const int tc = tile / 1000, tk = tile % 1000;
     dim3 g2((int)((Cout + tc - 1) / tc), (int)((Kp + tk - 1) / tk), (int)(splits * nsets));
     switch (tile) {

@@ -466,12 +466,12 @@ def _bn_bwd(dout, dpre, y, res, stats, gamma, beta, M, C, act, need_res, direct_
 _WG_PLANS: dict = {}
 
 
-def _wgrad_splits(M, Cout, Cin, KH, KW, Kp):
-    key = (M, Cout, Cin, KH, KW, Kp)
+def _wgrad_splits(M, Cout, Cin, KH, KW, Kp, H, W, stride, pad):
+    key = (M, Cout, Cin, KH, KW, Kp, H, W, stride, pad)
     v = _WG_PLANS.get(key)
     if v is None:
         s = ctypes.c_int64(0)
-        _ext.call("mda_wgrad_plan", M, Cout, Cin, KH, KW, Kp, s)
+        _ext.call("mda_wgrad_plan", M, Cout, Cin, KH, KW, Kp, H, W, stride, pad, s)
         v = _WG_PLANS[key] = s.value
     return v
 
@@ -1063,7 +1063,7 @@ class _ConvBNActTrain(torch.autograd.Function):
         dw = None
         if ctx.needs_input_grad[1]:
             Kw = ctx.kp_w
-            sp = _wgrad_splits(M, Cout, Cin, KH, KW, Kw)
+            sp = _wgrad_splits(M, Cout, Cin, KH, KW, Kw, H, W, stride, pad)
             direct_w = weight.grad is not None and weight.grad.is_contiguous()
             target = weight.grad if direct_w else torch.empty_like(weight, memory_format=torch.contiguous_format)
 
@@ -1160,7 +1160,7 @@ def _conv_bn_backward_dual(ctx, dout, dpre):
         if weight.grad is None or not weight.grad.is_contiguous():
             raise RuntimeError("DOT single-pass backward: conv weights need bound flat gradients")
         Kw = ctx.kp_w
-        sp = _wgrad_splits(M, Cout, Cin, KH, KW, Kw)
+        sp = _wgrad_splits(M, Cout, Cin, KH, KW, Kw, H, W, stride, pad)
         target = weight.grad
 
         def wg():  # both sets in one launch (x read by both)
@@ -1365,7 +1365,7 @@ def conv_wgrad(x, dy, weight_shape, stride, pad):
     Ho, Wo = dy.shape[2], dy.shape[3]
     Kp = (KH * KW * Cin + 63) // 64 * 64
     M = N * Ho * Wo
-    sp = _wgrad_splits(M, Cout, Cin, KH, KW, Kp)
+    sp = _wgrad_splits(M, Cout, Cin, KH, KW, Kp, H, W, stride, pad)
     part = torch.empty(sp * Cout * Kp, dtype=torch.float32, device=x.device)
     out = torch.empty(weight_shape, dtype=torch.float32, device=x.device)
     _ext.call("mda_conv_wgrad", x, dy, part, out, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
@@ -1488,7 +1488,7 @@ class _ConvTrain(torch.autograd.Function):
                       stride, pad, KpT, tile, splits)
         dw = None
         if ctx.needs_input_grad[1]:
-            sp = _wgrad_splits(M, Cout, Cin, KH, KW, Kp)
+            sp = _wgrad_splits(M, Cout, Cin, KH, KW, Kp, H, W, stride, pad)
             direct_w = weight.grad is not None and weight.grad.is_contiguous()
             target = weight.grad if direct_w else torch.empty_like(weight, memory_format=torch.contiguous_format)
 

@@ -58,7 +58,7 @@ def main():
         tile, splits = conv_plan(N * H * H, Cin, KpT)
         part = torch.empty(splits * N * H * H * Cin, dtype=torch.float32, device=dev) if splits > 1 else None
         M = N * Ho * Ho
-        sp = hip_train._wgrad_splits(M, Cout, Cin, k, k, Kp)
+        sp = hip_train._wgrad_splits(M, Cout, Cin, k, k, Kp, H, H, s, p)
         wpart = torch.empty(sp * Cout * Kp, dtype=torch.float32, device=dev)
         grad = torch.zeros(Cout, Cin, k, k, device=dev)
 

@@ -22,6 +22,7 @@ SHAPES = [
     (16, 128, 16, 256, 3, 2, 1, True),
     (16, 64, 32, 128, 1, 2, 0, True),   # 1x1 shortcut
     (16, 256, 8, 256, 3, 1, 1, True),
+    (16, 128, 16, 128, 3, 1, 1, True),  # halo weight gradient, 16-wide rows
     (8, 16, 32, 16, 3, 1, 1, True),     # vec8 loaders (resnet20 widths)
     (4, 24, 15, 40, 3, 2, 1, True),
 ]

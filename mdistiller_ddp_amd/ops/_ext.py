@@ -75,6 +75,8 @@ SIGNATURES = {
     "mda_shuffle_tail_bwd": "ppppp" + "i" * 7 + "s",
     "mda_pack_conv_weights_pad": "pp" + "i" * 6 + "s",
     "mda_wgrad_plan": "iiiiiiiiiip",
+    "mda_conv_fwd_bnacc_pair": "piiiiiiipppiiiipppiis",
+    "mda_conv_dgrad_bnsum2": "pppiiiiiiiiiiiipppippppiis",
     "mda_pack_conv_weights": "ppp" + "i" * 6 + "s",
     "mda_pack_conv_weights_multi": "piiis",
     "mda_pack_tiles": "iiiip",
@@ -211,8 +213,12 @@ def _arg(a, code):
     return float(a)
 
 
-def call(name: str, *args, stream=None):
-    """Invoke a HIP launcher; ``stream`` defaults to the current torch stream."""
+NOT_SERVED = -1  # csrc/common.h MDA_NOT_SERVED: an optional fused launcher did not launch
+
+
+def call(name: str, *args, stream=None, ok=(0,)):
+    """Invoke a HIP launcher; ``stream`` defaults to the current torch stream.
+    Returns the launcher's status; any status outside ``ok`` raises."""
     lib = load(required=True)
     fn = getattr(lib, name)
     codes = SIGNATURES[name]
@@ -226,8 +232,9 @@ def call(name: str, *args, stream=None):
             stream = torch.cuda.current_stream().cuda_stream
         conv.append(stream)
     err = fn(*conv)
-    if err != 0:
+    if err not in ok:
         raise RuntimeError(f"{name} failed with hipError {err}")
+    return err
 
 
 def host_call(name: str, *args):

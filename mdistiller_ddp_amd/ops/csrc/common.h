@@ -6,6 +6,9 @@
 #include <stdint.h>
 
 #define MDA_API extern "C" __attribute__((visibility("default")))
+// status of an optional fused launcher that did not launch (shape / mode not
+// served): the caller takes the unfused path.  Distinct from every hipError_t.
+#define MDA_NOT_SERVED (-1)
 
 typedef uint16_t bf16_t;
 

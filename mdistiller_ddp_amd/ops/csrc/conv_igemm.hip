@@ -118,6 +118,15 @@ struct ConvParams {
   // math of the strided dgrad was ~1.6 us of VALU per K-step -- the whole
   // kernel time (scripts/dgrad_stamps.py)
   uint32_t dv_Cin[2], dv_KW[2], dv_cb[2], dv_HoWo[2], dv_Wo[2], dv_s[2];
+  // strided dgrad (PAR) with a second, 1 x 1 / stride-par / pad-0 conv on the
+  // same input folded in (a residual block's projection shortcut): parity
+  // class cls2 -- the dx pixels that conv samples -- runs cin2 / 64 more
+  // K-steps with A = x2 [N, H, W, cin2] at the class's dy pixel minus sh2
+  // rows / columns and B = w2 [Cout][kp2] (that conv's dgrad operand), so dx
+  // is the SUM of both input gradients in one launch
+  const bf16_t* x2;
+  const bf16_t* w2;
+  int cin2, kp2, cls2, sh2;
 };
 
 // n / d for 0 <= n < 2^31 with the host-made (mul, shr) of d
@@ -157,7 +166,7 @@ struct ParClass {
   int kh0, kw0, nkh, nkw;      // first tap and tap counts (step par)
 };
 
-__device__ __forceinline__ ParClass par_class(const ConvParams& p, int cls) {
+__host__ __device__ __forceinline__ ParClass par_class(const ConvParams& p, int cls) {
   // GEMM view of dgrad: p.H/p.W = dy extent, p.Ho/p.Wo = dx extent, p.stride = s
   ParClass c;
   const int s = p.par;
@@ -859,9 +868,53 @@ struct GldsOcc {
   static constexpr int W = RING == 1 ? (BM * BN >= 16384 ? 2 : 4) : ((BM * BN >= 16384) ? 1 : 2);
 };
 
+// XCD-aware tile order: blocks b, b + 8, ... share an XCD (and its L2); each
+// XCD gets a contiguous run of tiles in (m, n) order, so the N tiles of one
+// block of rows -- which read the same A rows -- run on one L2 (bijective
+// for any tile count; cdna_hip_programming.md T1)
+__device__ __forceinline__ void glds_tile(bool xcd, int& mt, int& nt) {
+  mt = blockIdx.x;
+  nt = blockIdx.y;
+  if (xcd) {
+    const int nwg = gridDim.x * gridDim.y;
+    const int bid = blockIdx.x + gridDim.x * blockIdx.y;
+    const int x = bid & 7, q = nwg >> 3, r = nwg & 7;
+    const int wg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+    mt = wg / gridDim.y;
+    nt = wg - mt * gridDim.y;
+  }
+}
+
+template <int BM, int BN, int MODE, int RING>
+__device__ __forceinline__ void glds_body(const ConvParams& p, char* smem, int mt, int nt);
+
 template <int BM, int BN, int MODE, int RING = GLDS_NBUF>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GldsOcc<BM, BN, RING>::W)))
 conv_glds_kernel(const ConvParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[GldsSmem<BM, BN, RING>::BYTES];
+  int mt, nt;
+  glds_tile(p.xcd != 0, mt, nt);
+  glds_body<BM, BN, MODE, RING>(p, smem, mt, nt);
+}
+
+// Two GEMMs that share the output pixels in ONE launch: N tiles [0, ny1) run
+// conv p, the rest conv q (a block's tile is block-uniform, so each block is
+// entirely one conv).  The residual block's projection shortcut (1x1, stride
+// s) beside its conv1 (3x3, stride s, pad 1): both read the block input at
+// the same output pixels, so the XCD order puts a row tile's conv1 and
+// shortcut blocks on one L2, and the shortcut costs no launch of its own.
+template <int BM, int BN, int MODE, int RING = GLDS_NBUF>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GldsOcc<BM, BN, RING>::W)))
+conv_glds_pair_kernel(const ConvParams p, const ConvParams q, int ny1) {
+  __shared__ __attribute__((aligned(16))) char smem[GldsSmem<BM, BN, RING>::BYTES];
+  int mt, nt;
+  glds_tile(p.xcd != 0, mt, nt);
+  if (nt < ny1) glds_body<BM, BN, MODE, RING>(p, smem, mt, nt);
+  else glds_body<BM, BN, MODE, RING>(q, smem, mt, nt - ny1);
+}
+
+template <int BM, int BN, int MODE, int RING>
+__device__ __forceinline__ void glds_body(const ConvParams& p, char* smem, int mt, int nt) {
   constexpr int MI = BM / 32, NI = BN / 32;
   constexpr int AROWS = BM / 32;
   constexpr int BLOADS = (BN * 8 + 255) / 256;
@@ -872,7 +925,6 @@ conv_glds_kernel(const ConvParams p) {
   static_assert(MODE != LOAD_SCALAR, "SCALAR gathers use conv_fwd_kernel");
   static_assert(RING == 1 || RING == GLDS_NBUF, "ring depth");
 
-  __shared__ __attribute__((aligned(16))) char smem[GldsSmem<BM, BN, RING>::BYTES];
   typedef __attribute__((address_space(3))) char lds_char;
   const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_char*)smem;
 
@@ -880,19 +932,6 @@ conv_glds_kernel(const ConvParams p) {
   const int lane = tid & 63;
   const int wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  // XCD-aware tile order: blocks b, b + 8, ... share an XCD (and its L2); each
-  // XCD gets a contiguous run of tiles in (m, n) order, so the N tiles of one
-  // block of rows -- which read the same A rows -- run on one L2 (bijective
-  // for any tile count; cdna_hip_programming.md T1)
-  int mt = blockIdx.x, nt = blockIdx.y;
-  if (p.xcd) {
-    const int nwg = gridDim.x * gridDim.y;
-    const int bid = blockIdx.x + gridDim.x * blockIdx.y;
-    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-    const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-    mt = wg / gridDim.y;
-    nt = wg - mt * gridDim.y;
-  }
   const int m0 = mt * BM;
   const int n0 = group_n0(p, nt, BN);
   const int nlim = group_nlim(p, n0);
@@ -918,7 +957,7 @@ conv_glds_kernel(const ConvParams p) {
   // for a strided-dgrad class, the dy row / column of the class's first tap
   // (dy pixel of class tap (th, tw) = (a_ih0 - th, a_iw0 - tw): no division
   // per stage)
-  int a_img[AROWS], a_ih0[AROWS], a_iw0[AROWS];
+  int a_img[AROWS], a_ih0[AROWS], a_iw0[AROWS], a_img2[AROWS];
 #pragma unroll
   for (int j = 0; j < AROWS; ++j) {
     const int m = m0 + trow + 32 * j;
@@ -929,6 +968,7 @@ conv_glds_kernel(const ConvParams p) {
     const int oh = hdiv(r, p.dv_Wo);
     const int ow = r - oh * p.Wo;
     a_img[j] = n * p.H * p.W * p.ldx + xoff;
+    a_img2[j] = n * p.H * p.W * p.cin2;
     if (PAR) {
       // (oh + pad - kh0) is a non-negative multiple of the stride for every
       // pixel of the class (par_class), up to the tail rows masked below
@@ -953,7 +993,16 @@ conv_glds_kernel(const ConvParams p) {
   }
 
   const int cin_blocks = p.Cin / BK;
-  const int total_steps = PAR ? pcv.nkh * pcv.nkw * cin_blocks : p.Kp / BK;
+  // the folded 1 x 1 conv's steps come after this class's own taps
+  const int own_steps = PAR ? pcv.nkh * pcv.nkw * cin_blocks : p.Kp / BK;
+  const bool X2 = PAR && p.x2 != nullptr && (int)blockIdx.z / p.zsplits == p.cls2;
+  const int total_steps = own_steps + (X2 ? p.cin2 / BK : 0);
+  const bf16_t* b_row2[BLOADS];
+#pragma unroll
+  for (int j = 0; j < BLOADS; ++j) {
+    const int co = n0 + trow + 32 * j;
+    b_row2[j] = X2 ? p.w2 + (int64_t)(b_ok[j] ? co : 0) * p.kp2 + chunk * 8 : zero;
+  }
   const int zs = PAR ? (int)blockIdx.z % p.zsplits : (int)blockIdx.z;
   const int s_begin = zs * p.steps_per_split;
   const int s_end = min(total_steps, s_begin + p.steps_per_split);
@@ -968,6 +1017,24 @@ conv_glds_kernel(const ConvParams p) {
       if (s >= s_end) s -= nst;
     } else {
       s = s_begin;
+    }
+    if (X2 && s >= own_steps) {  // the folded 1 x 1 conv: its dy pixel, its weights
+      const int c2 = (s - own_steps) * BK + chunk * 8;
+      const uint32_t abase2 = lds0 + (uint32_t)(buf * STAGE) + wave_off;
+#pragma unroll
+      for (int j = 0; j < AROWS; ++j) {
+        const int ih = a_ih0[j] - p.sh2, iw = a_iw0[j] - p.sh2;
+        const bool ok = live && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+        const bf16_t* src = ok ? p.x2 + (a_img2[j] + (ih * p.W + iw) * p.cin2 + c2) : zero;
+        glds16(src, abase2 + (uint32_t)(j * 32 * 128));
+      }
+      const uint32_t bbase2 = abase2 + (uint32_t)(BM * 128);
+#pragma unroll
+      for (int j = 0; j < BLOADS; ++j) {
+        const bf16_t* src = (live && b_ok[j]) ? b_row2[j] + (s - own_steps) * BK : zero;
+        glds16(src, bbase2 + (uint32_t)(j * 32 * 128));
+      }
+      return;
     }
     int tap, c0;
     bool kok = live;
@@ -1905,6 +1972,18 @@ extern "C" int mda_conv1x1_stream_try(const void* x, const void* w, const float*
 
 namespace {
 
+// loader constants of the glds kernel (XCD order, K rotation, multiply-shift divisors)
+void glds_prep(ConvParams& p) {
+  p.xcd = use_xcd_remap() ? 1 : 0;
+  p.krot = use_krot() ? 1 : 0;
+  make_hdiv((uint32_t)std::max(p.Cin, 1), p.dv_Cin);
+  make_hdiv((uint32_t)std::max(p.KW, 1), p.dv_KW);
+  make_hdiv((uint32_t)std::max(p.Cin / BK, 1), p.dv_cb);
+  make_hdiv((uint32_t)std::max(p.Ho * p.Wo, 1), p.dv_HoWo);
+  make_hdiv((uint32_t)std::max(p.Wo, 1), p.dv_Wo);
+  make_hdiv((uint32_t)std::max(p.stride, 1), p.dv_s);
+}
+
 int dispatch(ConvParams& p, int mode, int64_t tile, int64_t splits, hipStream_t st, int halo = 0) {
   if (p.Kp % BK || p.Kp < p.K) return (int)hipErrorInvalidValue;
   if (p.ldx <= 0) p.ldx = p.Cin;
@@ -1923,14 +2002,7 @@ int dispatch(ConvParams& p, int mode, int64_t tile, int64_t splits, hipStream_t 
                                           p.Cout, fwd ? p.stride : 1, p.act, st);
     if (rc != -1) return rc;
   }
-  p.xcd = use_xcd_remap() ? 1 : 0;
-  p.krot = use_krot() ? 1 : 0;
-  make_hdiv((uint32_t)std::max(p.Cin, 1), p.dv_Cin);
-  make_hdiv((uint32_t)std::max(p.KW, 1), p.dv_KW);
-  make_hdiv((uint32_t)std::max(p.Cin / BK, 1), p.dv_cb);
-  make_hdiv((uint32_t)std::max(p.Ho * p.Wo, 1), p.dv_HoWo);
-  make_hdiv((uint32_t)std::max(p.Wo, 1), p.dv_Wo);
-  make_hdiv((uint32_t)std::max(p.stride, 1), p.dv_s);
+  glds_prep(p);
   if (p.cout_g < p.Cout) {  // grouped: group-aligned tiles on the glds kernel only
     if (p.Cout % p.cout_g || p.ldx != p.Cin * (p.Cout / p.cout_g) || p.cout_g % 8 || p.Cin % 8)
       return (int)hipErrorInvalidValue;
@@ -1945,6 +2017,9 @@ int dispatch(ConvParams& p, int mode, int64_t tile, int64_t splits, hipStream_t 
   if (tile == 0 || splits == 0) mda_conv_plan(p.M, p.Cout, p.Kp, &tile, &splits);
   if (splits > 1 && p.partial == nullptr) return (int)hipErrorInvalidValue;
   int rc;
+  if (p.x2 != nullptr && (halo || p.par <= 1 || splits != 1 || p.cin2 % BK || p.cls2 < 0 ||
+                          p.cls2 >= p.par * p.par))
+    return MDA_NOT_SERVED;  // a folded 1 x 1 conv needs the strided (parity) glds path
   if (halo) {
     const int nchunks = p.Cin / BK;
     // the multi-chunk kernel double-buffers patches of at most HALO_PROWS rows
@@ -2010,7 +2085,11 @@ int dispatch(ConvParams& p, int mode, int64_t tile, int64_t splits, hipStream_t 
   } else if (p.par > 1) {
     // strided dgrad by parity class (glds kernel, Cout % 64 == 0 only)
     const int s2 = p.par * p.par;
-    const int steps = ((p.KH + p.par - 1) / p.par) * ((p.KW + p.par - 1) / p.par) * (p.Cin / BK);
+    int steps = ((p.KH + p.par - 1) / p.par) * ((p.KW + p.par - 1) / p.par) * (p.Cin / BK);
+    if (p.x2 != nullptr) {  // the folded 1 x 1 conv's class: its own taps + cin2 / 64
+      const ParClass c = par_class(p, p.cls2);
+      steps = std::max(steps, c.nkh * c.nkw * (p.Cin / BK) + p.cin2 / BK);
+    }
     p.zsplits = (int)splits;
     p.steps_per_split = (int)((steps + splits - 1) / splits);
     const int bm = (int)(tile / 1000), bn = (int)(tile % 1000);
@@ -2138,6 +2217,15 @@ MDA_API int mda_conv_dgrad_bnsum(const void* dy, const void* wt, void* dx, float
 // Grouped dgrad (groups > 1): dx[.., g*Cin/G + ci] sums only group g's output
 // channels; wt packed [Cin][KpT] with k = tap * (Cout/G) + co_in_group
 // (mda_pack_conv_weights_gc).  The GEMM runs with group-aligned tiles.
+static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, float* partial,
+                           const void* res, int64_t N, int64_t H, int64_t W, int64_t Cin,
+                           int64_t Ho, int64_t Wo, int64_t Cout, int64_t KH, int64_t KW,
+                           int64_t stride, int64_t pad, int64_t Kp, int64_t tile, int64_t splits,
+                           const void* bn_y, const void* bn_res, const float* bn_stats,
+                           int64_t bn_act, void* region, int64_t groups, const float* bn_vres,
+                           int64_t bn_mh, int64_t bn_rstride, const void* x2, const void* w2,
+                           int64_t cin2, int64_t kp2, hipStream_t st);
+
 MDA_API int mda_conv_dgrad_bnsum_g(const void* dy, const void* wt, void* dx, float* partial,
                                    const void* res, int64_t N, int64_t H, int64_t W, int64_t Cin,
                                    int64_t Ho, int64_t Wo, int64_t Cout, int64_t KH, int64_t KW,
@@ -2146,6 +2234,43 @@ MDA_API int mda_conv_dgrad_bnsum_g(const void* dy, const void* wt, void* dx, flo
                                    const float* bn_stats, int64_t bn_act, void* region,
                                    int64_t groups, const float* bn_vres, int64_t bn_mh,
                                    int64_t bn_rstride, hipStream_t st) {
+  return conv_dgrad_impl(dy, wt, dx, partial, res, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride,
+                         pad, Kp, tile, splits, bn_y, bn_res, bn_stats, bn_act, region, groups,
+                         bn_vres, bn_mh, bn_rstride, nullptr, nullptr, 0, 0, st);
+}
+
+// mda_conv_dgrad_bnsum_g of a stride-s conv with a 1 x 1 / stride-s / pad-0
+// conv on the same input folded in (ConvParams::x2): dx = dgrad(dy; wt) +
+// dgrad(dy2; wt2), dy2 [N, Ho, Wo, cin2] (the folded conv's output gradient,
+// same extent as dy), wt2 its dgrad operand [Cin][kp2].  A residual block's
+// conv1 and projection shortcut share their input: one launch for both input
+// gradients, no parked gradient, no residual add.  Returns MDA_NOT_SERVED
+// (nothing launched) when the shapes do not take the parity (strided glds) path.
+MDA_API int mda_conv_dgrad_bnsum2(const void* dy, const void* wt, void* dx, int64_t N, int64_t H,
+                                  int64_t W, int64_t Cin, int64_t Ho, int64_t Wo, int64_t Cout,
+                                  int64_t KH, int64_t KW, int64_t stride, int64_t pad, int64_t Kp,
+                                  const void* bn_y, const void* bn_res, const float* bn_stats,
+                                  int64_t bn_act, void* region, const float* bn_vres,
+                                  const void* dy2, const void* wt2, int64_t cin2, int64_t kp2,
+                                  hipStream_t st) {
+  if (dy2 == nullptr || wt2 == nullptr || cin2 <= 0 || cin2 % BK || kp2 < cin2 || kp2 % BK)
+    return MDA_NOT_SERVED;
+  int64_t tile = 0, splits = 0;
+  mda_conv_plan(N * H * W, Cin, Kp, &tile, &splits);
+  if (splits != 1) return MDA_NOT_SERVED;
+  return conv_dgrad_impl(dy, wt, dx, nullptr, nullptr, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride,
+                         pad, Kp, tile, splits, bn_y, bn_res, bn_stats, bn_act, region, 1, bn_vres,
+                         0, 0, dy2, wt2, cin2, kp2, st);
+}
+
+static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, float* partial,
+                           const void* res, int64_t N, int64_t H, int64_t W, int64_t Cin,
+                           int64_t Ho, int64_t Wo, int64_t Cout, int64_t KH, int64_t KW,
+                           int64_t stride, int64_t pad, int64_t Kp, int64_t tile, int64_t splits,
+                           const void* bn_y, const void* bn_res, const float* bn_stats,
+                           int64_t bn_act, void* region, int64_t groups, const float* bn_vres,
+                           int64_t bn_mh, int64_t bn_rstride, const void* x2, const void* w2,
+                           int64_t cin2, int64_t kp2, hipStream_t st) {
   if (Cout % 8 || groups < 1 || Cin % groups || Cout % groups) return (int)hipErrorInvalidValue;
   if (region != nullptr && (splits != 1 || Cin % 8 || Cin > SLOT_CMAX || bn_y == nullptr ||
                             bn_stats == nullptr))
@@ -2162,6 +2287,12 @@ MDA_API int mda_conv_dgrad_bnsum_g(const void* dy, const void* wt, void* dx, flo
   p.bnb_slot = (BnRegion*)region;
   p.bnb_act = (int)bn_act;
   p.bnb_vres = bn_res != nullptr ? bn_vres : nullptr;
+  p.x2 = (const bf16_t*)x2;
+  p.w2 = (const bf16_t*)w2;
+  p.cin2 = (int)cin2;
+  p.kp2 = (int)kp2;
+  p.cls2 = -1;
+  p.sh2 = 0;
   p.x = (const bf16_t*)dy; p.w = (const bf16_t*)wt; p.scale = nullptr; p.bias = nullptr;
   p.res = (const bf16_t*)res; p.y = (bf16_t*)dx; p.preact = nullptr; p.partial = partial;
   // GEMM view: rows = dx pixels, cols = Cin, k = (tap, co); "input" image = dy
@@ -2179,6 +2310,16 @@ MDA_API int mda_conv_dgrad_bnsum_g(const void* dy, const void* wt, void* dx, flo
   // strided dgrad: one GEMM per output-parity class with only its taps
   if (stride > 1 && mode == LOAD_DGRAD_FAST && use_glds() && use_par_dgrad() && groups == 1)
     p.par = (int)stride;
+  if (x2 != nullptr) {
+    if (p.par <= 1 || groups != 1 || bn_mh != 0) return MDA_NOT_SERVED;
+    // the 1 x 1 / stride-s / pad-0 conv samples dx pixels (s i, s j): parity
+    // class (pad mod s, pad mod s), whose dy pixel minus pad / s is (i, j)
+    const int ph = (int)(pad % stride);
+    p.cls2 = ph * (int)stride + ph;
+    p.sh2 = (int)(pad / stride);
+    if (tile == 0 || splits == 0) mda_conv_plan(p.M, p.Cout, p.Kp, &tile, &splits);
+    if (splits != 1) return MDA_NOT_SERVED;
+  }
   if (groups > 1 && (p.Cin % 8 || p.cout_g % 8)) return (int)hipErrorInvalidValue;
   // stride-1 3x3 pad-1 dgrad is a "same" conv of dy with the mirrored taps
   return dispatch(p, mode, tile, splits, st, (groups == 1 && halo_eligible(p)) ? 2 : 0);
@@ -2300,4 +2441,72 @@ MDA_API int mda_conv_fwd_bnacc_g(const void* x, const void* w, void* y, float* p
   int rc = dispatch(p, mode, tile, splits, st, halo);
   if (rc || splits == 1) return rc;
   return mda_bn_stats_acc(y, p.M, Cout, region, st);
+}
+
+// A residual block's conv1 (KH x KW, stride s, pad) and its projection shortcut
+// (1 x 1, stride s, pad 0) on the same input x, as ONE training launch
+// (conv_glds_pair_kernel): both raw bf16 outputs, each with its BN batch sums
+// in its own region.  Returns MDA_NOT_SERVED (nothing launched) when the pair is not served
+// -- different loader modes, a split-K or halo-kernel conv1, grouped convs --
+// and the caller launches the two convs on their own.
+MDA_API int mda_conv_fwd_bnacc_pair(const void* x, int64_t N, int64_t H, int64_t W, int64_t Cin,
+                                    int64_t Ho, int64_t Wo, int64_t stride, const void* w1,
+                                    void* y1, void* reg1, int64_t Cout1, int64_t K1, int64_t pad1,
+                                    int64_t Kp1, const void* w2, void* y2, void* reg2,
+                                    int64_t Cout2, int64_t Kp2, hipStream_t st) {
+  static const bool on = [] {
+    const char* e = getenv("MDA_CONV_PAIR");
+    return !(e && e[0] == '0');
+  }();
+  if (!on || !use_glds()) return MDA_NOT_SERVED;
+  auto mk = [&](ConvParams& p, const void* w, void* y, void* reg, int64_t Cout, int64_t K,
+                int64_t pad, int64_t Kp) {
+    p = ConvParams{};
+    p.ldx = (int)Cin;
+    p.cout_g = (int)Cout;
+    p.x = (const bf16_t*)x; p.w = (const bf16_t*)w; p.y = (bf16_t*)y;
+    p.N = N; p.H = H; p.W = W; p.Cin = Cin; p.Ho = Ho; p.Wo = Wo; p.Cout = Cout; p.KH = K;
+    p.KW = K; p.stride = stride; p.pad = pad; p.K = K * K * Cin; p.Kp = Kp; p.M = N * Ho * Wo;
+    p.zsplits = 1;
+    p.stats_slot = (BnRegion*)reg;
+    p.stamps = g_stamps;
+    p.x_bytes = (int)(N * H * W * Cin * 2);
+    p.w_bytes = (int)(Cout * Kp * 2);
+    glds_prep(p);
+  };
+  if (Cout1 % 8 || Cout2 % 8 || Cout1 > SLOT_CMAX || Cout2 > SLOT_CMAX || Cin % 8) return MDA_NOT_SERVED;
+  if (N * H * W * Cin * 2 >= ((int64_t)1 << 31) || N * Ho * Wo * std::max(Cout1, Cout2) >= ((int64_t)1 << 31))
+    return MDA_NOT_SERVED;
+  ConvParams p, q;
+  mk(p, w1, y1, reg1, Cout1, K1, pad1, Kp1);
+  mk(q, w2, y2, reg2, Cout2, 1, 0, Kp2);
+  if (p.Kp % BK || q.Kp % BK || p.Kp < p.K || q.Kp < q.K) return MDA_NOT_SERVED;
+  const int mode = (Cin % BK == 0) ? LOAD_FAST : LOAD_VEC8;
+  if (halo_eligible(p)) return MDA_NOT_SERVED;
+  int64_t tile = 0, splits = 0;
+  mda_conv_plan(p.M, p.Cout, p.Kp, &tile, &splits);
+  if (splits != 1 || (p.Kp / BK) <= ring1_max()) return MDA_NOT_SERVED;
+  p.steps_per_split = p.Kp / BK;
+  q.steps_per_split = q.Kp / BK;
+  const int bm = (int)(tile / 1000), bn = (int)(tile % 1000);
+  const int ny1 = (int)((Cout1 + bn - 1) / bn), ny2 = (int)((Cout2 + bn - 1) / bn);
+  dim3 grid((unsigned)((p.M + bm - 1) / bm), (unsigned)(ny1 + ny2), 1);
+#define PAIR_CASE(BM_, BN_)                                                                     \
+  case BM_ * 1000 + BN_:                                                                        \
+    if (mode == LOAD_FAST)                                                                      \
+      hipLaunchKernelGGL((conv_glds_pair_kernel<BM_, BN_, LOAD_FAST>), grid, dim3(256), 0, st, p, q, ny1); \
+    else                                                                                        \
+      hipLaunchKernelGGL((conv_glds_pair_kernel<BM_, BN_, LOAD_VEC8>), grid, dim3(256), 0, st, p, q, ny1); \
+    break;
+  switch (tile) {
+    PAIR_CASE(128, 128)
+    PAIR_CASE(128, 64)
+    PAIR_CASE(128, 32)
+    PAIR_CASE(64, 128)
+    PAIR_CASE(64, 64)
+    PAIR_CASE(64, 32)
+    default: return MDA_NOT_SERVED;
+  }
+#undef PAIR_CASE
+  return (int)hipGetLastError();
 }

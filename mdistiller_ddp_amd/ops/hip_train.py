@@ -750,7 +750,8 @@ class GradFork:
         return self.members == 2
 
     def park(self, g) -> bool:
-        """First arrival: keep ``g`` and return True (caller returns None)."""
+        """First arrival: keep ``g`` (a gradient, or a :class:`_DeferredDgrad`)
+        and return True (caller returns None)."""
         if not self.armed or self.pending is not None:
             return False
         self.pending = g
@@ -759,15 +760,55 @@ class GradFork:
         return True
 
     def take(self):
-        """Second arrival: the parked gradient (ordered on the current stream), or None."""
+        """Second arrival: the parked gradient (ordered on the current stream) --
+        a tensor, or a :class:`_DeferredDgrad` -- or None."""
         if not self.armed or self.pending is None:
             return None
         g, self.pending = self.pending, None
         cur = torch.cuda.current_stream(g.device)
         cur.wait_event(self.event)
-        g.record_stream(cur)
+        for t in (g.tensors() if isinstance(g, _DeferredDgrad) else (g,)):
+            t.record_stream(cur)
         self.event = None
         return g
+
+
+class _DeferredDgrad:
+    """A 1 x 1 / stride-s / pad-0 conv's input gradient, not computed: its
+    output gradient ``dy`` and dgrad operand ``wt`` parked on the residual fork
+    for the other consumer's dgrad to fold in (``mda_conv_dgrad_bnsum2``)."""
+
+    __slots__ = ("dy", "wt", "cin2", "kp2", "stride", "device")
+
+    def __init__(self, dy, wt, cin2, kp2, stride):
+        self.dy, self.wt, self.cin2, self.kp2, self.stride = dy, wt, cin2, kp2, stride
+        self.device = dy.device
+
+    def tensors(self):
+        return (self.dy, self.wt)
+
+    def materialize(self, x_shape):
+        """The input gradient itself (the fold was not served)."""
+        from .hip_layers import conv_plan
+        N, Cin, H, W = x_shape
+        dx = torch.empty(x_shape, dtype=torch.bfloat16, device=self.device,
+                         memory_format=torch.channels_last)
+        Ho, Wo = self.dy.shape[2], self.dy.shape[3]
+        tile, splits = conv_plan(N * H * W, Cin, self.kp2)
+        part = (torch.empty(splits * N * H * W * Cin, dtype=torch.float32, device=self.device)
+                if splits > 1 else None)
+        _ext.call("mda_conv_dgrad", self.dy, self.wt, dx, part, N, H, W, Cin, Ho, Wo, self.cin2,
+                  1, 1, self.stride, 0, self.kp2, tile, splits)
+        return dx
+
+
+_MERGE_ON = [os.environ.get("MDA_DGRAD_MERGE", "1") != "0"]
+_MERGE_COUNT = [0]  # folded dgrads launched (tests)
+
+
+def set_dgrad_merge(on: bool) -> None:
+    """A projection shortcut's input gradient folded into conv1's dgrad on / off (A/B)."""
+    _MERGE_ON[0] = bool(on)
 
 
 def _fork_sum(fork, g):
@@ -853,6 +894,48 @@ def can_defer_to_depthwise(x, dwconv, dwbn) -> bool:
             and dwbn is not None and dwbn.training and train_supported(x, dwconv, dwbn))
 
 
+# A residual block's conv1 and its projection shortcut read the same input at
+# the same output pixels: with both on the native kernels, conv1's forward
+# launches the two convs as ONE kernel (mda_conv_fwd_bnacc_pair) and the
+# shortcut's forward picks up its raw output and BN-sum region instead of
+# launching.  The block arms the pair right before conv1 (arm_conv_pair).
+# Opt-in: measured +6 us/step on the flagship (1x MI355X, 3 interleaved fresh
+# processes each, scripts/ab_env.sh: 0.8529 vs 0.8468 ms) -- the shortcut's
+# blocks share conv1's CUs and slow its critical blocks more than the saved
+# launch is worth.
+_PAIR_ON = [os.environ.get("MDA_CONV_PAIR", "0") == "1"]
+_PAIR = [None]    # (x, conv1 weight, shortcut conv) armed by the block
+_PAIR_DONE = {}   # id(shortcut weight) -> (x, raw output, region) made by conv1's launch
+_PAIR_COUNT = [0]  # paired launches issued (tests)
+
+
+def set_conv_pair(on: bool) -> None:
+    """conv1 + projection shortcut forward in one launch on / off (A/B)."""
+    _PAIR_ON[0] = bool(on)
+
+
+def arm_conv_pair(x, conv1, bn1, conv_sc, bn_sc) -> bool:
+    """Arm the paired forward of ``conv1`` (+ ``bn1``) and the 1x1 projection
+    shortcut ``conv_sc`` (+ ``bn_sc``) on input ``x``; True when armed (the
+    caller then runs the shortcut inline, right after conv1)."""
+    _PAIR[0] = None
+    packs = _ACTIVE[0]
+    if not (_PAIR_ON[0] and _BN_FUSED[0] and packs is not None and packs.armed and _DUAL[0] is None):
+        return False
+    if not (isinstance(conv_sc, nn.Conv2d) and conv_sc.kernel_size == (1, 1)
+            and conv_sc.stride == conv1.stride and tuple(conv_sc.padding) == (0, 0)
+            and conv1.groups == 1 and conv_sc.groups == 1 and conv1.bias is None
+            and conv_sc.bias is None and conv1.in_channels == conv_sc.in_channels):
+        return False
+    if not (train_supported(x, conv1, bn1) and train_supported(x, conv_sc, bn_sc)):
+        return False
+    need_dx = x.requires_grad
+    if packs.lookup(conv1.weight, need_dx) is None or packs.lookup(conv_sc.weight, need_dx) is None:
+        return False
+    _PAIR[0] = (x, conv1.weight, conv_sc)
+    return True
+
+
 class _ConvBNActTrain(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, gamma, beta, residual, meta, bn, want_preact, forks=(None, None),
@@ -883,6 +966,7 @@ class _ConvBNActTrain(torch.autograd.Function):
         gc = G > 1 and cin_w % 8 == 0 and (weight.shape[0] // G) % 8 == 0 and _GROUPED_COMPACT[0]
         link_in = getattr(x, "_mda_bnlink", None) if (need_dx and (G == 1 or gc) and _BNB_ON[0]) else None
         chpad = G == 1 and (not need_dx) and needs_channel_pad(cin_w)
+        x_in = x
         x = pad_channels8(x) if chpad else _cl_bf16(x)
         N, Cin, H, W = x.shape
         Cout, _, KH, KW = weight.shape
@@ -953,9 +1037,33 @@ class _ConvBNActTrain(torch.autograd.Function):
         if _BN_FUSED[0] or gc:
             # conv whose epilogue adds the BN sums into the stream's slot, then
             # apply with the finalize in its prologue (2 launches)
-            reg = _region(Cout, dev)
-            _ext.call("mda_conv_fwd_bnacc_g", x, wf, y, part, reg, N, H, W, Cin, Ho, Wo, Cout,
-                      KH, KW, stride, pad, Kp, tile, splits, G if gc else 1)
+            done = _PAIR_DONE.pop(id(weight), None)
+            pr, _PAIR[0] = _PAIR[0], None
+            if done is not None and done[0] is x_in and G == 1:
+                # this is a paired shortcut: conv1's launch produced y and its sums
+                y, reg = done[1], done[2]
+                out = y if defer else torch.empty_like(y)
+            else:
+                reg = _region(Cout, dev)
+                rc = _ext.NOT_SERVED
+                if (pr is not None and pr[0] is x_in and pr[1] is weight and ent is not None
+                        and G == 1 and not chpad and splits == 1 and residual is None):
+                    sc = pr[2]
+                    e2 = packs.lookup(sc.weight, need_dx)
+                    if e2 is not None:
+                        Cout2, Kp2 = sc.out_channels, e2["meta"][4]
+                        y2 = torch.empty((N, Cout2, Ho, Wo), dtype=torch.bfloat16, device=dev,
+                                         memory_format=torch.channels_last)
+                        reg2 = _region(Cout2, dev)
+                        rc = _ext.call("mda_conv_fwd_bnacc_pair", x, N, H, W, Cin, Ho, Wo, stride,
+                                       wf, y, reg, Cout, KH, pad, Kp, e2["wf"], y2, reg2, Cout2, Kp2,
+                                       ok=(0, _ext.NOT_SERVED))
+                        if rc == 0:
+                            _PAIR_DONE[id(sc.weight)] = (x_in, y2, reg2)
+                            _PAIR_COUNT[0] += 1
+                if rc != 0:
+                    _ext.call("mda_conv_fwd_bnacc_g", x, wf, y, part, reg, N, H, W, Cin, Ho, Wo,
+                              Cout, KH, KW, stride, pad, Kp, tile, splits, G if gc else 1)
             if defer:
                 # no apply: the consumer's apply finalizes this BN (VirtualBN)
                 ctx.vbn = VirtualBN(reg, gamma.detach(), beta.detach(), bn, stats, act)
@@ -1038,7 +1146,33 @@ class _ConvBNActTrain(torch.autograd.Function):
             other = x_fork.take() if x_fork is not None else None
             parks = other is None and x_fork is not None and x_fork.armed
             link = ctx.link_in
-            if ctx.gc:
+            folded = False
+            if (parks and _MERGE_ON[0] and KH == 1 and KW == 1 and pad == 0 and stride > 1
+                    and Cout % 64 == 0 and KpT == Cout and not ctx.gc and ctx.groups == 1
+                    and x_fork.park(_DeferredDgrad(dy, wt, Cout, KpT, stride))):
+                # projection shortcut: its input gradient is folded into the
+                # other consumer's (conv1's) dgrad launch
+                dx = None
+                parks = False
+            elif isinstance(other, _DeferredDgrad):
+                reg = _region(Cin, dev) if link is not None else None
+                rc = _ext.call("mda_conv_dgrad_bnsum2", dy, wt, dx, N, H, W, Cin, Ho, Wo, Cout, KH,
+                               KW, stride, pad, KpT, link.y if reg is not None else None,
+                               link.res if reg is not None else None,
+                               link.stats if reg is not None else None,
+                               link.act if reg is not None else 0, reg,
+                               link.vres if reg is not None else None, other.dy, other.wt,
+                               other.cin2, other.kp2, ok=(0, _ext.NOT_SERVED))
+                if rc == 0:
+                    _MERGE_COUNT[0] += 1
+                    if reg is not None:
+                        link.arm(dx, reg)
+                    folded = True
+                else:
+                    other = other.materialize((N, Cin, H, W))
+            if dx is None or folded:
+                pass
+            elif ctx.gc:
                 reg = _region(Cin, dev) if (link is not None and not parks and splits == 1) else None
                 _ext.call("mda_conv_dgrad_bnsum_g", dy, wt, dx, part, other, N, H, W, Cin, Ho, Wo,
                           Cout, KH, KW, stride, pad, KpT, tile, splits,

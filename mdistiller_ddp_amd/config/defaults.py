@@ -106,10 +106,11 @@ CFG.RUNTIME.CHECK_REPLICAS = 0       # >0: every N steps assert param checksums 
 # Distributed (ext) --------------------------------------------------------
 CFG.DIST = CN()
 CFG.DIST.BACKEND = "auto"            # auto -> nccl(RCCL) on GPU, gloo on CPU
-CFG.DIST.BUCKET_MB = 8.0             # gradient bucket size (MB of fp32)
+CFG.DIST.BUCKET_MB = 0.0             # gradient bucket size (MB of fp32); 0 = auto:
+                                     # total / 4 clamped to [0.5, 8] MB (parallel/grad_reducer.py)
 CFG.DIST.TIMEOUT_S = 600
 CFG.DIST.GRAD_DTYPE = "fp32"         # fp32 | bf16 wire format for gradient all-reduce
-CFG.DIST.GRAPH_COMM = "auto"         # events | split | capture | auto (= split):
+CFG.DIST.GRAPH_COMM = "auto"         # events | split | capture | auto (= events):
                                      # per-bucket all-reduce behind events of the captured backward
                                      # (events), eager between the fwd+bwd and update graphs (split),
                                      # or inside one multi-branch graph (capture)

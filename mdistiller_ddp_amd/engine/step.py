@@ -200,11 +200,19 @@ class TrainStep:
         if channels_last:
             _to_channels_last(distiller)
         self.world = get_world_size()
+        # EXPERIMENT.DETERMINISTIC: fixed-order reductions on the native path
+        # (ops/hip_train.py set_deterministic) and PyTorch's deterministic algorithms
+        self.deterministic = bool(cfg.EXPERIMENT.get("DETERMINISTIC", False))
+        if self.device.type == "cuda":
+            from ..ops import hip_train as _ht
+            _ht.set_deterministic(self.deterministic)
+            if self.deterministic:
+                torch.backends.cudnn.deterministic = True
         self.flat = FlatParams(distiller.get_learnable_parameters(), 2 if self.is_dot else 1)
         self.opt = build_optimizer(cfg, self.flat, grad_scale=1.0 / self.world, trainer=trainer)
         self.use_graph = (bool(use_graph) and self.device.type == "cuda"
                           and getattr(distiller, "graph_capturable", True))
-        if self.use_graph:
+        if self.use_graph and not self.deterministic:
             # MIOpen find mode: algorithms are chosen during the eager warm-up
             # steps, so nothing is searched or JIT-built inside a capture
             torch.backends.cudnn.benchmark = True
@@ -269,7 +277,7 @@ class TrainStep:
         its bucket's event, so they overlap the rest of the backward
         (GradReducer.arm_capture).  ``True`` (capture): the all-reduce inside
         the single step graph (a multi-branch graph, slow on ROCm's executor).
-        ``auto`` = split.
+        ``auto`` = events (DOT with its two backward graphs: split).
         """
         if self.world <= 1 or not self.use_graph:
             return False
@@ -280,9 +288,9 @@ class TrainStep:
             if not rccl:
                 raise ValueError("DIST.GRAPH_COMM=capture needs the RCCL (nccl) backend")
             return True
-        if mode == "events":
+        if mode in ("events", "auto"):
             return "events"
-        return False  # split (auto: events only once validated on a multi-GPU node)
+        return False  # split
 
     # ------------------------------------------------------------------
     def set_epoch(self, epoch: float) -> None:
@@ -391,9 +399,18 @@ class TrainStep:
         preds, losses = self._fwd(b)
         armed = self._arm_wgrad_stream()
         deferred = (not armed) and self._arm_wgrad_defer()
-        events = overlap_comm == "events" and not self.is_dot
+        # DOT's single pass writes both gradient sets of a parameter together:
+        # its buckets launch both sets from the same events
+        events = overlap_comm == "events" and (not self.is_dot or self.dot_single)
         try:
             if self.is_dot and self.dot_single:
+                if events:
+                    from ..ops import hip_train
+                    self.reducer.sets = (0, 1)
+                    self.reducer.arm_capture(hip_train.flush_wgrad_reduces if deferred else None)
+                    events = "armed"
+                elif self.world > 1 and not torch.cuda.is_current_stream_capturing():
+                    self.reducer.calibrate()  # counts for a later events capture
                 self._dot_single_backward(losses)
             elif self.is_dot:
                 self.flat.bind_grads(1)
@@ -419,6 +436,8 @@ class TrainStep:
                 self.reducer.abort_capture()
             raise
         finally:
+            if self.is_dot and self.dot_single and events != "armed":
+                self.reducer.end_calibration()
             self._flush_wgrad_defer(deferred)
             self._join_wgrad_stream(armed)
             join_branches()
@@ -522,13 +541,13 @@ class TrainStep:
         ``events`` mode each bucket's all-reduce waits only for its event."""
         if self.world <= 1:
             return
-        if self.is_dot:
-            self.reducer.reduce_sets((0, 1))
-        elif replay and self.graph_comm == "events" and self.reducer.graph_events is not None:
+        if replay and self.graph_comm == "events" and self.reducer.graph_events is not None:
             if os.environ.get("MDA_EVENTS_SYNC") == "1":  # diagnostic: the replay drained first
                 torch.cuda.current_stream().synchronize()
             self.reducer.launch_from_events()
             self.reducer.wait_launched()
+        elif self.is_dot:
+            self.reducer.reduce_sets((0, 1))
         else:
             self.reducer.finish()
         exchange = getattr(self.distiller, "exchange", None)

@@ -13,8 +13,13 @@
 //
 // versus MIOpen's 4 forward + 3 backward BN kernels plus separate add / ReLU
 // (and its backward) launches per layer in the reference stack.
-// Reductions are deterministic: fixed per-block partials in fp32, combined
-// in a fixed order in fp64 by the last-arriving block.
+// Determinism: the partial-row kernels in this first part (stats /
+// bn_bwd_reduce2 + a finalize) combine fixed per-block fp32 partials in a
+// fixed order in fp64, so they are deterministic.  The default fused path
+// below (one-shot BnRegion channel sums, csrc/bnslot.h) adds block partials
+// with fp64 atomics, whose order varies run to run: its results agree to fp64
+// rounding only.  EXPERIMENT.DETERMINISTIC selects the partial-row kernels
+// (ops/hip_train.py set_deterministic).
 #include "common.h"
 
 namespace {

@@ -215,21 +215,27 @@ vid_sums_kernel(const bf16_t* __restrict__ pred, const bf16_t* __restrict__ ft, 
     for (int k = 0; k < 8; ++k) red[r0 * C + cg * 8 + k] = s[k];
   }
   __syncthreads();
+  // this block's partial row (summed in block order by the finalize kernel:
+  // deterministic, no float atomics)
+  double* part = acc + (int64_t)C * (1 + blockIdx.x);
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     float t = 0.f;
     for (int r = 0; r < rpi; ++r) t += red[r * C + c];
-    __hip_atomic_fetch_add(acc + c, (double)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    part[c] = (double)t;
   }
 }
 
 __global__ void __launch_bounds__(256)
-vid_finalize_kernel(const double* __restrict__ acc, const float* __restrict__ ls, int M, int C,
-                    float eps, float* __restrict__ loss) {
+vid_finalize_kernel(double* __restrict__ acc, const float* __restrict__ ls, int M, int C,
+                    float eps, float* __restrict__ loss, int nb) {
   __shared__ double red[256];
   double t = 0.0;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    double sc = 0.0;
+    for (int b = 0; b < nb; ++b) sc += acc[(int64_t)C * (1 + b) + c];
+    acc[c] = sc;  // S_c, read by the backward
     const double v = (double)vid_var(ls[c], eps);
-    t += acc[c] / v + (double)M * log(v);
+    t += sc / v + (double)M * log(v);
   }
   red[threadIdx.x] = t;
   __syncthreads();
@@ -277,17 +283,20 @@ vid_bwd_kernel(const bf16_t* __restrict__ pred, const bf16_t* __restrict__ ft,
 }  // namespace
 
 // acc: [C] fp64, zeroed by the caller; loss: [1] fp32.
+// acc: (1 + VID_MAX_BLOCKS) * C doubles -- S_c, then the per-block partial rows
+constexpr int VID_MAX_BLOCKS = 512;
+
 MDA_API int mda_vid_loss(const void* pred, const void* ft, const float* log_scale, int64_t M,
                          int64_t C, float eps, double* acc, float* loss, hipStream_t st) {
   if (C % 8 || C > 2048 || M <= 0) return (int)hipErrorInvalidValue;
   const int C8 = (int)C / 8, rpi = 256 / C8;
-  int nb = (int)std::min<int64_t>((M + 4 * rpi - 1) / (4 * rpi), 512);
+  int nb = (int)std::min<int64_t>((M + 4 * rpi - 1) / (4 * rpi), VID_MAX_BLOCKS);
   if (nb < 1) nb = 1;
   hipLaunchKernelGGL(vid_sums_kernel, dim3(nb), dim3(256), 0, st, (const bf16_t*)pred,
                      (const bf16_t*)ft, (int)M, (int)C, acc);
   { const int rc = (int)hipGetLastError(); if (rc) return rc; }
-  hipLaunchKernelGGL(vid_finalize_kernel, dim3(1), dim3(256), 0, st, (const double*)acc, log_scale,
-                     (int)M, (int)C, eps, loss);
+  hipLaunchKernelGGL(vid_finalize_kernel, dim3(1), dim3(256), 0, st, acc, log_scale,
+                     (int)M, (int)C, eps, loss, nb);
   MDA_CHECK_LAUNCH();
 }
 

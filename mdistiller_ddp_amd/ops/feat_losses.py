@@ -699,7 +699,8 @@ class _VIDNLL(torch.autograd.Function):
     def forward(ctx, pred, f_t, log_scale, eps):
         N, C, H, W = pred.shape
         M = N * H * W
-        acc = torch.zeros(C, dtype=torch.float64, device=pred.device)
+        # S_c, then one partial row per block of the sums kernel (fixed-order sum)
+        acc = torch.empty((1 + 512) * C, dtype=torch.float64, device=pred.device)
         loss = torch.empty(1, dtype=torch.float32, device=pred.device)
         ls = log_scale.detach().float().contiguous()
         _ext.call("mda_vid_loss", pred, f_t, ls, M, C, float(eps), acc, loss)

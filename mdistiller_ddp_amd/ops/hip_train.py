@@ -639,6 +639,40 @@ def set_grouped_compact(on: bool) -> None:
     _GROUPED_COMPACT[0] = bool(on)
 
 
+_DET = {"on": False, "saved": None}
+
+
+def set_deterministic(on: bool) -> None:
+    """Deterministic mode (``EXPERIMENT.DETERMINISTIC``): every
+    reduction of the native training path in a fixed order, so two runs of
+    the same step are bitwise equal.  The fast path sums BN batch / backward
+    statistics with fp64 atomics into one-shot regions (csrc/bnslot.h: in the
+    conv and depthwise epilogues, the consumer dgrad's BN-sum epilogue, the
+    pool + FC head) whose order varies run to run; here BN runs on per-block
+    partial rows and a fixed-order finalize launch instead (the
+    ``MDA_BN_FUSED=0`` kernels), and the fusions that exist only on the
+    regions (VirtualBN, BnLink sums, the depthwise fusions, the paired
+    forward) are off.  Everything else is fixed-order in both modes (split-K
+    combines, weight-gradient partial reduces, losses, optimizer, VID).
+    Turning it off restores the switches as they were."""
+    on = bool(on)
+    if on == _DET["on"]:
+        return
+    if on:
+        _DET["saved"] = (_BN_FUSED[0], _BNB_ON[0], _VRES_ON[0], _DW_VIN_ON[0], _DW_BNB_ON[0],
+                         _PAIR_ON[0])
+        _BN_FUSED[0] = _BNB_ON[0] = _VRES_ON[0] = _DW_VIN_ON[0] = _DW_BNB_ON[0] = False
+        _PAIR_ON[0] = False
+    else:
+        (_BN_FUSED[0], _BNB_ON[0], _VRES_ON[0], _DW_VIN_ON[0], _DW_BNB_ON[0],
+         _PAIR_ON[0]) = _DET["saved"]
+    _DET["on"] = on
+
+
+def deterministic() -> bool:
+    return _DET["on"]
+
+
 def train_supported(x, conv, bn) -> bool:
     if not (x.is_cuda and x.dim() == 4 and isinstance(conv, nn.Conv2d)):
         return False

@@ -18,17 +18,25 @@ distiller's learnable parameters only:
 * DOT's two gradient sets are reduced (the reference's DDP syncs only the
   first backward), honouring the bf16 wire format too.
 
-Under hipGraph capture with the RCCL backend (``TrainStep`` graph-comm
-mode) the same hooks fire inside the captured backward, so each bucket's
-all-reduce is recorded as a fork onto RCCL's stream that joins back before
-the optimizer node: the graph itself overlaps communication with the rest
-of backward, and a replay has no host round-trip at all.
+Under hipGraphs (``TrainStep``, ``DIST.GRAPH_COMM``): ``events`` (the
+default at world > 1) -- the same hooks fire inside the captured backward and
+record one external event per bucket where its last gradient is written;
+after each replay is launched the host enqueues, on a comm stream, "wait for
+bucket k's event, all-reduce bucket k" in bucket order, so the head-side
+buckets are on the wire while the replay is still computing the stem's
+gradients (:meth:`GradReducer.arm_capture`, :meth:`launch_from_events`).
+DOT's single-pass backward writes both gradient sets of a parameter in one
+launch, so each event launches both sets' slices (``sets``).  ``split``
+all-reduces eagerly between the fwd+bwd and update graphs; ``capture`` puts
+the collectives inside one multi-branch graph.
 
 Bucket size: xGMI is point-to-point (7 links/GPU); RCCL's ring all-reduce of
 an S-byte bucket costs ~latency + 2(N-1)/N * S / link_bw per channel, so a
-few MB per bucket already amortises the ~10-20 us latency while keeping two
-or three buckets in flight behind backward.  ``DIST.BUCKET_MB`` (default 8)
-sets it; the north-star student (4.7 MB fp32) becomes 1-2 buckets.
+few MB per bucket already amortises the ~10-20 us latency.  The overlap
+comes from the buckets that complete early, so ``DIST.BUCKET_MB = 0`` (the
+default) sizes them from the model: a quarter of the gradient, clamped to
+[0.5, 8] MB (:func:`auto_bucket_mb`) -- four buckets for the north-star
+student (4.7 MB fp32), 8 MB buckets for ImageNet students.
 """
 from __future__ import annotations
 
@@ -51,6 +59,18 @@ def notify_grad(*params) -> None:
                 r.ready_param(p)
 
 
+def auto_bucket_mb(numel: int) -> float:
+    """``DIST.BUCKET_MB = 0``: a quarter of the flat fp32 gradient, clamped to
+    [0.5, 8] MB.  The overlap comes from the buckets that complete early in the
+    backward (the head's), so a small model wants several buckets -- the
+    flagship ResNet8x4 student (4.7 MB) gets four of ~1.2 MB, the first
+    launched after the last stage's backward -- while a large one keeps
+    buckets big enough to amortise a collective's launch and latency over
+    point-to-point xGMI (ResNet-18: 8 MB buckets)."""
+    total = numel * 4 / float(1 << 20)
+    return min(8.0, max(0.5, total / 4.0))
+
+
 class GradReducer:
     def __init__(self, flat, bucket_mb: float = 8.0, overlap: bool = True, group=None,
                  wire_dtype: str = "fp32"):
@@ -64,6 +84,12 @@ class GradReducer:
         self.calls = 0
         self.early_launches = 0  # buckets launched from inside backward (overlap)
         self.avoid_streams = []  # streams the comm stream must differ from (TrainStep sets them)
+        # gradient sets each bucket all-reduce covers (DOT's single-pass backward
+        # writes both sets of a parameter in one launch: (0, 1)); None = the bound set
+        self.sets = None
+        if not bucket_mb or bucket_mb <= 0:
+            bucket_mb = auto_bucket_mb(flat.numel)
+        self.bucket_mb = float(bucket_mb)
         bucket_elems = max(64, int(bucket_mb * (1 << 20) / 4))
         # buckets aligned to parameter boundaries, in flat (= backward) order
         order = sorted(range(len(flat.params)), key=lambda i: flat.offsets[i])
@@ -101,6 +127,8 @@ class GradReducer:
         self._armed = False
         self._error = None
         # captured-backward overlap (DIST.GRAPH_COMM=events, see arm_capture)
+        self._arm_stream = None    # the stream the armed backward started on
+        self._from_events = False  # launching behind graph events (no stream joins)
         self._cap = None           # events recorded so far while capturing: [(bucket, event)]
         self._cap_flush = None     # called before a bucket's event is recorded
         self.graph_events = None   # [(bucket, event)] of the captured graph, bucket order
@@ -127,7 +155,7 @@ class GradReducer:
             return
         b = self._param_bucket[i]
         self._pending[b] -= 1
-        if self._pending[b] < 0 and b in self._works and self._error is None:
+        if self._pending[b] < 0 and b < self._next and self._error is None:
             # more contributions than the calibration step counted, after the
             # bucket was already all-reduced: the reduced values are stale.
             # Recorded, not raised here: the peers are about to enter the
@@ -162,18 +190,49 @@ class GradReducer:
             w = self._wires[key] = torch.empty(n, dtype=torch.bfloat16, device=device)
         return w
 
+    def _join_writers(self, stream) -> None:
+        """Make ``stream`` wait for every stream a gradient of the step may be
+        written on: the one the backward started on (``arm``) and the residual
+        branch streams.  A bucket completes in the hook of its LAST gradient,
+        which runs with that gradient's stream current -- a projection
+        shortcut's weight gradient is written on the branch stream, the rest
+        of its bucket on the main one (an all-reduce ordered after the branch
+        alone raced the main stream's writes: replicas diverged ~1 run in 3)."""
+        from ..runtime import streams as S
+        dev = torch.cuda.current_device()
+        capturing = self._cap is not None
+        for o in (self._arm_stream, S._branch_streams.get(dev)):
+            if o is None or o.cuda_stream == stream.cuda_stream:
+                continue
+            if capturing:
+                # inside a capture only a stream that is part of it can be
+                # joined (a branch stream the captured step never forked is idle)
+                with torch.cuda.stream(o):
+                    if not torch.cuda.is_current_stream_capturing():
+                        continue
+            stream.wait_stream(o)
+
     def _launch(self, b, async_op):
-        t = self._slice(b)
+        if self._arm_stream is not None and self._cap is None and not self._from_events:
+            self._join_writers(torch.cuda.current_stream())
+        if self.sets is not None:  # every listed gradient set's slice of the bucket
+            s, e, _ = self.buckets[b]
+            for k in self.sets:
+                self._launch_t((b, k), self.flat.grads[k][s:e], async_op)
+            return
+        self._launch_t(b, self._slice(b), async_op)
+
+    def _launch_t(self, key, t, async_op):
         self.bytes_reduced += t.numel() * (2 if self.wire_bf16 else 4)
         self.calls += 1
         if self.wire_bf16:
-            tb = self._wire_buf(("b", b), t.numel(), t.device)
+            tb = self._wire_buf(("b", key), t.numel(), t.device)
             tb.copy_(t)
             work = dist.all_reduce(tb, group=self.group, async_op=True)
-            self._works[b] = (work, t, tb)
+            self._works[key] = (work, t, tb)
         else:
             work = dist.all_reduce(t, group=self.group, async_op=async_op)
-            self._works[b] = (work, None, None)
+            self._works[key] = (work, None, None)
 
     def arm(self) -> None:
         """Call before a backward whose gradients should be reduced on the fly."""
@@ -184,6 +243,7 @@ class GradReducer:
         self._armed = self.overlap
         if not self._armed:
             return
+        self._arm_stream = torch.cuda.current_stream() if self.flat.grads.is_cuda else None
         if self._expected is None:
             self._calib = [0] * len(self.flat.params)
         else:
@@ -200,8 +260,9 @@ class GradReducer:
             self._error = (f"GradReducer: bucket contribution counts went negative "
                            f"{self._pending} (a parameter got more gradient writes than "
                            f"the calibration step counted)")
+        launched = {k[0] if isinstance(k, tuple) else k for k in self._works}
         for b in range(len(self.buckets)):
-            if b not in self._works:
+            if b not in launched:
                 self._launch(b, async_op=True)
         for b, (work, t, tb) in self._works.items():
             if work is not None:
@@ -243,6 +304,7 @@ class GradReducer:
         # autograd engine runs with ANOTHER current stream (a leaf's
         # AccumulateGrad runs on the stream the leaf was made on, not capturing)
         self._cap_stream = torch.cuda.current_stream()
+        self._arm_stream = self._cap_stream
         self._pending = [sum(self._expected[i] for i in idx) for (_, _, idx) in self.buckets]
         _ARMED.append(self)
 
@@ -254,6 +316,9 @@ class GradReducer:
             with torch.cuda.stream(self._cap_stream):
                 self._cap_flush()
         from ..runtime.streams import HipEvent
+        # the event must also cover gradients written on a residual branch
+        # stream (a join edge in the captured graph; see _join_writers)
+        self._join_writers(self._cap_stream)
         ev = HipEvent()  # (torch.cuda.Event(external=True) is refused on ROCm)
         ev.record(external=True, stream=self._cap_stream)
         self._cap.append((b, ev))
@@ -300,11 +365,15 @@ class GradReducer:
         # (no wait on the current stream: that would wait for the whole replay;
         # each all-reduce waits only for its bucket's event)
         self._works = {}
-        with torch.cuda.stream(self._comm):
-            for b, ev in self.graph_events:
-                ev.wait(self._comm)
-                self._launch(b, async_op=True)
-                self.early_launches += 1
+        self._from_events = True  # each bucket's event already covers its writers
+        try:
+            with torch.cuda.stream(self._comm):
+                for b, ev in self.graph_events:
+                    ev.wait(self._comm)
+                    self._launch(b, async_op=True)
+                    self.early_launches += 1
+        finally:
+            self._from_events = False
 
     def wait_launched(self) -> None:
         cur = torch.cuda.current_stream()
@@ -316,6 +385,26 @@ class GradReducer:
             if tb is not None:
                 t.copy_(tb)
         self._works = {}
+
+    def calibrate(self) -> None:
+        """Count each parameter's gradient contributions in the backward that
+        follows, launching nothing (a trainer that reduces whole gradient sets
+        itself, DOT, still needs the counts for :meth:`arm_capture`); close
+        with :meth:`end_calibration`."""
+        if not self.enabled or self._expected is not None:
+            return
+        self._works = {}
+        self._next = 0
+        self._armed = True
+        self._calib = [0] * len(self.flat.params)
+        _ARMED.append(self)
+
+    def end_calibration(self) -> None:
+        if self._calib is not None:
+            self._expected, self._calib = self._calib, None
+        self._armed = False
+        if self in _ARMED:
+            _ARMED.remove(self)
 
     def reduce_all(self) -> None:
         """Non-overlapped reduction of the currently bound gradient set."""

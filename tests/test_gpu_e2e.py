@@ -301,3 +301,41 @@ def test_teacher_lookahead_matches_inline_teacher(typ, trainer, tgraph):
     assert abs(outs[0][1]["loss"] - outs[1][1]["loss"]) <= max(
         1e-4 * abs(outs[1][1]["loss"]), 3 * abs(outs[2][1]["loss"] - outs[1][1]["loss"]))
     print(f"lookahead {typ}: rel {rel:.3g} spread {spread:.3g}")
+
+
+@pytest.mark.timeout(300)
+def test_deterministic_mode_graph_runs_are_bitwise_equal():
+    """EXPERIMENT.DETERMINISTIC (ops/hip_train.py set_deterministic): two
+    20-step hipGraph runs of the flagship DKD step from the same state and data
+    end bitwise equal (the default mode's fp64-atomic BN sums drift ~2.5e-3
+    over 20 steps, profiles/r4_multirank_determinism.txt)."""
+    import copy
+    from mdistiller_ddp_amd.config import get_cfg
+    from mdistiller_ddp_amd.engine.build import build_distiller
+    from mdistiller_ddp_amd.engine.step import TrainStep
+    from mdistiller_ddp_amd.data.synthetic import SyntheticLoader
+    from mdistiller_ddp_amd.ops import hip_train
+    cfg = get_cfg()
+    cfg.merge_from_file("configs/cifar100/dkd/res32x4_res8x4.yaml")
+    cfg.DISTILLER.RANDOM_TEACHER = True
+    cfg.EXPERIMENT.DETERMINISTIC = True
+    torch.manual_seed(0)
+    d0 = build_distiller(cfg, 100, "cuda")
+    ld = SyntheticLoader("cifar100", 64, "cuda", steps_per_epoch=20, channels_last=True)
+    batches = [{k: v.clone() for k, v in b.items()} for b in ld]
+    out = []
+    try:
+        for _ in range(2):
+            d = copy.deepcopy(d0)
+            d.train()
+            st = TrainStep(d, cfg, "cuda", use_graph=True, dtype=torch.bfloat16)
+            assert hip_train.deterministic()
+            st.set_epoch(1.0)
+            for b in batches:
+                st.step(b)
+            torch.cuda.synchronize()
+            assert st._graphs is not None
+            out.append(st.flat.data.clone())
+    finally:
+        hip_train.set_deterministic(False)
+    assert torch.equal(out[0], out[1]), (out[0] - out[1]).abs().max()

@@ -35,6 +35,8 @@ def _worker(rank, world, port, scenario, outdir):
     comm = "split"
     if scenario.endswith("_events"):
         scenario, comm = scenario[:-len("_events")], "events"
+    elif scenario.endswith("_default"):  # every DIST knob at its default
+        scenario, comm = scenario[:-len("_default")], None
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
                       RANK=str(rank), LOCAL_RANK="0")
     import torch.distributed as dist
@@ -55,12 +57,13 @@ def _worker(rank, world, port, scenario, outdir):
     cfg.DISTILLER.STUDENT = "resnet8x4"
     cfg.DISTILLER.RANDOM_TEACHER = True
     cfg.SOLVER.TRAINER = trainer
-    cfg.DIST.BUCKET_MB = 1.0 if comm == "split" else 0.5  # several buckets in flight
-    if os.environ.get("MDA_TEST_BUCKET_MB"):  # (diagnostics: one bucket size for both modes)
-        cfg.DIST.BUCKET_MB = float(os.environ["MDA_TEST_BUCKET_MB"])
-    cfg.DIST.GRAPH_COMM = comm
-    if scenario == "dot":
-        cfg.DIST.GRAD_DTYPE = "bf16"
+    if comm is not None:
+        cfg.DIST.BUCKET_MB = 1.0 if comm == "split" else 0.5  # several buckets in flight
+        if os.environ.get("MDA_TEST_BUCKET_MB"):  # (diagnostics: one bucket size for both modes)
+            cfg.DIST.BUCKET_MB = float(os.environ["MDA_TEST_BUCKET_MB"])
+        cfg.DIST.GRAPH_COMM = comm
+        if scenario == "dot":
+            cfg.DIST.GRAD_DTYPE = "bf16"
     cfg.CRD.NCE.K = 256
     torch.manual_seed(1000 + rank)  # different init per rank
     d = build_distiller(cfg, 100, dev, num_data=1000)
@@ -100,6 +103,8 @@ def _worker(rank, world, port, scenario, outdir):
     out["flat"] = flat.cpu()
     out["events"] = st.reducer.graph_events is not None and len(st.reducer.graph_events) > 1
     out["early"] = st.reducer.early_launches
+    out["buckets"] = len(st.reducer.buckets)
+    out["graph_comm"] = st.graph_comm
     allf = [torch.empty_like(flat) for _ in range(world)]
     dist.all_gather(allf, flat)
     out["params_equal"] = all(torch.equal(allf[0], a) for a in allf)
@@ -183,3 +188,24 @@ def test_two_ranks_one_gpu_graph_replicas(scenario):
     if scenario == "crd":
         assert all(r["memory_equal"] for r in res), res
         assert all(r["memory_moved"] > 0 and r["memory_finite"] for r in res), res
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("scenario", ["dkd", "dot", "crd"])
+def test_default_dist_path_is_overlapped(scenario):
+    """With every DIST knob at its default, world > 1 under hipGraphs runs the
+    events path (per-bucket all-reduce behind the captured backward's events)
+    for the base, DOT (single pass: both gradient sets per event) and CRD
+    trainers: the automatic bucket size splits the ResNet8x4 student into
+    several buckets, every replay launches them all from their events, and
+    the replicas stay bit-identical."""
+    res = _spawn(scenario + "_default")
+    for r in res:
+        assert r["init_equal"] and r["graph"], r
+        assert r["graph_comm"] == "events", r
+        assert r["buckets"] >= 3, r
+        assert r["events"] and r["early"] >= r["buckets"] - 1, r
+        assert r["params_equal"] and r["finite"], r
+        assert r["moved"] > 1e-4, r
+    if scenario == "crd":
+        assert all(r["memory_equal"] for r in res), res

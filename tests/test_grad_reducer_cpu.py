@@ -84,3 +84,15 @@ def test_reused_parameter_reduced_after_all_contributions_and_overflow_raises():
         assert r["mean_ok"], r
         assert r["early"] >= 1, r
         assert r["raised"], r
+
+
+def test_auto_bucket_size_rule():
+    """DIST.BUCKET_MB = 0: a quarter of the gradient, clamped to [0.5, 8] MB --
+    four buckets for the flagship ResNet8x4 student, 8 MB ones for ResNet-18."""
+    from mdistiller_ddp_amd.parallel.grad_reducer import auto_bucket_mb
+    from mdistiller_ddp_amd.models.cifar import resnet8x4
+    from mdistiller_ddp_amd.models.imagenet.resnet import resnet18
+    n8 = sum(p.numel() for p in resnet8x4(num_classes=100).parameters())
+    assert abs(auto_bucket_mb(n8) - n8 * 4 / (1 << 20) / 4) < 1e-9
+    assert auto_bucket_mb(sum(p.numel() for p in resnet18().parameters())) == 8.0
+    assert auto_bucket_mb(1000) == 0.5

@@ -332,6 +332,9 @@ class TrainStep:
         u = self._units.get(key)
         if u is None:
             u = self._units[key] = torch.ones_like(v)
+            if u.numel() == 1:
+                from ..ops.losses import register_unit_seed
+                register_unit_seed(u)
         return u
 
     # module types whose whole backward runs on the native kernels that carry

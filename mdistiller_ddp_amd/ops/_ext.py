@@ -29,7 +29,7 @@ _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int64, "f": ctypes.c_float, "s": ctyp
 # name -> argument codes (stream last).  Kept in sync with csrc/*.hip `extern "C"` launchers.
 SIGNATURES = {
     # losses (csrc/losses.hip)
-    "mda_logit_loss": "iiippppppppiifffffpfs",
+    "mda_logit_loss": "iiippppppppiifffffpfps",
     "mda_axpby": "ipppppis",
     # feature losses (csrc/feat.hip)
     "mda_at_loss": "iipppppp" + "iiii" + "fs",

@@ -97,6 +97,8 @@ at_loss_kernel(const TS* __restrict__ fs, const TT* __restrict__ ft, TS* __restr
 // loss = scale * sum l (scale = weight / N: the reference's mean over the
 // batch then sum), grad = scale * dl/ds.  8 channels per thread-iteration,
 // per-block partials summed in block order by the last-arriving block.
+// margin == nullptr selects the plain squared error l = (s-t)^2 (FitNet's
+// hint MSE, reference distillers/FitNet.py:41-43, scale = weight / numel).
 __global__ void __launch_bounds__(256)
 ofd_loss_kernel(const bf16_t* __restrict__ s, const bf16_t* __restrict__ t,
                 const float* __restrict__ margin, bf16_t* __restrict__ grad, float* __restrict__ partial,
@@ -116,11 +118,15 @@ ofd_loss_kernel(const bf16_t* __restrict__ s, const bf16_t* __restrict__ t,
     for (int e = 0; e < 8; ++e) {
       const float sv = __uint_as_float((e & 1) ? (ws[e >> 1] & 0xffff0000u) : (ws[e >> 1] << 16));
       const float tv = __uint_as_float((e & 1) ? (wt[e >> 1] & 0xffff0000u) : (wt[e >> 1] << 16));
-      const float mv = margin[c0 + e];
       float l = 0.f, d = 0.f;
-      if (sv > mv && tv <= mv) { const float q = sv - mv; l += q * q; d += 2.f * q; }
-      if (sv > tv && tv > mv && tv <= 0.f) { const float q = sv - tv; l += q * q; d += 2.f * q; }
-      if (tv > 0.f) { const float q = sv - tv; l += q * q; d += 2.f * q; }
+      if (margin == nullptr) {  // plain squared error (FitNet hint)
+        const float q = sv - tv; l = q * q; d = 2.f * q;
+      } else {
+        const float mv = margin[c0 + e];
+        if (sv > mv && tv <= mv) { const float q = sv - mv; l += q * q; d += 2.f * q; }
+        if (sv > tv && tv > mv && tv <= 0.f) { const float q = sv - tv; l += q * q; d += 2.f * q; }
+        if (tv > 0.f) { const float q = sv - tv; l += q * q; d += 2.f * q; }
+      }
       acc += l;
       g[e] = scale * d;
     }

@@ -14,8 +14,11 @@
 //               w = min(epoch / warmup, 1) when an epoch pointer is given (else 1)
 //   g_ce[b,c] = d losses[0] / d s[b,c]     (same dtype as s)
 //   g_kd[b,c] = d losses[1] / d s[b,c]
+//   g_sum[b,c] = g_ce + g_kd (optional, fp32 sum rounded once)
 // The autograd backward combines them as go_ce*g_ce + go_kd*g_kd
-// (mda_axpby) so the two-backward DOT trainer works unchanged.
+// (mda_axpby) so the two-backward DOT trainer works unchanged; with the
+// training step's constant unit seeds it returns g_sum (or g_ce) and
+// launches nothing (ops/losses.py register_unit_seed).
 #include "common.h"
 
 namespace {
@@ -32,7 +35,8 @@ logit_loss_kernel(const TS* __restrict__ s, const TT* __restrict__ t,
                   TG* __restrict__ g_kd, float* __restrict__ partial,
                   unsigned* __restrict__ counter, float* __restrict__ losses,
                   int B, int C, float inv_T, float ce_w, float kd_w, float alpha,
-                  float beta, const float* __restrict__ epoch, float warmup) {
+                  float beta, const float* __restrict__ epoch, float warmup,
+                  TG* __restrict__ g_sum) {
   // DKD/ReviewKD-style linear warm-up of the KD term, min(epoch / warmup, 1),
   // read from device memory so a replayed hipGraph sees the current epoch
   if (epoch != nullptr && warmup > 0.f) kd_w *= fminf(*epoch / warmup, 1.f);
@@ -71,12 +75,15 @@ logit_loss_kernel(const TS* __restrict__ s, const TT* __restrict__ t,
     s_y = wave_sum(s_y);
     ce_row = (m1 + lz1 - s_y);  // -log softmax(s)_y
     const float gce_scale = ce_w * invB;
+    float gcv[NPL];
 #pragma unroll
     for (int i = 0; i < NPL; ++i) {
       int c = lane + 64 * i;
+      gcv[i] = 0.f;
       if (c < C) {
         float p = __expf(sv[i] - m1 - lz1);
-        io<TG>::st(g_ce, base + c, gce_scale * (p - (c == y ? 1.f : 0.f)));
+        gcv[i] = gce_scale * (p - (c == y ? 1.f : 0.f));
+        io<TG>::st(g_ce, base + c, gcv[i]);
       }
     }
     if (MODE == MODE_KD || MODE == MODE_DKD) {
@@ -109,7 +116,9 @@ logit_loss_kernel(const TS* __restrict__ s, const TT* __restrict__ t,
             float lp = tv[i] * inv_T - mt - lzt;
             float p = __expf(lp);
             kl += p * (lp - lq);
-            io<TG>::st(g_kd, base + c, gscale * (__expf(lq) - p));
+            const float gk = gscale * (__expf(lq) - p);
+            io<TG>::st(g_kd, base + c, gk);
+            if (g_sum) io<TG>::st(g_sum, base + c, gcv[i] + gk);
           }
         }
         kd_row = wave_sum(kl) * T * T;
@@ -175,6 +184,7 @@ logit_loss_kernel(const TS* __restrict__ s, const TT* __restrict__ t,
               gz = alpha * qh * tck + beta * (qh - ph);
             }
             io<TG>::st(g_kd, base + c, gs * gz);
+            if (g_sum) io<TG>::st(g_sum, base + c, gcv[i] + gs * gz);
           }
         }
         nckd = wave_sum(nckd);
@@ -216,23 +226,23 @@ logit_loss_kernel(const TS* __restrict__ s, const TT* __restrict__ t,
 template <typename TS, typename TT, int MODE, int NPL>
 int launch_t(const void* s, const void* t, const int64_t* y, void* gce, void* gkd, float* part,
              unsigned* cnt, float* losses, int B, int C, float invT, float cew, float kdw, float a,
-             float b, const float* ep, float wu, hipStream_t st) {
+             float b, const float* ep, float wu, void* gsum, hipStream_t st) {
   dim3 grid((B + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK);
   hipLaunchKernelGGL((logit_loss_kernel<TS, TT, TS, NPL, MODE>), grid, dim3(256), 0, st,
                      (const TS*)s, (const TT*)t, y, (TS*)gce, (TS*)gkd, part, cnt, losses, B, C,
-                     invT, cew, kdw, a, b, ep, wu);
+                     invT, cew, kdw, a, b, ep, wu, (TS*)gsum);
   MDA_CHECK_LAUNCH();
 }
 
 template <typename TS, typename TT, int MODE>
 int launch_npl(const void* s, const void* t, const int64_t* y, void* gce, void* gkd, float* part,
                unsigned* cnt, float* losses, int B, int C, float invT, float cew, float kdw,
-               float a, float b, const float* ep, float wu, hipStream_t st) {
+               float a, float b, const float* ep, float wu, void* gsum, hipStream_t st) {
   int npl = (C + 63) / 64;
 #define NPL_CASE(N)                                                                          \
   if (npl <= N)                                                                              \
     return launch_t<TS, TT, MODE, N>(s, t, y, gce, gkd, part, cnt, losses, B, C, invT, cew, \
-                                     kdw, a, b, ep, wu, st);
+                                     kdw, a, b, ep, wu, gsum, st);
   NPL_CASE(2) NPL_CASE(4) NPL_CASE(8) NPL_CASE(16) NPL_CASE(32)
 #undef NPL_CASE
   return (int)hipErrorInvalidValue;
@@ -241,14 +251,15 @@ int launch_npl(const void* s, const void* t, const int64_t* y, void* gce, void* 
 template <int MODE>
 int launch_mode(int dts, int dtt, const void* s, const void* t, const int64_t* y, void* gce,
                 void* gkd, float* part, unsigned* cnt, float* losses, int B, int C, float invT,
-                float cew, float kdw, float a, float b, const float* ep, float wu, hipStream_t st) {
+                float cew, float kdw, float a, float b, const float* ep, float wu, void* gs,
+                hipStream_t st) {
   if (dts == DT_F32 && dtt == DT_F32)
-    return launch_npl<float, float, MODE>(s, t, y, gce, gkd, part, cnt, losses, B, C, invT, cew, kdw, a, b, ep, wu, st);
+    return launch_npl<float, float, MODE>(s, t, y, gce, gkd, part, cnt, losses, B, C, invT, cew, kdw, a, b, ep, wu, gs, st);
   if (dts == DT_BF16 && dtt == DT_BF16)
-    return launch_npl<bf16_t, bf16_t, MODE>(s, t, y, gce, gkd, part, cnt, losses, B, C, invT, cew, kdw, a, b, ep, wu, st);
+    return launch_npl<bf16_t, bf16_t, MODE>(s, t, y, gce, gkd, part, cnt, losses, B, C, invT, cew, kdw, a, b, ep, wu, gs, st);
   if (dts == DT_BF16 && dtt == DT_F32)
-    return launch_npl<bf16_t, float, MODE>(s, t, y, gce, gkd, part, cnt, losses, B, C, invT, cew, kdw, a, b, ep, wu, st);
-  return launch_npl<float, bf16_t, MODE>(s, t, y, gce, gkd, part, cnt, losses, B, C, invT, cew, kdw, a, b, ep, wu, st);
+    return launch_npl<bf16_t, float, MODE>(s, t, y, gce, gkd, part, cnt, losses, B, C, invT, cew, kdw, a, b, ep, wu, gs, st);
+  return launch_npl<float, bf16_t, MODE>(s, t, y, gce, gkd, part, cnt, losses, B, C, invT, cew, kdw, a, b, ep, wu, gs, st);
 }
 
 // out = (*a) * x + (*b) * y ; a/b are device scalars (graph-replay safe).
@@ -273,13 +284,14 @@ MDA_API int mda_logit_loss(int64_t mode, int64_t dts, int64_t dtt, const void* s
                            const int64_t* y, void* g_ce, void* g_kd, float* partial,
                            unsigned* counter, float* losses, int64_t B, int64_t C, float inv_T,
                            float ce_w, float kd_w, float alpha, float beta, const float* epoch,
-                           float warmup, hipStream_t st) {
+                           float warmup, void* g_sum, hipStream_t st) {
   if (C > 64 * MAXNPL || B <= 0) return (int)hipErrorInvalidValue;
+  if (mode == MODE_CE) g_sum = nullptr;
   if (mode == MODE_CE)
-    return launch_mode<MODE_CE>(dts, dtt, s, t, y, g_ce, g_kd, partial, counter, losses, B, C, inv_T, ce_w, kd_w, alpha, beta, epoch, warmup, st);
+    return launch_mode<MODE_CE>(dts, dtt, s, t, y, g_ce, g_kd, partial, counter, losses, B, C, inv_T, ce_w, kd_w, alpha, beta, epoch, warmup, g_sum, st);
   if (mode == MODE_KD)
-    return launch_mode<MODE_KD>(dts, dtt, s, t, y, g_ce, g_kd, partial, counter, losses, B, C, inv_T, ce_w, kd_w, alpha, beta, epoch, warmup, st);
-  return launch_mode<MODE_DKD>(dts, dtt, s, t, y, g_ce, g_kd, partial, counter, losses, B, C, inv_T, ce_w, kd_w, alpha, beta, epoch, warmup, st);
+    return launch_mode<MODE_KD>(dts, dtt, s, t, y, g_ce, g_kd, partial, counter, losses, B, C, inv_T, ce_w, kd_w, alpha, beta, epoch, warmup, g_sum, st);
+  return launch_mode<MODE_DKD>(dts, dtt, s, t, y, g_ce, g_kd, partial, counter, losses, B, C, inv_T, ce_w, kd_w, alpha, beta, epoch, warmup, g_sum, st);
 }
 
 MDA_API int mda_axpby(int64_t dt, const float* a, const void* x, const float* b, const void* y,

@@ -78,6 +78,24 @@ def workspace(device) -> _Workspace:
     return ws
 
 
+_UNIT_SEEDS: list = []   # strong references: their memory is never reused
+_UNIT_PTRS: set = set()
+
+
+def register_unit_seed(t: torch.Tensor) -> None:
+    """``t`` is a scalar that holds 1.0 for as long as the process lives and is
+    never written (the training step's backward seed, engine/step.py).  A
+    logit-loss backward that receives it returns the stored gradient as is
+    instead of launching the ``go * g`` scaling."""
+    if t.numel() == 1 and t.data_ptr() not in _UNIT_PTRS:
+        _UNIT_SEEDS.append(t)
+        _UNIT_PTRS.add(t.data_ptr())
+
+
+def _is_unit(go) -> bool:
+    return go is not None and go.numel() == 1 and go.data_ptr() in _UNIT_PTRS
+
+
 def _supported(s, t, C):
     return (s.dim() == 2 and s.dtype in _DT and (t is None or t.dtype in _DT)
             and C <= 2048 and s.shape[0] <= 8192)
@@ -92,19 +110,37 @@ class _LogitLoss(torch.autograd.Function):
         B, C = s.shape
         g_ce = torch.empty_like(s)
         g_kd = torch.empty_like(s) if mode != 0 else g_ce
+        # g_ce + g_kd for the unit-seed backward (not needed by DOT's stacked sets)
+        from .hip_train import _DUAL
+        g_sum = torch.empty_like(s) if (mode != 0 and _DUAL[0] is None) else None
         losses = torch.empty(2, dtype=torch.float32, device=s.device)
         ws = workspace(s.device)
         _ext.call("mda_logit_loss", mode, _DT[s.dtype], _DT[t.dtype], s, t, target, g_ce, g_kd,
                   ws.partial, ws.counter, losses, B, C, inv_T, ce_w, kd_w, alpha, beta,
-                  _epoch_ptr(epoch, warmup), float(warmup or 0.0))
-        ctx.save_for_backward(g_ce, g_kd)
+                  _epoch_ptr(epoch, warmup), float(warmup or 0.0), g_sum)
+        ctx.save_for_backward(g_ce, g_kd, g_sum)
         ctx.mode = mode
+        # an unused loss output gets no zero-filled gradient (one launch less)
+        ctx.set_materialize_grads(False)
         return losses[0], losses[1]
 
     @staticmethod
     def backward(ctx, go_ce, go_kd):
-        g_ce, g_kd = ctx.saved_tensors
+        g_ce, g_kd, g_sum = ctx.saved_tensors
         from .hip_train import _DUAL, dual_alloc
+        if go_ce is None and go_kd is None:
+            return (None,) * 11
+        if _DUAL[0] is None:
+            # the training step's constant unit seeds: nothing to scale
+            uce, ukd = _is_unit(go_ce), _is_unit(go_kd)
+            if ctx.mode == 0 or go_kd is None:
+                if uce:
+                    return (g_ce,) + (None,) * 10
+            elif go_ce is None:
+                if ukd:
+                    return (g_kd,) + (None,) * 10
+            elif uce and ukd and g_sum is not None:
+                return (g_sum,) + (None,) * 10
         if _DUAL[0] is not None:
             # DOT single-pass backward: [go_kd * g_kd ; go_ce * g_ce] stacked,
             # the KD set first (ops/hip_train.py _Dual)

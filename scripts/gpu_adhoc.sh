@@ -1,2 +1,4 @@
 export PYTHONPATH=$PWD TMPDIR=/tmp
-timeout -k 10 1100 python -u -m pytest tests/test_gpu_multirank.py "tests/test_gpu_e2e.py::test_deterministic_mode_graph_runs_are_bitwise_equal" tests/test_gpu_kernels_losses_optim.py tests/test_gpu_vid_nst.py -x -v --timeout 400 --timeout-method thread > gpurun_out/t_mr.log 2>&1; rc=$?; grep -E "PASS|FAIL|Error|passed|failed" gpurun_out/t_mr.log | tail -14; exit $rc
+TESTS="tests/test_gpu_kernels_losses_optim.py tests/test_gpu_vid_nst.py" bash scripts/gpu_run.sh && \
+BENCH="--steps 500 --warmup 30;--steps 500 --warmup 30 EXPERIMENT.DETERMINISTIC True;--steps 500 --warmup 30 --batch 8;--cfg configs/cifar100/vanilla.yaml --steps 500 --warmup 30" bash scripts/gpu_run.sh && \
+PROF="configs/cifar100/dkd/res32x4_res8x4.yaml:flag_r5b;configs/cifar100/vanilla.yaml:van_r5b" TOP=60 bash scripts/gpu_run.sh

@@ -157,3 +157,30 @@ def test_ofd_fused_loss_matches_torch(N, C, H):
     (lr * 0.5).backward()
     torch.testing.assert_close(l, lr, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(sh.grad.float(), sr.grad, rtol=2e-2, atol=1e-4)
+
+
+@pytest.mark.parametrize("mode", ["ce", "kd", "dkd"])
+def test_unit_seed_backward_matches_scaled_path(mode):
+    """With the training step's registered unit seeds the loss backward
+    returns the kernel's stored (summed) gradient without a launch; it must
+    equal the go * g path of an ordinary seed to within one bf16 rounding."""
+    torch.manual_seed(0)
+    B, C = 64, 100
+    s0 = torch.randn(B, C, device="cuda").to(torch.bfloat16)
+    t = torch.randn(B, C, device="cuda").to(torch.bfloat16)
+    y = torch.randint(0, C, (B,), device="cuda")
+    unit = torch.ones((), device="cuda")
+    L.register_unit_seed(unit)
+    grads = []
+    for seed in (unit, torch.ones((), device="cuda")):
+        s = s0.clone().requires_grad_(True)
+        with use_backend("hip"):
+            if mode == "ce":
+                terms = [L.ce(s, y, 1.0)]
+            elif mode == "kd":
+                terms = list(L.ce_kd(s, t, y, 4.0, 0.1, 0.9))
+            else:
+                terms = list(L.ce_dkd(s, t, y, 1.0, 1.0, 8.0, 4.0))
+        torch.autograd.backward(terms, [seed] * len(terms))
+        grads.append(s.grad.float())
+    torch.testing.assert_close(grads[0], grads[1], rtol=1e-2, atol=1e-5)

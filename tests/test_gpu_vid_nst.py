@@ -103,3 +103,23 @@ def test_convreg_bias_native_matches_fp32(k):
     assert m.conv.bias.grad.abs().max().item() == 0.0
     assert m_r.conv.bias.grad.abs().max().item() < 1e-3 * m_r.conv.weight.grad.abs().max().item() + 1e-5
     assert rel(m.bn.weight.grad, m_r.bn.weight.grad) < 5e-2
+
+
+@pytest.mark.parametrize("N,C,H", [(64, 256, 8), (64, 128, 16), (8, 64, 32)])
+def test_fitnet_hint_mse_native_matches_fp32(N, C, H):
+    """FitNet's hint loss (csrc/feat.hip mda_ofd_loss, no margin) vs
+    weight * F.mse_loss in fp32 (reference `distillers/FitNet.py:41-43`)."""
+    from mdistiller_ddp_amd.distillers.FitNet import hint_loss
+    torch.manual_seed(0)
+    fs = torch.randn(N, C, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    ft = torch.randn(N, C, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    a = fs.clone().requires_grad_(True)
+    with use_backend("hip"):
+        loss = hint_loss(a, ft, 100.0)
+    (2.0 * loss).backward()
+    b = fs.float().clone().requires_grad_(True)
+    ref = 100.0 * torch.nn.functional.mse_loss(b, ft.float())
+    (2.0 * ref).backward()
+    assert loss.grad_fn is not None and "HintMSE" in type(loss.grad_fn).__name__
+    torch.testing.assert_close(loss.float(), ref, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(a.grad.float(), b.grad, rtol=1e-2, atol=1e-6)

@@ -28,6 +28,9 @@ import contextlib
 
 import os
 
+# zero fills and the stem image pad ride in the weight-pack launch (A/B knob)
+_PACK_EXTRAS = os.environ.get("MDA_PACK_EXTRAS", "1") != "0"
+
 import torch
 
 from ..parallel import GradReducer, get_world_size
@@ -516,13 +519,19 @@ class TrainStep:
                 packs = self._packs
                 if packs is None:
                     packs = self._packs = hip_train.PackCache()
-        if len(zero) > 1 and zero[0].dtype == zero[1].dtype:
-            torch._foreach_zero_(zero)
-        else:
-            for t in zero:
-                t.zero_()
+        # the zero fills (and, for a captured step, the stem's padded image)
+        # ride in the weight-pack launch
+        img = b.get("image") if (self.use_graph and _PACK_EXTRAS) else None
+        zx = zero if _PACK_EXTRAS else ()
+        if packs is None or not packs.pack_all(self.device, zero=zx, image=img) or not zx:
+            if len(zero) > 1 and zero[0].dtype == zero[1].dtype:
+                torch._foreach_zero_(zero)
+            else:
+                for t in zero:
+                    t.zero_()
+            if packs is not None and not packs.armed:
+                packs.pack_all(self.device)
         if packs is not None:
-            packs.pack_all(self.device)
             hip_train.set_active_packs(packs)
         try:
             preds, losses = self._forward(b)
@@ -607,7 +616,10 @@ class TrainStep:
             self.use_graph = False
             return out
         if self.is_dot and self.dot_dual and not self.dot_single and self.graph_comm is not True:
-            return self._capture_dot_dual(static, pool, s, out)
+            try:
+                return self._capture_dot_dual(static, pool, s, out)
+            finally:
+                self._bn_end()
         feed = None
         if self._lookahead_on(static) and getattr(self.distiller, "teacher", None) is not None:
             feed = self._capture_teacher_feed(static, pool, s)
@@ -617,6 +629,10 @@ class TrainStep:
         try:
             self._capture_step(static, pool, s)
         finally:
+            # the step's arena window closes with its capture: a teacher graph
+            # captured next (split look-ahead) must not take regions from it,
+            # or the step's zero fill at its start races that graph's replay
+            self._bn_end()
             if feed is not None:
                 feed.mode = None  # eager steps (e.g. a partial batch) run the teacher inline
         if feed is not None and self.teacher_split:

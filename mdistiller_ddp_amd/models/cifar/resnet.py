@@ -49,7 +49,8 @@ class BasicBlock(nn.Module):
         # on the native kernels conv1's launch computes both (arm_conv_pair)
         paired = self.downsample is not None and arm_conv_pair(
             x, self.conv1, self.bn1, self.downsample[0], self.downsample[1])
-        h, _ = conv_bn_act(x, self.conv1, self.bn1, "relu", fork=fork)
+        # h feeds conv2 only: conv2's dgrad may finish bn1's backward
+        h, _ = conv_bn_act(x, self.conv1, self.bn1, "relu", fork=fork, private=True)
         if self.downsample is None:
             res = x
         else:
@@ -63,8 +64,10 @@ class BasicBlock(nn.Module):
             res = (self._shortcut(x, fork, defer) if paired
                    else run_branch(x, lambda t: self._shortcut(t, fork, defer)))
             fork = None
+        # the block output is a stage feature only when features are consumed
         return conv_bn_act(h, self.conv2, self.bn2, "relu", residual=res,
-                           want_preact=self.is_last and self._need_preact, res_fork=fork)
+                           want_preact=self.is_last and self._need_preact, res_fork=fork,
+                           private=not (self.is_last and self._need_preact))
 
 
 class Bottleneck(nn.Module):
@@ -90,13 +93,14 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         fork = grad_fork(x)
-        h, _ = conv_bn_act(x, self.conv1, self.bn1, "relu", fork=fork)
-        h, _ = conv_bn_act(h, self.conv2, self.bn2, "relu")
+        h, _ = conv_bn_act(x, self.conv1, self.bn1, "relu", fork=fork, private=True)
+        h, _ = conv_bn_act(h, self.conv2, self.bn2, "relu", private=True)
         res = x if self.downsample is None else run_branch(
             x, lambda t: self._shortcut(t, fork, can_defer_residual(h, self.conv3, self.bn3)))
         return conv_bn_act(h, self.conv3, self.bn3, "relu", residual=res,
                            want_preact=self.is_last and self._need_preact,
-                           res_fork=fork if self.downsample is None else None)
+                           res_fork=fork if self.downsample is None else None,
+                           private=not (self.is_last and self._need_preact))
 
 
 class Stage(nn.Sequential):
@@ -174,7 +178,9 @@ class ResNet(nn.Module, ModelBase):
 
     def forward(self, x):
         need = self._need_preact
-        x, f0_pre = conv_bn_act(x, self.conv1, self.bn1, "relu", want_preact=need)
+        # logit-only consumers (need False): no feature takes a gradient, so
+        # the stage outputs are private to the native layers (BnLink.private)
+        x, f0_pre = conv_bn_act(x, self.conv1, self.bn1, "relu", want_preact=need, private=not need)
         f0 = x
         x, f1_pre = self.layer1(x)
         f1 = x

@@ -36,7 +36,7 @@ class BasicBlock(nn.Module):
         return conv_bn_act(x, self.shortcut[0], self.shortcut[1], "none")[0]
 
     def forward(self, x):
-        h, _ = conv_bn_act(x, self.conv1, self.bn1, "relu")
+        h, _ = conv_bn_act(x, self.conv1, self.bn1, "relu", private=True)
         return conv_bn_act(h, self.conv2, self.bn2, "relu", residual=self._res(x),
                            want_preact=self.is_last and self._need_preact)
 
@@ -61,8 +61,8 @@ class Bottleneck(BasicBlock):
                 nn.BatchNorm2d(self.expansion * planes))
 
     def forward(self, x):
-        h, _ = conv_bn_act(x, self.conv1, self.bn1, "relu")
-        h, _ = conv_bn_act(h, self.conv2, self.bn2, "relu")
+        h, _ = conv_bn_act(x, self.conv1, self.bn1, "relu", private=True)
+        h, _ = conv_bn_act(h, self.conv2, self.bn2, "relu", private=True)
         return conv_bn_act(h, self.conv3, self.bn3, "relu", residual=self._res(x),
                            want_preact=self.is_last and self._need_preact)
 

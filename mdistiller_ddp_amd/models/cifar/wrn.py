@@ -31,7 +31,7 @@ class BasicBlock(nn.Module):
 
     def forward(self, x):
         xa, _ = bn_act(x, self.bn1, "relu")
-        o, _ = conv_bn_act(xa, self.conv1, self.bn2, "relu")
+        o, _ = conv_bn_act(xa, self.conv1, self.bn2, "relu", private=self.droprate == 0)
         if self.droprate > 0:
             o = F.dropout(o, p=self.droprate, training=self.training)
         res = x if self.equalInOut else conv_bn_act(xa, self.convShortcut, None, "none")[0]

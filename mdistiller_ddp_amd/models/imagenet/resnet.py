@@ -61,10 +61,11 @@ class BasicBlock(nn.Module):
         # conv1 + projection shortcut in one launch on the native kernels
         paired = self.downsample is not None and arm_conv_pair(
             x, self.conv1, self.bn1, self.downsample[0], self.downsample[1])
-        h, _ = conv_bn_act(x, self.conv1, self.bn1, "relu", fork=fork)
+        h, _ = conv_bn_act(x, self.conv1, self.bn1, "relu", fork=fork, private=True)
         res, res_fork = self._res(x, fork, h, self.conv2, self.bn2, paired)  # after conv1: its backward runs first
         return conv_bn_act(h, self.conv2, self.bn2, "relu", residual=res,
-                           want_preact=self.is_last and self._need_preact, res_fork=res_fork)
+                           want_preact=self.is_last and self._need_preact, res_fork=res_fork,
+                           private=not (self.is_last and self._need_preact))
 
 
 class Bottleneck(BasicBlock):
@@ -86,11 +87,12 @@ class Bottleneck(BasicBlock):
 
     def forward(self, x):
         fork = grad_fork(x)
-        h, _ = conv_bn_act(x, self.conv1, self.bn1, "relu", fork=fork)
-        h, _ = conv_bn_act(h, self.conv2, self.bn2, "relu")
+        h, _ = conv_bn_act(x, self.conv1, self.bn1, "relu", fork=fork, private=True)
+        h, _ = conv_bn_act(h, self.conv2, self.bn2, "relu", private=True)
         res, res_fork = self._res(x, fork, h, self.conv3, self.bn3)  # after conv1: its backward runs first
         return conv_bn_act(h, self.conv3, self.bn3, "relu", residual=res,
-                           want_preact=self.is_last and self._need_preact, res_fork=res_fork)
+                           want_preact=self.is_last and self._need_preact, res_fork=res_fork,
+                           private=not (self.is_last and self._need_preact))
 
 
 class ResNet(nn.Module, ModelBase):

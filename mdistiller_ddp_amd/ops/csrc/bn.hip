@@ -580,14 +580,6 @@ MDA_API int mda_bn_finalize(const float* partial, int64_t nblk, int64_t M, int64
 
 namespace {
 
-struct FinArgs {
-  const float* gamma; const float* beta;
-  float* running_mean; float* running_var;
-  float* stats;          // [4][C]: mean, rstd, scale, shift (written by block 0)
-  float momentum, eps;
-  int64_t* nbt;
-};
-
 // Block sums a[8], b[8] of the thread's channel group -> region shard.
 __device__ __forceinline__ void region_block_add(BnRegion* r, float (&a)[8], float (&b)[8], int C,
                                                  int rpi) {
@@ -615,26 +607,6 @@ __device__ __forceinline__ void region_block_add(BnRegion* r, float (&a)[8], flo
     for (; rr < rpi; ++rr) acc[0] += sm[q][rr * C + c];
     acc_add(region_acc(r, C, shard, q) + c, (double)((acc[0] + acc[1]) + (acc[2] + acc[3])));
   }
-}
-
-// Channel c's totals over the SH shards (plain loads when the sums come from
-// an earlier launch, device-coherent ones behind an in-kernel barrier): all
-// 2*SH loads of a channel in flight together.
-template <bool COHERENT>
-__device__ __forceinline__ void region_channel(BnRegion* r, int C, int c, double& t0, double& t1) {
-  const int SH = slot_shards(C);
-  double a[SLOT_SHMAX], b[SLOT_SHMAX];
-#pragma unroll
-  for (int k = 0; k < SLOT_SHMAX; ++k) {
-    const double* pa = region_acc(r, C, k, 0) + c;
-    const double* pb = region_acc(r, C, k, 1) + c;
-    a[k] = k < SH ? (COHERENT ? acc_load(pa) : *pa) : 0.0;
-    b[k] = k < SH ? (COHERENT ? acc_load(pb) : *pb) : 0.0;
-  }
-  t0 = 0.0;
-  t1 = 0.0;
-#pragma unroll
-  for (int k = 0; k < SLOT_SHMAX; ++k) { t0 += a[k]; t1 += b[k]; }
 }
 
 // Standalone statistics pass (y already materialised: depthwise convs,
@@ -693,31 +665,11 @@ __device__ __forceinline__ void apply8(const uint4& yv, const uint4& rv, bool ha
   z = make_uint4(zo[0], zo[1], zo[2], zo[3]);
 }
 
-// Batch statistics of channel c from a region -> scale / shift (and, by block
-// 0, the [4][C] stats of the backward and the running-stat update).
+// Batch statistics of channel c from a region -> scale / shift (block 0
+// writes the [4][C] stats and the running statistics; bnslot.h fin_channel_w).
 __device__ __forceinline__ void fin_channel(BnRegion* reg, int64_t M, int C, int c, const FinArgs& f,
                                             float& sc, float& sh) {
-  double t0, t1;
-  region_channel<false>(reg, C, c, t0, t1);
-  const double mean = t0 / (double)M;
-  double var = t1 / (double)M - mean * mean;
-  if (var < 0) var = 0;
-  const float rstd = (float)(1.0 / sqrt(var + (double)f.eps));
-  const float g = f.gamma ? f.gamma[c] : 1.f;
-  const float bb = f.beta ? f.beta[c] : 0.f;
-  sc = g * rstd;
-  sh = bb - (float)mean * sc;
-  if (blockIdx.x == 0) {
-    f.stats[c] = (float)mean;
-    f.stats[C + c] = rstd;
-    f.stats[2 * C + c] = sc;
-    f.stats[3 * C + c] = sh;
-    if (f.running_mean) {
-      const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
-      f.running_mean[c] = (1.f - f.momentum) * f.running_mean[c] + f.momentum * (float)mean;
-      f.running_var[c] = (1.f - f.momentum) * f.running_var[c] + f.momentum * (float)unbiased;
-    }
-  }
+  fin_channel_w<false>(reg, M, C, c, f, sc, sh, blockIdx.x == 0);
 }
 
 // z = y*scale + shift (+ res); out = act(z); preact = z -- with the finalize

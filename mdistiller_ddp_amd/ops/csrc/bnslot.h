@@ -62,12 +62,13 @@ __device__ __forceinline__ double acc_load(const double* a) {
 // the last of a group bumps `top`; thread 0 of every block polls `top`.
 // Spins are bounded (~2 s): on timeout *err is set and the kernel
 // completes with wrong values instead of hanging the GPU.
-__device__ __forceinline__ void region_grid_barrier(BnRegion* r, unsigned* err) {
+// nb blocks in the grid, bid = this block's linear index (2-D / 3-D grids).
+__device__ __forceinline__ void region_grid_barrier_n(BnRegion* r, unsigned* err, unsigned nb,
+                                                      unsigned bid) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    const unsigned nb = gridDim.x;
-    const unsigned g = blockIdx.x % BAR_GROUPS;
+    const unsigned g = bid % BAR_GROUPS;
     const unsigned ngroups = nb < BAR_GROUPS ? nb : BAR_GROUPS;
     const unsigned gsize = (nb - g + BAR_GROUPS - 1) / BAR_GROUPS;
     const unsigned t = __hip_atomic_fetch_add(&r->grp[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -82,4 +83,66 @@ __device__ __forceinline__ void region_grid_barrier(BnRegion* r, unsigned* err) 
     }
   }
   __syncthreads();
+}
+
+__device__ __forceinline__ void region_grid_barrier(BnRegion* r, unsigned* err) {
+  region_grid_barrier_n(r, err, gridDim.x, blockIdx.x);
+}
+
+// Finalize / running-stat operands of one training BN (forward).
+struct FinArgs {
+  const float* gamma; const float* beta;
+  float* running_mean; float* running_var;
+  float* stats;          // [4][C]: mean, rstd, scale, shift (written by one block)
+  float momentum, eps;
+  int64_t* nbt;
+};
+
+// Channel c's totals over the SH shards (plain loads when the sums come from
+// an earlier launch, device-coherent ones behind an in-kernel barrier): all
+// 2*SH loads of a channel in flight together.
+template <bool COHERENT>
+__device__ __forceinline__ void region_channel(BnRegion* r, int C, int c, double& t0, double& t1) {
+  const int SH = slot_shards(C);
+  double a[SLOT_SHMAX], b[SLOT_SHMAX];
+#pragma unroll
+  for (int k = 0; k < SLOT_SHMAX; ++k) {
+    const double* pa = region_acc(r, C, k, 0) + c;
+    const double* pb = region_acc(r, C, k, 1) + c;
+    a[k] = k < SH ? (COHERENT ? acc_load(pa) : *pa) : 0.0;
+    b[k] = k < SH ? (COHERENT ? acc_load(pb) : *pb) : 0.0;
+  }
+  t0 = 0.0;
+  t1 = 0.0;
+#pragma unroll
+  for (int k = 0; k < SLOT_SHMAX; ++k) { t0 += a[k]; t1 += b[k]; }
+}
+
+// Batch statistics of channel c from a region -> scale / shift; `writer`
+// (one block per channel) also stores the [4][C] stats of the backward and
+// updates the running statistics.
+template <bool COHERENT>
+__device__ __forceinline__ void fin_channel_w(BnRegion* reg, int64_t M, int C, int c, const FinArgs& f,
+                                              float& sc, float& sh, bool writer) {
+  double t0, t1;
+  region_channel<COHERENT>(reg, C, c, t0, t1);
+  const double mean = t0 / (double)M;
+  double var = t1 / (double)M - mean * mean;
+  if (var < 0) var = 0;
+  const float rstd = (float)(1.0 / sqrt(var + (double)f.eps));
+  const float g = f.gamma ? f.gamma[c] : 1.f;
+  const float bb = f.beta ? f.beta[c] : 0.f;
+  sc = g * rstd;
+  sh = bb - (float)mean * sc;
+  if (writer) {
+    f.stats[c] = (float)mean;
+    f.stats[C + c] = rstd;
+    f.stats[2 * C + c] = sc;
+    f.stats[3 * C + c] = sh;
+    if (f.running_mean) {
+      const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
+      f.running_mean[c] = (1.f - f.momentum) * f.running_mean[c] + f.momentum * (float)mean;
+      f.running_var[c] = (1.f - f.momentum) * f.running_var[c] + f.momentum * (float)unbiased;
+    }
+  }
 }

@@ -855,7 +855,14 @@ pack_kernel(const float* __restrict__ w, bf16_t* __restrict__ wf, bf16_t* __rest
 // written as T-long contiguous runs of both packed layouts:
 //   wf[co][tap*Cin + ci]   and   wt[ci][tap*Cout + co].
 // Depthwise layers ride along (Cin = -1 rows): fp32 [C,1,3,3] -> tap-major
-// [9, C] (csrc/dwconv.hip's operand), 256 elements per tile.
+// [9, C] (csrc/dwconv.hip's operand), 256 elements per tile.  So does the
+// rest of the step's prologue, each one launch less in the captured chain:
+//   Cin = -2  channel-padded stem operand {w, wf, 0, Cout, -2, KH, KW, Kp,
+//             C | Cp << 16}: wf[co][tap*Cp + ci], 256 elements per tile
+//   Cin = -3  zero fill {ptr, nbytes (multiple of 4)}: 16 KB per tile (the
+//             flat gradients and the step's BN-region arena)
+//   Cin = -4  image pad {x, y, dt, M, -4, C}: [M, C] fp32/bf16 NHWC ->
+//             [M, 8] bf16 (zeros beyond C), 256 pixels per tile
 // Padding columns (k >= K, and the dgrad tail) are never touched: they are
 // zeroed once by the per-layer pack at registration and stay zero.
 // (The previous element-per-thread version scattered 2-byte stores at
@@ -882,13 +889,60 @@ pack_multi_kernel(const int64_t* __restrict__ table, int L) {
   int l = 0;
   while (l + 1 < L && (int64_t)blockIdx.x >= tb[(l + 1) * PACK_FIELDS + 9]) ++l;
   const int64_t* e = tb + l * PACK_FIELDS;
-  if (e[4] < 0) {  // depthwise row {w [C,1,3,3], dst fp32 [9, C], 0, C, -1, ...}: 256 elements a tile
-    const float* w = (const float*)e[0];
-    float* dst = (float*)e[1];
-    const int C = (int)e[3];
-    const int i = (int)(blockIdx.x - e[9]) * 256 + threadIdx.x;
-    if (i < 9 * C) dst[i] = w[(i % C) * 9 + i / C];
-    return;  // block-uniform branch (l depends on blockIdx only)
+  if (e[4] < 0) {  // block-uniform branches (l depends on blockIdx only)
+    const int64_t t = (int64_t)blockIdx.x - e[9];
+    if (e[4] == -1) {  // depthwise {w [C,1,3,3], dst fp32 [9, C], 0, C, -1}
+      const float* w = (const float*)e[0];
+      float* dst = (float*)e[1];
+      const int C = (int)e[3];
+      const int i = (int)t * 256 + threadIdx.x;
+      if (i < 9 * C) dst[i] = w[(i % C) * 9 + i / C];
+    } else if (e[4] == -2) {  // channel-padded stem operand
+      const float* w = (const float*)e[0];
+      bf16_t* wf = (bf16_t*)e[1];
+      const int Cout = (int)e[3], KH = (int)e[5], KW = (int)e[6], Kp = (int)e[7];
+      const int C = (int)(e[8] & 0xffff), Cp = (int)(e[8] >> 16);
+      const int64_t i = t * 256 + threadIdx.x;
+      if (i < (int64_t)Cout * Kp) {
+        const int co = (int)(i / Kp), k = (int)(i - (int64_t)co * Kp);
+        float v = 0.f;
+        if (k < KH * KW * Cp) {
+          const int tap = k / Cp, ci = k - tap * Cp;
+          if (ci < C) v = w[(((int64_t)co * C + ci) * KH + tap / KW) * KW + tap % KW];
+        }
+        wf[i] = f2bf(v);
+      }
+    } else if (e[4] == -3) {  // zero fill: 16-byte stores, 4-byte tail
+      char* base = (char*)e[0];
+      const int64_t nb = e[1];
+      const int64_t o0 = t * 16384;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t o = o0 + ((int64_t)r * 256 + threadIdx.x) * 16;
+        if (o + 16 <= nb) {
+          *(uint4*)(base + o) = make_uint4(0u, 0u, 0u, 0u);
+        } else if (o < nb) {
+          for (int64_t q = o; q < nb; q += 4) *(uint32_t*)(base + q) = 0u;
+        }
+      }
+    } else {  // image pad to 8 channels
+      const int64_t M = e[3];
+      const int C = (int)e[5];
+      const int64_t m = t * 256 + threadIdx.x;
+      if (m < M) {
+        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (e[2] == DT_F32) {
+          const float* x = (const float*)e[0];
+          for (int c = 0; c < C; ++c) v[c] = x[m * C + c];
+        } else {
+          const bf16_t* x = (const bf16_t*)e[0];
+          for (int c = 0; c < C; ++c) v[c] = bf2f(x[m * C + c]);
+        }
+        *(uint4*)((bf16_t*)e[1] + m * 8) = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
+                                                      pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+      }
+    }
+    return;
   }
   const float* w = (const float*)e[0];
   bf16_t* wf = (bf16_t*)e[1];

@@ -115,7 +115,7 @@ __global__ void __launch_bounds__(256)
 pool_fc_bwd_kernel(const T* __restrict__ dl, const T* __restrict__ dpooled,
                    const T* __restrict__ pooled, const float* __restrict__ W,
                    float* __restrict__ dW, float* __restrict__ db, T* __restrict__ dx, int N,
-                   int HW, int C, int J, float inv_hw, int accum, HeadBn bn) {
+                   int HW, int C, int J, float inv_hw, int accum, HeadBn bn, int ksplit) {
   extern __shared__ float sh[];
   if ((int)blockIdx.x < J) {
     // ---- dW[j, :] = sum_n dl[n, j] * pooled[n, :];  db[j] = sum_n dl[n, j]
@@ -124,11 +124,15 @@ pool_fc_bwd_kernel(const T* __restrict__ dl, const T* __restrict__ dpooled,
     __syncthreads();
     if (dW != nullptr) {
       for (int c = threadIdx.x; c < C; c += blockDim.x) {
-        float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // 8 loads in flight
+        float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         int n = 0;
-        for (; n + 8 <= N; n += 8)
+        for (; n + 32 <= N; n += 32) {  // 32 loads in flight per round
+          float v[32];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) a[u] += sh[n + u] * io<T>::ld(pooled, (int64_t)(n + u) * C + c);
+          for (int u = 0; u < 32; ++u) v[u] = io<T>::ld(pooled, (int64_t)(n + u) * C + c);
+#pragma unroll
+          for (int u = 0; u < 32; ++u) a[u & 7] += sh[n + u] * v[u];
+        }
         for (; n < N; ++n) a[0] += sh[n] * io<T>::ld(pooled, (int64_t)n * C + c);
         const float acc = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
         float* o = dW + (int64_t)j * C + c;
@@ -143,8 +147,12 @@ pool_fc_bwd_kernel(const T* __restrict__ dl, const T* __restrict__ dpooled,
     }
     return;
   }
-  // ---- dx[n, p, :] = (dpooled[n, :] + dl[n, :] @ W) / HW   for every p
-  const int n = blockIdx.x - J;
+  // ---- dx[n, p, :] = (dpooled[n, :] + dl[n, :] @ W) / HW   for every p;
+  // ksplit blocks per image, each owning HW / ksplit pixels (the dx vector is
+  // recomputed per block: W is L2-resident and the pixel loop is the cost)
+  const int n = (blockIdx.x - J) / ksplit;
+  const int part = (blockIdx.x - J) - n * ksplit;
+  const int hw_b = HW / ksplit, p_lo = part * hw_b;
   float* sdl = sh;                                   // [J]
   float* sv = sh + (N > J ? N : J);                  // [C] the stored (rounded) dx value
   float* sred = sv + C;                              // [2][P][C] BN partials
@@ -152,11 +160,15 @@ pool_fc_bwd_kernel(const T* __restrict__ dl, const T* __restrict__ dpooled,
   __syncthreads();
   T* dxn = dx + (int64_t)n * HW * C;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // 8 loads in flight
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     int j = 0;
-    for (; j + 8 <= J; j += 8)
+    for (; j + 32 <= J; j += 32) {  // 32 weight loads in flight per round
+      float w[32];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) a[u] += sdl[j + u] * W[(int64_t)(j + u) * C + c];
+      for (int u = 0; u < 32; ++u) w[u] = W[(int64_t)(j + u) * C + c];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) a[u & 7] += sdl[j + u] * w[u];
+    }
     for (; j < J; ++j) a[0] += sdl[j] * W[(int64_t)j * C + c];
     const float acc = (dpooled ? io<T>::ld(dpooled, (int64_t)n * C + c) : 0.f) +
                       (((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7])));
@@ -194,12 +206,26 @@ pool_fc_bwd_kernel(const T* __restrict__ dl, const T* __restrict__ dpooled,
       }
       const bf16_t* yn = bn.y ? bn.y + (int64_t)n * HW * C : nullptr;
       const bf16_t* rn = bn.res ? bn.res + (int64_t)n * HW * C : nullptr;
-      for (int p = pg; p < HW; p += P) {
+      for (int p0 = p_lo + pg; p0 < p_lo + hw_b; p0 += 4 * P) {
+        // up to 4 pixels' BN-input loads in flight before any math
+        uint4 yv4[4], rv4[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int p = p0 + k * P;
+          const bool ok = bn.reg != nullptr && p < p_lo + hw_b;
+          const int64_t o = (int64_t)(ok ? p : p_lo) * C + c0;
+          yv4[k] = ok ? *(const uint4*)(yn + o) : make_uint4(0u, 0u, 0u, 0u);
+          rv4[k] = (ok && rn) ? *(const uint4*)(rn + o) : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+        const int p = p0 + k * P;
+        if (p >= p_lo + hw_b) break;
         const int64_t o = (int64_t)p * C + c0;
         *(uint4*)(dxn + o) = dv;
         if (bn.reg != nullptr) {
-          const uint4 yv = *(const uint4*)(yn + o);
-          const uint4 rv = rn ? *(const uint4*)(rn + o) : make_uint4(0u, 0u, 0u, 0u);
+          const uint4 yv = yv4[k];
+          const uint4 rv = rv4[k];
           const uint32_t yw[4] = {yv.x, yv.y, yv.z, yv.w}, rw[4] = {rv.x, rv.y, rv.z, rv.w};
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
@@ -213,6 +239,7 @@ pool_fc_bwd_kernel(const T* __restrict__ dl, const T* __restrict__ dpooled,
             s2[e] += g * ((yf - mu[e]) * rs[e]);
           }
         }
+        }
       }
     }
     if (bn.reg == nullptr) return;
@@ -225,7 +252,7 @@ pool_fc_bwd_kernel(const T* __restrict__ dl, const T* __restrict__ dpooled,
       }
     }
     __syncthreads();
-    const int shard = n % slot_shards(C);
+    const int shard = (blockIdx.x - J) % slot_shards(C);
     for (int t = threadIdx.x; t < 2 * C; t += blockDim.x) {
       const int q = t / C, c = t - q * C;
       float a = 0.f;
@@ -234,7 +261,7 @@ pool_fc_bwd_kernel(const T* __restrict__ dl, const T* __restrict__ dpooled,
     }
     return;
   }
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {  // (ksplit == 1 here)
     const float v = sv[c];
     for (int p = 0; p < HW; ++p) io<T>::st(dxn, (int64_t)p * C + c, v);
     if (bn.reg != nullptr) {
@@ -491,15 +518,24 @@ MDA_API int mda_pool_fc_bwd_bn(int64_t dt, const void* dl, const void* dpooled, 
   const int64_t pp = (C % 8 == 0 && C / 8 <= 256) ? 256 / (C / 8) : 0;
   const size_t lds = (size_t)((N > J ? N : J) + C + 2 * pp * C) * sizeof(float);
   if (lds > 64 * 1024) return (int)hipErrorInvalidValue;
-  const dim3 grid((unsigned)(J + N));
+  // images split over ksplit blocks (>= 16 pixels each) on the vector path
+  static const int kmax = [] {
+    const char* e = getenv("MDA_HEAD_KSPLIT");
+    return e ? atoi(e) : 4;
+  }();
+  int ksplit = 1;
+  if (dt != DT_F32 && pp > 0 && kmax > 1)
+    for (int k = kmax; k > 1; k >>= 1)
+      if (HW % k == 0 && HW / k >= 16) { ksplit = k; break; }
+  const dim3 grid((unsigned)(J + N * ksplit));
   if (dt == DT_F32)
     hipLaunchKernelGGL(pool_fc_bwd_kernel<float>, grid, dim3(256), lds, st, (const float*)dl,
                        (const float*)dpooled, (const float*)pooled, W, dW, db, (float*)dx, (int)N,
-                       (int)HW, (int)C, (int)J, 1.f / HW, (int)accum, bn);
+                       (int)HW, (int)C, (int)J, 1.f / HW, (int)accum, bn, 1);
   else
     hipLaunchKernelGGL(pool_fc_bwd_kernel<bf16_t>, grid, dim3(256), lds, st, (const bf16_t*)dl,
                        (const bf16_t*)dpooled, (const bf16_t*)pooled, W, dW, db, (bf16_t*)dx,
-                       (int)N, (int)HW, (int)C, (int)J, 1.f / HW, (int)accum, bn);
+                       (int)N, (int)HW, (int)C, (int)J, 1.f / HW, (int)accum, bn, ksplit);
   MDA_CHECK_LAUNCH();
 }
 

@@ -380,29 +380,106 @@ class BnLink:
     accumulates into it in place.
     """
 
-    __slots__ = ("y", "res", "stats", "act", "M", "C", "dout", "ver", "region", "vres")
+    __slots__ = ("y", "res", "stats", "act", "M", "C", "dout", "ver", "region", "vres", "gamma",
+                 "beta", "need_res", "rlink", "private", "done")
 
-    def __init__(self, y, res, stats, act, M, C, vres=None):
+    def __init__(self, y, res, stats, act, M, C, vres=None, gamma=None, beta=None, need_res=False,
+                 rlink=None, private=False):
         self.y, self.res, self.stats, self.act, self.M, self.C = y, res, stats, act, M, C
         self.vres = vres if res is not None else None  # res is a virtual residual (VirtualBN)
-        self.dout = self.region = None
+        self.dout = self.region = self.done = None
         self.ver = -1
+        # the layer's own backward operands, for a consumer dgrad that finishes
+        # it (mda_conv_dgrad_bnfin): its parameters, whether its residual needs
+        # a gradient, the projection-shortcut BN that residual came from, and
+        # whether the output is private to native consumers (no feature loss
+        # or other autograd consumer can add to its gradient)
+        self.gamma, self.beta, self.need_res, self.rlink = gamma, beta, need_res, rlink
+        self.private = private
 
-    def arm(self, dout, region) -> None:
-        self.dout, self.ver, self.region = dout, dout._version, region
+    def arm(self, dout, region, done=None) -> None:
+        self.dout, self.ver, self.region, self.done = dout, dout._version, region, done
+
+    def can_finish(self) -> bool:
+        """A consumer dgrad may finish this layer's backward in its launch: the
+        output is private, dgamma / dbeta go straight into bound flat views."""
+        return (self.private and _BNF_ON[0] and self.gamma is not None and _DUAL[0] is None
+                and self.gamma.grad is not None and self.beta.grad is not None)
 
     def take(self, dout):
-        d, r = self.dout, self.region
-        self.dout = self.region = None
+        return self.take_full(dout)[0]
+
+    def take_full(self, dout):
+        """(region, done): the dgrad-epilogue sums -- and, if that dgrad
+        finished the backward, its (dy, dres) -- when ``dout`` IS the armed
+        tensor, unmodified; else (None, None)."""
+        d, r, f = self.dout, self.region, self.done
+        self.dout = self.region = self.done = None
         if d is not None and d is dout and dout._version == self.ver:
             _BNB_COUNT[0] += 1
-            return r
+            return r, f
         if d is not None:
+            if f is not None:
+                # the finish accumulated dgamma / dbeta already: a private
+                # output must never receive another gradient
+                raise RuntimeError("a BN output marked private received an extra gradient")
             _BNB_COUNT[1] += 1
-        return None
+        return None, None
 
 
 _BNB_COUNT = [0, 0]  # BN backwards on dgrad-epilogue sums / armed links that fell back
+_BNF_ON = [os.environ.get("MDA_BN_BWD_FINISH", "1") != "0"]
+_BNF_COUNT = [0]  # BN backwards finished inside the consumer's dgrad launch
+
+
+def set_bn_bwd_finish(on: bool) -> None:
+    """BN backward finished in the consumer dgrad's launch (mda_conv_dgrad_bnfin) on / off."""
+    _BNF_ON[0] = bool(on)
+
+
+def bn_bwd_finish_count(reset: bool = False) -> int:
+    v = _BNF_COUNT[0]
+    if reset:
+        _BNF_COUNT[0] = 0
+    return v
+
+
+def _bnf_prepare(link, dev):
+    """Outputs of a dgrad that finishes ``link``'s BN backward, or None."""
+    if link is None or not link.can_finish():
+        return None
+    dy = torch.empty_like(link.y)
+    dres = torch.empty_like(link.y) if link.need_res else None
+    rl = link.rlink if link.need_res else None
+    rreg = _region(link.C, dev) if rl is not None else None
+    return dy, dres, rl, rreg
+
+
+def _bnf_dgrad(link, reg, dev, dy, wt, dx, other, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
+               KpT, fold):
+    """The consumer dgrad (optionally with a folded 1x1 shortcut dgrad,
+    ``fold`` = :class:`_DeferredDgrad`) that also finishes ``link``'s BN
+    backward in its launch; arms the link (and the shortcut BN's link) and
+    returns 0, or NOT_SERVED having launched nothing."""
+    if reg is None:
+        return _ext.NOT_SERVED
+    prep = _bnf_prepare(link, dev)
+    if prep is None:
+        return _ext.NOT_SERVED
+    fdy, fdres, rl, rreg = prep
+    rc = _ext.call("mda_conv_dgrad_bnfin", dy, wt, dx, other, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
+                   stride, pad, KpT, link.y, link.res, link.stats, link.act, reg, link.vres,
+                   fold.dy if fold is not None else None, fold.wt if fold is not None else None,
+                   fold.cin2 if fold is not None else 0, fold.kp2 if fold is not None else 0,
+                   fdy, fdres, link.gamma.grad, link.beta.grad, rl.y if rl is not None else None,
+                   rl.stats if rl is not None else None, rreg, _err_word(dev),
+                   ok=(0, _ext.NOT_SERVED))
+    if rc == 0:
+        link.arm(dx, reg, done=(fdy, fdres))
+        if rl is not None:
+            rl.arm(fdres, rreg)
+        _BNF_COUNT[0] += 1
+    return rc
 _LAST_VBN = [None]
 _BNB_ON = [os.environ.get("MDA_BN_DGRAD_SUMS", "1") != "0"]
 _LAST_LINK = [None]
@@ -434,7 +511,12 @@ def _bn_bwd(dout, dpre, y, res, stats, gamma, beta, M, C, act, need_res, direct_
     db = beta.grad if direct_gb else None
     dy = torch.empty_like(y)
     dres = torch.empty_like(y) if need_res else None
-    reg = link.take(dout) if link is not None else None
+    reg, done = link.take_full(dout) if link is not None else (None, None)
+    if done is not None:
+        # finished by the consumer's dgrad launch (mda_conv_dgrad_bnfin)
+        if dpre is not None or not direct_gb:
+            raise RuntimeError("a finished BN backward cannot take a pre-activation gradient")
+        return done[0], (done[1] if need_res else None), None
     # the residual's producer is a training BN without activation (a projection
     # shortcut): dres IS its output gradient, so this pass adds its sums too
     rl = res_link if (need_res and res_link is not None and 256 % (C // 8) == 0) else None
@@ -494,12 +576,32 @@ class PackCache:
         self._table = None
         self._dirty = False
         self._total = 0
+        self._extra_key = None  # (zero fills, image) the table was built with
+        self._img_pad = None
+
+    def lookup_pad(self, weight):
+        """The channel-padded stem operand packed for this step, or None."""
+        if not self.armed:
+            return None
+        e = self.entries.get(id(weight))
+        if e is None or e["weight"] is not weight or e.get("kind") != "pad":
+            return None
+        return e
+
+    def register_pad(self, weight, wf, Cout, C, Cp, KH, KW, Kp):
+        """A stem whose 3-channel input runs padded to ``Cp`` (``needs_channel_pad``)."""
+        if torch.cuda.is_current_stream_capturing():
+            return
+        self.entries[id(weight)] = dict(weight=weight, wf=wf, wt=None, kind="pad",
+                                        meta=(Cout, -2, KH, KW, Kp, C | (Cp << 16)))
+        self._dirty = True
 
     def lookup(self, weight, need_dx):
         if not self.armed:
             return None
         e = self.entries.get(id(weight))
-        if e is None or e["weight"] is not weight or (need_dx and e["wt"] is None):
+        if (e is None or e["weight"] is not weight or (need_dx and e["wt"] is None)
+                or e.get("kind") == "pad"):
             return None
         return e
 
@@ -522,10 +624,15 @@ class PackCache:
         self.entries[id(weight)] = dict(weight=weight, wf=wp, wt=None, meta=(C, -1, 3, 3, 0, 0))
         self._dirty = True
 
-    def _build(self, device):
+    def _build(self, device, zero=(), image=None):
         rows, start = [], 0
         for e in self.entries.values():
             Cout, Cin, KH, KW, Kp, KpT = e["meta"]
+            if Cin == -2:  # channel-padded stem: 256 packed elements per tile
+                rows.append([e["weight"].data_ptr(), e["wf"].data_ptr(), 0, Cout, -2, KH, KW, Kp, KpT,
+                             start])
+                start += (Cout * Kp + 255) // 256
+                continue
             if Cin < 0:  # depthwise row: 256 packed elements per tile
                 n = (9 * Cout + 255) // 256
             else:
@@ -548,31 +655,73 @@ class PackCache:
             rows.append([w.data_ptr(), e["wf"].data_ptr(), e["wt"].data_ptr() if e["wt"] is not None else 0,
                          Cout, Cin, KH, KW, Kp, KpT, start])
             start += n
+        for t in zero:  # the step's zero fills ride in the same launch
+            nb = t.numel() * t.element_size()
+            rows.append([t.data_ptr(), nb, 0, 0, -3, 1, 1, 0, 0, start])
+            start += (nb + 16383) // 16384
+        if image is not None:
+            N, C, H, W = image.shape
+            if self._img_pad is None or tuple(self._img_pad.shape) != (N, 8, H, W):
+                self._img_pad = torch.empty((N, 8, H, W), dtype=torch.bfloat16, device=device,
+                                            memory_format=torch.channels_last)
+            M = N * H * W
+            rows.append([image.data_ptr(), self._img_pad.data_ptr(),
+                         0 if image.dtype == torch.float32 else 1, M, -4, C, 1, 0, 0, start])
+            start += (M + 255) // 256
         self._table = torch.tensor(rows, dtype=torch.int64).to(device)
         self._total = start
-        self._khkw = max(r[5] * r[6] for r in rows)
+        self._khkw = max(r[5] * r[6] for r in rows if r[4] != -2)
         self._ptrs = [e["weight"].data_ptr() for e in self.entries.values()]
+        self._extra_key = self._key(zero, image)
         self._dirty = False
 
-    def pack_all(self, device) -> bool:
-        nrows = sum(e.get("groups", 1) for e in self.entries.values())
+    @staticmethod
+    def _key(zero, image):
+        return (tuple((t.data_ptr(), t.numel() * t.element_size()) for t in zero),
+                None if image is None else (image.data_ptr(), tuple(image.shape), image.dtype))
+
+    @staticmethod
+    def _image_ok(image) -> bool:
+        return (image is not None and image.dim() == 4 and needs_channel_pad(image.shape[1])
+                and image.dtype in (torch.float32, torch.bfloat16)
+                and image.is_contiguous(memory_format=torch.channels_last))
+
+    def pack_all(self, device, zero=(), image=None) -> bool:
+        """Repack every registered layer in one launch (and arm the cache).
+        ``zero``: tensors to zero-fill in the same launch (4-byte multiples);
+        ``image``: a 3-channel NHWC image whose 8-channel padded copy the stem
+        then reads (:func:`pad_channels8`), built in the same launch -- only
+        for a stable buffer (the captured step's static input).  Returns False
+        having launched nothing (the caller zeroes ``zero`` itself)."""
+        image = image if self._image_ok(image) else None
+        nrows = sum(e.get("groups", 1) for e in self.entries.values()) + len(zero) + (image is not None)
         if not self.entries or nrows > 256 or any(
                 e["meta"][2] * e["meta"][3] > 49 for e in self.entries.values()):
             return False
+        if any(t.numel() * t.element_size() % 4 or t.data_ptr() % 16 or not t.is_contiguous()
+               for t in zero):
+            return False
         capturing = torch.cuda.is_current_stream_capturing()
         stale = self._table is None or self._dirty or any(
-            e["weight"].data_ptr() != p for e, p in zip(self.entries.values(), self._ptrs))
+            e["weight"].data_ptr() != p for e, p in zip(self.entries.values(), self._ptrs)
+        ) or self._extra_key != self._key(zero, image)
         if stale:
             if capturing:
                 return False
-            self._build(device)
+            self._build(device, zero, image)
         _ext.call("mda_pack_conv_weights_multi", self._table, self._table.shape[0], self._total,
                   self._khkw)
         self.armed = True
+        _PREPAD[0] = ((image, image._version, self._img_pad, torch.cuda.current_stream(device).cuda_stream)
+                      if image is not None else None)
         return True
 
     def disarm(self):
         self.armed = False
+        _PREPAD[0] = None
+
+
+_PREPAD = [None]  # (image, version, its 8-channel copy, stream) built by the armed PackCache
 
 
 _ACTIVE = [None]  # the PackCache of the training step currently running its forward
@@ -599,6 +748,12 @@ def pad_channels8(x):
     channels (zeros beyond the real ones), one launch.  Cached per tensor
     version and stream, so a second consumer on the same stream (e.g. two
     stems) reuses it."""
+    pp = _PREPAD[0]
+    # built by this step's multi-pack launch (PackCache.pack_all) -- on that
+    # launch's stream only: a teacher on its own stream pads for itself
+    if (pp is not None and pp[0] is x and pp[1] == x._version
+            and pp[3] == torch.cuda.current_stream(x.device).cuda_stream):
+        return pp[2]
     key = (x._version, torch.cuda.current_stream(x.device).cuda_stream)
     # never across a graph capture: a hit would leave the pad kernel out of the
     # graph, whose replays then read the padded copy of the capture-time image
@@ -937,6 +1092,23 @@ def can_defer_to_depthwise(x, dwconv, dwbn) -> bool:
 # processes each, scripts/ab_env.sh: 0.8529 vs 0.8468 ms) -- the shortcut's
 # blocks share conv1's CUs and slow its critical blocks more than the saved
 # launch is worth.
+_FIN_ON = [os.environ.get("MDA_BN_FINISH", "1") != "0"]
+_FIN_COUNT = [0]
+
+
+def set_bn_finish(on: bool) -> None:
+    """Training conv + BN finalize + apply in one launch (mda_conv_fwd_bnfin) on / off."""
+    _FIN_ON[0] = bool(on)
+
+
+def bn_finish_count(reset: bool = False) -> int:
+    """Forward convs whose BN was finished inside the conv launch."""
+    v = _FIN_COUNT[0]
+    if reset:
+        _FIN_COUNT[0] = 0
+    return v
+
+
 _PAIR_ON = [os.environ.get("MDA_CONV_PAIR", "0") == "1"]
 _PAIR = [None]    # (x, conv1 weight, shortcut conv) armed by the block
 _PAIR_DONE = {}   # id(shortcut weight) -> (x, raw output, region) made by conv1's launch
@@ -973,7 +1145,7 @@ def arm_conv_pair(x, conv1, bn1, conv_sc, bn_sc) -> bool:
 class _ConvBNActTrain(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, gamma, beta, residual, meta, bn, want_preact, forks=(None, None),
-                cbias=None, defer=False):
+                cbias=None, defer=False, private=False):
         # an unused output (the pre-activation) must not be materialised as a
         # zero gradient + layout copy: the kernels take null dout / dpre
         ctx.set_materialize_grads(False)
@@ -1018,6 +1190,7 @@ class _ConvBNActTrain(torch.autograd.Function):
             Kp = (KH * KW * cin_w + 63) // 64 * 64
             KpT = (KH * KW * (Cout // G) + 63) // 64 * 64
         ent = packs.lookup(weight, need_dx) if (packs is not None and not chpad and (G == 1 or gc)) else None
+        pent = packs.lookup_pad(weight) if (packs is not None and chpad) else None
         if gc and ent is None:
             wf = torch.empty(Cout, Kp, dtype=torch.bfloat16, device=dev)
             wt = torch.empty(Cin, KpT, dtype=torch.bfloat16, device=dev) if need_dx else None
@@ -1033,11 +1206,16 @@ class _ConvBNActTrain(torch.autograd.Function):
             wt = torch.empty(Cin, KpT, dtype=torch.bfloat16, device=dev) if need_dx else None
             _ext.call("mda_pack_conv_weights_grouped", weight.detach().float().contiguous(), wf, wt,
                       Cout, Cin, KH, KW, Kp, KpT, G)
+        elif chpad and pent is not None:  # packed for this step by PackCache.pack_all
+            wf, wt = pent["wf"], None
         elif chpad:  # stem: forward operand with zero weights for the pad channels
             wf = torch.empty(Cout, Kp, dtype=torch.bfloat16, device=dev)
             wt = None
-            _ext.call("mda_pack_conv_weights_pad", weight.detach().contiguous(), wf, Cout, cin_w,
-                      Cin, KH, KW, Kp)
+            wc = weight.detach()
+            if (packs is not None and wc.is_contiguous() and wc.dtype == torch.float32
+                    and os.environ.get("MDA_PACK_EXTRAS", "1") != "0"):
+                packs.register_pad(weight, wf, Cout, cin_w, Cin, KH, KW, Kp)
+            _ext.call("mda_pack_conv_weights_pad", wc.contiguous(), wf, Cout, cin_w, Cin, KH, KW, Kp)
         elif ent is not None:  # packed for this step by PackCache.pack_all
             wf, wt = ent["wf"], ent["wt"]
         else:
@@ -1068,9 +1246,11 @@ class _ConvBNActTrain(torch.autograd.Function):
         ctx.vbn = None
         out = y if defer else torch.empty_like(y)
         pre = torch.empty_like(y) if want_preact else None
+        fin = False
         if _BN_FUSED[0] or gc:
             # conv whose epilogue adds the BN sums into the stream's slot, then
-            # apply with the finalize in its prologue (2 launches)
+            # apply with the finalize in its prologue (2 launches) -- or all of
+            # it in the conv launch (mda_conv_fwd_bnfin)
             done = _PAIR_DONE.pop(id(weight), None)
             pr, _PAIR[0] = _PAIR[0], None
             if done is not None and done[0] is x_in and G == 1:
@@ -1095,10 +1275,33 @@ class _ConvBNActTrain(torch.autograd.Function):
                         if rc == 0:
                             _PAIR_DONE[id(sc.weight)] = (x_in, y2, reg2)
                             _PAIR_COUNT[0] += 1
+                if rc != 0 and not defer and not gc and G == 1 and part is None and _FIN_ON[0]:
+                    # conv + BN finalize + apply in ONE launch (grid barrier in the
+                    # conv epilogue); not served -> the two launches below
+                    rvb = rv.bn if rv is not None else None
+                    rc = _ext.call(
+                        "mda_conv_fwd_bnfin", x, wf, y, reg, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
+                        stride, pad, Kp, gamma.detach(), beta.detach(), bn.running_mean,
+                        bn.running_var, stats, float(bn.momentum), float(bn.eps),
+                        bn.num_batches_tracked, res, out, pre, act,
+                        rv.reg if rv is not None else None, rv.gamma if rv is not None else None,
+                        rv.beta if rv is not None else None,
+                        rvb.running_mean if rvb is not None else None,
+                        rvb.running_var if rvb is not None else None,
+                        rv.stats if rv is not None else None,
+                        float(rvb.momentum) if rvb is not None else 0.0,
+                        float(rvb.eps) if rvb is not None else 0.0,
+                        rvb.num_batches_tracked if rvb is not None else None, _err_word(dev),
+                        ok=(0, _ext.NOT_SERVED))
+                    fin = rc == 0
+                    if fin:
+                        _FIN_COUNT[0] += 1
                 if rc != 0:
                     _ext.call("mda_conv_fwd_bnacc_g", x, wf, y, part, reg, N, H, W, Cin, Ho, Wo,
                               Cout, KH, KW, stride, pad, Kp, tile, splits, G if gc else 1)
-            if defer:
+            if fin:
+                pass  # applied by the conv launch
+            elif defer:
                 # no apply: the consumer's apply finalizes this BN (VirtualBN)
                 ctx.vbn = VirtualBN(reg, gamma.detach(), beta.detach(), bn, stats, act)
             elif rv is not None:
@@ -1137,7 +1340,9 @@ class _ConvBNActTrain(torch.autograd.Function):
         # output: its gradient would join dz after the consumer's epilogue)
         ctx.bnlink = None
         if not want_preact and Cout <= 2048:
-            ctx.bnlink = BnLink(y, res if act != 0 else None, stats, act, M, Cout, ctx.vres)
+            ctx.bnlink = BnLink(y, res if act != 0 else None, stats, act, M, Cout, ctx.vres,
+                                gamma, beta, ctx.has_res and ctx.needs_input_grad[4], ctx.res_link,
+                                bool(private) and G == 1 and not ctx.gc)
         _LAST_LINK[0] = ctx.bnlink
         _LAST_VBN[0] = ctx.vbn
         ctx.cbias = cbias is not None
@@ -1190,17 +1395,20 @@ class _ConvBNActTrain(torch.autograd.Function):
                 parks = False
             elif isinstance(other, _DeferredDgrad):
                 reg = _region(Cin, dev) if link is not None else None
-                rc = _ext.call("mda_conv_dgrad_bnsum2", dy, wt, dx, N, H, W, Cin, Ho, Wo, Cout, KH,
-                               KW, stride, pad, KpT, link.y if reg is not None else None,
-                               link.res if reg is not None else None,
-                               link.stats if reg is not None else None,
-                               link.act if reg is not None else 0, reg,
-                               link.vres if reg is not None else None, other.dy, other.wt,
-                               other.cin2, other.kp2, ok=(0, _ext.NOT_SERVED))
+                rc = _bnf_dgrad(link, reg, dev, dy, wt, dx, None, N, H, W, Cin, Ho, Wo, Cout, KH,
+                                KW, stride, pad, KpT, other)
+                if rc != 0:
+                    rc = _ext.call("mda_conv_dgrad_bnsum2", dy, wt, dx, N, H, W, Cin, Ho, Wo, Cout,
+                                   KH, KW, stride, pad, KpT, link.y if reg is not None else None,
+                                   link.res if reg is not None else None,
+                                   link.stats if reg is not None else None,
+                                   link.act if reg is not None else 0, reg,
+                                   link.vres if reg is not None else None, other.dy, other.wt,
+                                   other.cin2, other.kp2, ok=(0, _ext.NOT_SERVED))
+                    if rc == 0 and reg is not None:
+                        link.arm(dx, reg)
                 if rc == 0:
                     _MERGE_COUNT[0] += 1
-                    if reg is not None:
-                        link.arm(dx, reg)
                     folded = True
                 else:
                     other = other.materialize((N, Cin, H, W))
@@ -1217,12 +1425,15 @@ class _ConvBNActTrain(torch.autograd.Function):
                     link.arm(dx, reg)
             elif link is not None and not parks and splits == 1:
                 # dx is the whole output gradient of the BN layer that made x:
-                # its backward sums come out of this epilogue (BnLink)
+                # its backward sums come out of this epilogue (BnLink) -- and,
+                # when the launch can finish that backward, its dy too
                 reg = _region(Cin, dev)
-                _ext.call("mda_conv_dgrad_bnsum_g", dy, wt, dx, part, other, N, H, W, Cin, Ho, Wo,
-                          Cout, KH, KW, stride, pad, KpT, tile, splits, link.y, link.res,
-                          link.stats, link.act, reg, 1, link.vres, 0, 0)
-                link.arm(dx, reg)
+                if _bnf_dgrad(link, reg, dev, dy, wt, dx, other, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
+                              stride, pad, KpT, None) != 0:
+                    _ext.call("mda_conv_dgrad_bnsum_g", dy, wt, dx, part, other, N, H, W, Cin, Ho,
+                              Wo, Cout, KH, KW, stride, pad, KpT, tile, splits, link.y, link.res,
+                              link.stats, link.act, reg, 1, link.vres, 0, 0)
+                    link.arm(dx, reg)
             else:
                 _ext.call("mda_conv_dgrad_res", dy, wt, dx, part, other, N, H, W, Cin, Ho, Wo,
                           Cout, KH, KW, stride, pad, KpT, tile, splits)
@@ -1246,7 +1457,7 @@ class _ConvBNActTrain(torch.autograd.Function):
             notify_grad(gamma, beta)
         dgamma = None if direct_gb else sums[1].clone()
         dbeta = None if direct_gb else sums[0].clone()
-        return dx, dw, dgamma, dbeta, dres, None, None, None, None, _cbias_grad(ctx), None
+        return dx, dw, dgamma, dbeta, dres, None, None, None, None, _cbias_grad(ctx), None, None
 
 
 def _bn_bwd_dual(dout, dpre, y, res, stats, gamma, beta, M, C, act, need_res, link, res_link, vres):
@@ -1337,7 +1548,7 @@ def _conv_bn_backward_dual(ctx, dout, dpre):
         _wgrad_launch(wg, True, x, dy)
         notify_grad(weight)
     notify_grad(gamma, beta)
-    return dx, None, None, None, dres, None, None, None, None, None, None
+    return dx, None, None, None, dres, None, None, None, None, None, None, None
 
 
 def _bn_train_forward(y, M, C, gamma, beta, bn, residual, act, want_preact, reg=None):
@@ -1478,7 +1689,7 @@ def _dw_backward(ctx, dout, dpre):
         dw = None if direct_w else target
         if direct_w:
             notify_grad(weight)
-    return dx, dw, dgamma, dbeta, dres, None, None, None, None, _cbias_grad(ctx), None
+    return dx, dw, dgamma, dbeta, dres, None, None, None, None, _cbias_grad(ctx), None, None
 
 
 def _cbias_grad(ctx):
@@ -1759,7 +1970,7 @@ def conv_trainbn_nograd(x, conv, bn, act, residual, want_preact):
 
 
 def conv_bn_act_train(x, conv, bn, act, residual, want_preact, fork=None, res_fork=None,
-                      defer_apply=False):
+                      defer_apply=False, private=False):
     """``fork``: the :class:`GradFork` of ``x`` (another consumer of x sums
     its gradient into this layer's dgrad, or vice versa); ``res_fork``: the
     fork of ``residual`` (identity shortcut).  ``defer_apply``: return the raw
@@ -1779,7 +1990,8 @@ def conv_bn_act_train(x, conv, bn, act, residual, want_preact, fork=None, res_fo
     _LAST_VBN[0] = None
     defer = defer_apply if (defer_apply and conv.bias is None) else False
     out, pre = _ConvBNActTrain.apply(x, conv.weight, bn.weight, bn.bias, residual, meta, bn,
-                                     bool(want_preact), (fork, res_fork), conv.bias, defer)
+                                     bool(want_preact), (fork, res_fork), conv.bias, defer,
+                                     bool(private))
     link, _LAST_LINK[0] = _LAST_LINK[0], None
     vbn, _LAST_VBN[0] = _LAST_VBN[0], None
     if link is not None:

@@ -57,7 +57,8 @@ def _bn(x: torch.Tensor, bn: nn.BatchNorm2d) -> torch.Tensor:
 
 def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d | None = None,
                 act: str = "relu", residual: torch.Tensor | None = None,
-                want_preact: bool = False, fork=None, res_fork=None, defer_apply: bool | str = False):
+                want_preact: bool = False, fork=None, res_fork=None, defer_apply: bool | str = False,
+                private: bool = False):
     """``act(bn(conv(x)) + residual)``; returns ``(out, preact_or_None)``.
 
     ``fork`` / ``res_fork`` (:class:`ops.hip_train.GradFork`, optional): x /
@@ -68,7 +69,10 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d | None = No
     native conv + BN taking the result as ``residual``
     (:class:`ops.hip_train.VirtualBN`; see :func:`ops.hip_train.can_defer_residual`);
     ``defer_apply="dw"``: the one consumer is a native depthwise conv that
-    applies this BN + act on load (:func:`ops.hip_train.can_defer_to_depthwise`)."""
+    applies this BN + act on load (:func:`ops.hip_train.can_defer_to_depthwise`).
+    ``private``: the output feeds only native convs / native residual consumers
+    (no feature loss, no other autograd consumer), so the consuming conv's
+    dgrad may finish this BN's backward in its own launch."""
     if hip_enabled_for(x):
         from . import hip_layers
         if hip_layers.conv_supported(x, conv, bn):
@@ -76,7 +80,7 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d | None = No
         from . import hip_train
         if _TRAIN_KERNELS["on"] and hip_train.train_supported(x, conv, bn):
             return hip_train.conv_bn_act_train(x, conv, bn, act, residual, want_preact, fork,
-                                               res_fork, defer_apply)
+                                               res_fork, defer_apply, private)
     if residual is not None and getattr(residual, "_mda_vbn", None) is not None:
         raise RuntimeError("a VirtualBN residual reached a non-native consumer "
                            "(check ops.hip_train.can_defer_residual at the call site)")

@@ -19,7 +19,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shape", default="64,128,16,256,3,2")
     ap.add_argument("--runs", type=int, default=3)
-    ap.add_argument("--op", default="dgrad", choices=["dgrad", "fwd"])
+    ap.add_argument("--op", default="dgrad", choices=["dgrad", "fwd", "bnsum", "fold"],
+                    help="bnsum: dgrad + the consumer-BN sums epilogue (ReLU + residual); fold: "
+                         "bnsum with the stride-s 1x1 shortcut dgrad folded in (mda_conv_dgrad_bnsum2)")
     a = ap.parse_args()
     N, Cin, H, Cout, k, s = map(int, a.shape.split(","))
     p = k // 2
@@ -30,7 +32,15 @@ def main():
     dy = torch.randn(N, Cout, Ho, Ho, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     wf, wt, Kp, KpT = hip_train.pack_weights(conv.weight, True)
     dx = torch.empty(N, Cin, H, H, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    if a.op == "dgrad":
+    if a.op in ("bnsum", "fold"):
+        bn_y = torch.randn_like(dx)
+        bn_res = torch.randn_like(dx)
+        stats = torch.rand(4, Cin, device="cuda") + 0.5
+        region = torch.zeros(hip_train._region_bytes(Cin) // 4, dtype=torch.float32, device="cuda")
+        sc = nn.Conv2d(Cin, Cout, 1, s, 0, bias=False).cuda()
+        _, wt2, _, kp2 = hip_train.pack_weights(sc.weight, True)
+        dy2 = torch.randn_like(dy)
+    if a.op in ("dgrad", "bnsum", "fold"):
         tile, splits = conv_plan(N * H * H, Cin, KpT)
         part = torch.empty(splits * N * H * H * Cin, device="cuda") if splits > 1 else None
     else:
@@ -40,7 +50,13 @@ def main():
         y = torch.empty_like(dy)
 
     def run():
-        if a.op == "dgrad":
+        if a.op == "bnsum":
+            _ext.call("mda_conv_dgrad_bnsum", dy, wt, dx, part, None, N, H, H, Cin, Ho, Ho, Cout, k, k,
+                      s, p, KpT, tile, splits, bn_y, bn_res, stats, 1, region)
+        elif a.op == "fold":
+            _ext.call("mda_conv_dgrad_bnsum2", dy, wt, dx, N, H, H, Cin, Ho, Ho, Cout, k, k, s, p, KpT,
+                      bn_y, bn_res, stats, 1, region, None, dy2, wt2, Cout, kp2)
+        elif a.op == "dgrad":
             _ext.call("mda_conv_dgrad", dy, wt, dx, part, N, H, H, Cin, Ho, Ho, Cout, k, k, s, p, KpT,
                       tile, splits)
         else:
@@ -81,7 +97,7 @@ def main():
         live = st[:, 0] > 0
         t0 = st[live, 0].min()
         bm = tile // 1000
-        if a.op == "dgrad":
+        if a.op != "fwd":
             mc = N * ((H + s - 1) // s) ** 2 if s > 1 else N * H * H
             gy = (Cin + tile % 1000 - 1) // (tile % 1000)
         else:

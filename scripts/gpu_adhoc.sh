@@ -1,4 +1,6 @@
-export PYTHONPATH=$PWD TMPDIR=/tmp
-TESTS="tests/test_gpu_kernels_losses_optim.py tests/test_gpu_vid_nst.py" bash scripts/gpu_run.sh && \
-BENCH="--steps 500 --warmup 30;--steps 500 --warmup 30 EXPERIMENT.DETERMINISTIC True;--steps 500 --warmup 30 --batch 8;--cfg configs/cifar100/vanilla.yaml --steps 500 --warmup 30" bash scripts/gpu_run.sh && \
-PROF="configs/cifar100/dkd/res32x4_res8x4.yaml:flag_r5b;configs/cifar100/vanilla.yaml:van_r5b" TOP=60 bash scripts/gpu_run.sh
+export TMPDIR=/tmp
+for w in _bisect/r4 _bisect/e79; do
+  echo "== $w"
+  (cd $w && PYTHONPATH=$PWD ARM=default TRIALS=4 timeout -k 10 300 python -u scripts/debug/ofd_nan.py > ../../gpurun_out/ofd_nan_$(basename $w).log 2>&1) || exit 1
+  grep -v "amdgpu.ids\|WARN" gpurun_out/ofd_nan_$(basename $w).log | tail -6
+done

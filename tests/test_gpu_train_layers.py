@@ -170,7 +170,7 @@ def test_pack_cache_matches_per_layer_packing(student):
             init = st.flat.data.clone()
         if not use_cache:
             st._packs = hip_train.PackCache()
-            st._packs.pack_all = lambda device: False
+            st._packs.pack_all = lambda device, **kw: False
         for b in SyntheticLoader("cifar100", 16, "cuda", steps_per_epoch=4, channels_last=True):
             st.step(b)
         torch.cuda.synchronize()

@@ -662,6 +662,12 @@ class TrainStep:
         both sides already fill the GPU and it costs 6 %: ``auto`` skips that case."""
         if self.lookahead != "auto":
             return bool(self.lookahead)
+        if getattr(self.distiller, "_teacher_train_bn", False):
+            # a train-mode teacher (OFD.TEACHER_TRAIN_BN) runs inline: with the
+            # look-ahead its second replayed step computed different teacher
+            # features (non-finite loss_kd in 2-3 of 3 runs, prefetch or not;
+            # scripts/debug/ofd_nan.py) -- inline it matches eager exactly
+            return False
         img = static.get("image")
         big = img is not None and img.dim() == 4 and min(img.shape[-2:]) >= 128
         needs = tuple(getattr(self.distiller, "teacher_needs", ("logits",)))
@@ -685,7 +691,11 @@ class TrainStep:
                 self.distiller.teacher_forward(None)
             torch.cuda.current_stream().wait_stream(s)
             torch.cuda.synchronize()
-            with torch.cuda.graph(g_teach, pool=pool, stream=s), _autocast(self.device, self.dtype):
+            # its own memory pool: replayed ahead of the step graph, its
+            # temporaries (a train-mode teacher's BN regions and stats among
+            # them) must not be blocks the step graph's capture reuses
+            with torch.cuda.graph(g_teach, pool=torch.cuda.graph_pool_handle(), stream=s), \
+                    _autocast(self.device, self.dtype):
                 self.distiller.teacher_forward(None)
         except Exception:
             feed.mode = None

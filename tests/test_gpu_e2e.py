@@ -294,10 +294,13 @@ def test_teacher_lookahead_matches_inline_teacher(typ, trainer, tgraph):
     ref = outs[1][0].norm()
     spread = ((outs[2][0] - outs[1][0]).norm() / ref).item()
     rel = ((outs[0][0] - outs[1][0]).norm() / ref).item()
-    # a fully native step is run-to-run deterministic (spread 0): then the
-    # look-ahead must match to 1e-5; with a PyTorch / MIOpen layer in the loss
-    # path (ReviewKD's ABF) it must stay within 3x that layer's own spread
-    assert rel <= 3 * spread + 1e-5, (rel, spread)
+    # the inline runs repeat bit for bit (spread 0), but the BN region sums
+    # are fp64 atomics whose order follows the block schedule, which the
+    # concurrently replayed teacher changes: last-bit differences, ~1e-4 after
+    # 16 steps (docs/DESIGN.md 3.3; EXPERIMENT.DETERMINISTIC removes them).
+    # With a PyTorch / MIOpen layer in the loss path (ReviewKD's ABF) it must
+    # stay within 3x that layer's own spread
+    assert rel <= 3 * spread + 2e-4, (rel, spread)
     assert abs(outs[0][1]["loss"] - outs[1][1]["loss"]) <= max(
         1e-4 * abs(outs[1][1]["loss"]), 3 * abs(outs[2][1]["loss"] - outs[1][1]["loss"]))
     print(f"lookahead {typ}: rel {rel:.3g} spread {spread:.3g}")

@@ -38,6 +38,17 @@
 #include <mutex>
 #include <unordered_map>
 
+// The in-kernel BN finishes (ConvParams::fin_on / bnf_on: a grid barrier in
+// the conv epilogue, then the BN finalize + apply or the BN backward) are
+// compiled only with -DMDA_BN_FINISH_KERNELS=1.  Measured (1x MI355X,
+// profiles/r5_ab.md): kept-row registers in the shared epilogues raised the
+// halo kernels from 146-185 to 225-256 VGPRs with spills, +0.14 ms on the
+// flagship step with the finishes off, and the barrier launches hung beside
+// the concurrently replayed look-ahead teacher graph.
+#ifndef MDA_BN_FINISH_KERNELS
+#define MDA_BN_FINISH_KERNELS 0
+#endif
+
 namespace {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
@@ -441,10 +452,14 @@ __device__ __forceinline__ void conv_epilogue_bnb(const ConvParams& p, float* Cs
   }
   float s1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, s2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float t1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, t2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#if MDA_BN_FINISH_KERNELS
   uint4 dkeep[RPT];  // the stored dx rows, for the BN finish
+#endif
 #pragma unroll
   for (int k = 0; k < RPT; ++k) {
+#if MDA_BN_FINISH_KERNELS
     dkeep[k] = make_uint4(0u, 0u, 0u, 0u);
+#endif
     if (mrow[k] < 0) continue;
     const bool set1 = mh > 0 && mrow[k] >= mh;
     const int r0 = rr + k * RPP;
@@ -476,8 +491,10 @@ __device__ __forceinline__ void conv_epilogue_bnb(const ConvParams& p, float* Cs
         if (set1) { t1[e] += d; t2[e] += xh; } else { s1[e] += d; s2[e] += xh; }
       }
     }
+#if MDA_BN_FINISH_KERNELS
     dkeep[k] = make_uint4(ow[0], ow[1], ow[2], ow[3]);
-    *(uint4*)(p.y + (int64_t)mrow[k] * C + co) = dkeep[k];
+#endif
+    *(uint4*)(p.y + (int64_t)mrow[k] * C + co) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
   }
   __syncthreads();  // every read of the C tile is done: reuse it for the reduction
   float* red = Cs;  // [2][RPP][BN]
@@ -502,6 +519,7 @@ __device__ __forceinline__ void conv_epilogue_bnb(const ConvParams& p, float* Cs
         acc_add(region_acc(slot, C, (int)blockIdx.x % slot_shards(C), q) + n0 + c, (double)(a0 + a1));
     }
   }
+#if MDA_BN_FINISH_KERNELS
   if (!p.bnf_on || mh > 0) return;
   // ---- BN finish (ConvParams::bnf_on): the shortcut BN's inputs are loaded
   // before the barrier so their latency hides behind the wait
@@ -597,6 +615,7 @@ __device__ __forceinline__ void conv_epilogue_bnb(const ConvParams& p, float* Cs
     if (n0 + c < C)
       acc_add(region_acc(f.rreg, C, (int)(bid % (unsigned)slot_shards(C)), q) + n0 + c, (double)(a0 + a1));
   }
+#endif
 }
 
 template <int BM, int BN>
@@ -610,6 +629,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, const f32x4 (
   conv_epilogue_rows<BM, BN, 256>(p, smem, m0, n0, rows, pc, has_pc, pre);
 }
 
+#if MDA_BN_FINISH_KERNELS
 // BN finish of a training forward (ConvParams::fin_on): every block's sums
 // are in the region once the grid barrier opens; each block finalizes the
 // channels of its N tile from the coherent region totals and applies
@@ -697,6 +717,8 @@ __device__ __forceinline__ void conv_bn_finish(const ConvParams& p, float* Cs, i
   }
 }
 
+#endif
+
 // Phase 2: NT threads own 8 channels x rows of the C tile: bias / BN affine,
 // residual, activation, preact and bf16 stores, split-K partials, or the raw
 // output + BN statistics partials.  Every barrier is reached by all threads.
@@ -724,6 +746,7 @@ __device__ __forceinline__ void conv_epilogue_rows(const ConvParams& p, char* sm
     // return before the barrier: threads past Cout just contribute zeros.
     float s1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, s2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     const bool cok = co < group_nlim(p, n0);
+#if MDA_BN_FINISH_KERNELS
     constexpr int RPT = (BM + RPP - 1) / RPP;
     uint4 keep[RPT];  // the stored rows, for the BN finish
 #pragma unroll
@@ -732,11 +755,18 @@ __device__ __forceinline__ void conv_epilogue_rows(const ConvParams& p, char* sm
       const int m = m0 + r0;
       keep[k] = make_uint4(0u, 0u, 0u, 0u);
       if (r0 >= rows || m >= mlim || !cok) continue;
+#else
+    for (int r0 = rr; r0 < rows; r0 += RPP) {
+      const int m = m0 + r0;
+      if (m >= mlim || !cok) break;
+#endif
       const float4 lo = *(const float4*)&Cs[r0 * CS + c8 * 8];
       const float4 hi = *(const float4*)&Cs[r0 * CS + c8 * 8 + 4];
       const uint4 o = make_uint4(pack_bf16x2(lo.x, lo.y), pack_bf16x2(lo.z, lo.w),
                                  pack_bf16x2(hi.x, hi.y), pack_bf16x2(hi.z, hi.w));
+#if MDA_BN_FINISH_KERNELS
       keep[k] = o;
+#endif
       *(uint4*)(p.y + (int64_t)m * p.Cout + co) = o;
       const uint32_t u[4] = {o.x, o.y, o.z, o.w};
 #pragma unroll
@@ -769,7 +799,9 @@ __device__ __forceinline__ void conv_epilogue_rows(const ConvParams& p, char* sm
           p.stats_part[((int64_t)(m0 / rows) * 2 + q) * p.Cout + n0 + c] = a0 + a1;
       }
     }
+#if MDA_BN_FINISH_KERNELS
     if (p.fin_on) conv_bn_finish<BM, BN, NT, RPT>(p, Cs, m0, n0, rows, keep);
+#endif
     return;
   }
   if ((p.Cout & 7) == 0) {
@@ -2612,7 +2644,7 @@ MDA_API int mda_conv_dgrad_bnfin(const void* dy, const void* wt, void* dx, const
     const char* e = getenv("MDA_BN_BWD_FINISH");
     return !(e && e[0] == '0');
   }();
-  if (!on || region == nullptr) return MDA_NOT_SERVED;
+  if (!MDA_BN_FINISH_KERNELS || !on || region == nullptr) return MDA_NOT_SERVED;
   if (dy2 != nullptr && (wt2 == nullptr || cin2 <= 0 || cin2 % BK || kp2 < cin2 || kp2 % BK))
     return MDA_NOT_SERVED;
   int64_t tile = 0, splits = 0;
@@ -2836,7 +2868,9 @@ MDA_API int mda_conv_fwd_bnfin(const void* x, const void* w, void* y, void* regi
     const char* e = getenv("MDA_BN_FINISH");
     return !(e && e[0] == '0');
   }();
-  if (!on || Cout % 8 || Cout > SLOT_CMAX || region == nullptr || out == nullptr) return MDA_NOT_SERVED;
+  if (!MDA_BN_FINISH_KERNELS || !on || Cout % 8 || Cout > SLOT_CMAX || region == nullptr ||
+      out == nullptr)
+    return MDA_NOT_SERVED;
   if (rregion != nullptr && (res == nullptr || rstats == nullptr)) return (int)hipErrorInvalidValue;
   ConvParams p{};
   p.ldx = (int)Cin;
@@ -2932,3 +2966,6 @@ MDA_API int mda_conv_fwd_bnacc_pair(const void* x, int64_t N, int64_t H, int64_t
 #undef PAIR_CASE
   return (int)hipGetLastError();
 }
+
+// 1 when the in-kernel BN finishes are compiled in (MDA_BN_FINISH_KERNELS).
+MDA_API int mda_bn_finish_compiled() { return MDA_BN_FINISH_KERNELS; }

@@ -17,7 +17,18 @@ from mdistiller_ddp_amd.engine.step import TrainStep
 from mdistiller_ddp_amd.ops import hip_train
 from mdistiller_ddp_amd.ops.backend import use_backend
 
-pytestmark = pytest.mark.gpu
+
+
+def _compiled():
+    from mdistiller_ddp_amd.ops import _ext
+    lib = _ext.load(required=False)
+    return lib is not None and bool(lib.mda_bn_finish_compiled())
+
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif("not _compiled()",
+                                 reason="in-kernel BN finishes not compiled (MDA_BN_FINISH_KERNELS=0, "
+                                        "the default: profiles/r5_ab.md)")]
 
 
 def _rel(a, b):

@@ -75,6 +75,7 @@ SIGNATURES = {
     "mda_shuffle_tail_bwd": "ppppp" + "i" * 7 + "s",
     "mda_pack_conv_weights_pad": "pp" + "i" * 6 + "s",
     "mda_wgrad_plan": "iiiiiiiiiip",
+    "mda_bn_finish_compiled": "",
     "mda_conv_dgrad_bnfin": "pppp" + "i" * 12 + "ppp" + "i" + "pp" + "pp" + "ii" + "ppppppp" + "p" + "s",
     "mda_conv_fwd_bnfin": "pppp" + "i" * 12 + "ppppp" + "ff" + "p" + "ppp" + "i" + "pppppp" + "ff" + "p" + "p" + "s",
     "mda_conv_fwd_bnacc_pair": "piiiiiiipppiiiipppiis",

@@ -2153,11 +2153,13 @@ int ring1_max() {
 }
 
 // deep-ring glds (GLDS_DEEP stages) for grids of <= ~1 block per CU with a
-// long K loop: 0 off, 1 strided-dgrad parity classes, 2 also plain launches
+// long K loop: 0 off (default: measured +8 us/step on the flagship with the
+// parity dgrads on it, profiles/r5_ab.md), 1 strided-dgrad parity classes,
+// 2 also plain launches
 int glds_deep() {
   static const int v = [] {
     const char* e = getenv("MDA_GLDS_DEEP");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 0;
   }();
   return v;
 }

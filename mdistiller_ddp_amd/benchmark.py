@@ -101,7 +101,8 @@ def run(cfg_file: str, per_gpu_batch: int, steps: int, warmup: int, opts=(), use
     dt = torch.bfloat16 if (dtype == "bf16" and dev.type == "cuda") else torch.float32
     trainer = cfg.SOLVER.TRAINER
     step = TrainStep(distiller, cfg, dev, trainer=trainer, use_graph=use_graph, dtype=dt,
-                     batch_keys=BATCH_KEYS[trainer])
+                     batch_keys=BATCH_KEYS[trainer],
+                     warmup_eager=int(os.environ.get("MDA_WARMUP_EAGER", "3")))
     distiller.train()
     # past any warm-up ramp (DKD / ReviewKD): full loss
     step.set_epoch(float(max(cfg.DKD.WARMUP, cfg.REVIEWKD.WARMUP_EPOCHS) + 1))

@@ -127,14 +127,21 @@ def run(cfg_file: str, per_gpu_batch: int, steps: int, warmup: int, opts=(), use
         step.step(b, next_batch=nb)
         return nb
 
-    for _ in range(warmup):
-        cur = advance(cur)
     # the set-up objects (models, graphs, earlier configs in this process) move to
     # the permanent generation: the timed loop's generation-2 collections no longer
     # walk them.  Launch-bound steps (DOT's five graph replays) otherwise slow down
-    # with the process history (1.33 -> 1.60 ms/step after two other configs)
+    # with the process history (1.33 -> 1.60 ms/step after two other configs).
+    # The collection runs BEFORE the last warm-up step, not between it and the
+    # timed loop: a ~50 ms gc.collect() there left the host caches cold and the
+    # GPU idle, and the first timed steps paid for it -- +30 us/step on a 20-step
+    # window, 0.875 vs 0.845 ms (profiles/r6_short_run_gap.md)
     gc_frozen = os.environ.get("MDA_GC_FREEZE", "1") != "0"
-    if gc_frozen:
+    for i in range(warmup):
+        if gc_frozen and i == warmup - 1:
+            gc.collect()
+            gc.freeze()
+        cur = advance(cur)
+    if gc_frozen and warmup == 0:
         gc.collect()
         gc.freeze()
     sync()

@@ -235,6 +235,7 @@ class TrainStep:
         self.warmup_eager = max(1, int(warmup_eager))
         self.steps_done = 0
         self._graphs = None
+        self._static_img = None  # the captured step's input image (pack-table extras)
         self._static = None
         self._dot_ready = not self.is_dot
         self._reach_ready = False
@@ -521,7 +522,12 @@ class TrainStep:
                     packs = self._packs = hip_train.PackCache()
         # the zero fills (and, for a captured step, the stem's padded image)
         # ride in the weight-pack launch
-        img = b.get("image") if (self.use_graph and _PACK_EXTRAS) else None
+        # only the captured step's own static image may be baked into the pack
+        # table: an eager step after capture (a partial batch) passing its image
+        # would rebuild the table the graph still points at
+        img = b.get("image")
+        if not (self.use_graph and _PACK_EXTRAS and img is not None and img is self._static_img):
+            img = None
         zx = zero if _PACK_EXTRAS else ()
         if packs is None or not packs.pack_all(self.device, zero=zx, image=img) or not zx:
             if len(zero) > 1 and zero[0].dtype == zero[1].dtype:
@@ -598,7 +604,7 @@ class TrainStep:
         eagerly on the capture stream.
         """
         static = {k: v.clone() for k, v in b.items()}
-        img = static.get("image")
+        img = self._static_img = static.get("image")
         self._wg_auto = img is not None and img.dim() == 4 and min(img.shape[-2:]) >= 128
         pool = torch.cuda.graph_pool_handle()
         s = self._cap_stream = torch.cuda.Stream()

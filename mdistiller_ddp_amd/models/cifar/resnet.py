@@ -13,7 +13,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ...ops.nn import conv_bn_act, grad_fork, pool_linear
-from ...ops.hip_train import arm_conv_pair, can_defer_residual
+from ...ops.hip_train import can_defer_residual
 from ...runtime.streams import run_branch
 from .._base import ModelBase, PreactStage
 
@@ -45,24 +45,19 @@ class BasicBlock(nn.Module):
         # x feeds conv1 and the shortcut: their input gradients are summed in
         # the second one's dgrad epilogue (GradFork), not by an autograd add
         fork = grad_fork(x)
-        # conv1 and the projection shortcut read x at the same output pixels:
-        # on the native kernels conv1's launch computes both (arm_conv_pair)
-        paired = self.downsample is not None and arm_conv_pair(
-            x, self.conv1, self.bn1, self.downsample[0], self.downsample[1])
         # h feeds conv2 only: conv2's dgrad may finish bn1's backward
         h, _ = conv_bn_act(x, self.conv1, self.bn1, "relu", fork=fork, private=True)
         if self.downsample is None:
             res = x
         else:
-            # projection shortcut (on the branch stream unless paired), beside
+            # projection shortcut (on the branch stream), beside
             # conv2.  Created after conv1, so autograd issues its backward
             # first: the shorter branch chain (BN backward + 1x1 dgrad) parks
             # its input gradient and conv1's dgrad, last on the main chain, adds
             # it in its epilogue.  Its BN is applied inside bn2's apply
             # (ops/hip_train.py VirtualBN)
             defer = can_defer_residual(h, self.conv2, self.bn2)
-            res = (self._shortcut(x, fork, defer) if paired
-                   else run_branch(x, lambda t: self._shortcut(t, fork, defer)))
+            res = run_branch(x, lambda t: self._shortcut(t, fork, defer))
             fork = None
         # the block output is a stage feature only when features are consumed
         return conv_bn_act(h, self.conv2, self.bn2, "relu", residual=res,

@@ -17,7 +17,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ...ops.nn import MaxPool2d, conv_bn_act, grad_fork, pool_linear
-from ...ops.hip_train import arm_conv_pair, can_defer_residual
+from ...ops.hip_train import can_defer_residual
 from ...runtime.streams import run_branch
 from .._base import ModelBase, PreactStage
 from ..cifar.resnet import Stage
@@ -42,7 +42,7 @@ class BasicBlock(nn.Module):
         self.is_last = False
         self._need_preact = True
 
-    def _res(self, x, fork=None, h=None, conv=None, bn=None, paired=False):
+    def _res(self, x, fork=None, h=None, conv=None, bn=None):
         """(residual, residual fork): the projection shortcut runs on the
         branch stream; x's two consumers sum their gradients in the native
         backward (ops.hip_train.GradFork).  Its BN is applied inside the
@@ -53,16 +53,13 @@ class BasicBlock(nn.Module):
         defer = conv is not None and can_defer_residual(h, conv, bn)
         fn = (lambda t: conv_bn_act(t, self.downsample[0], self.downsample[1],
                                     "none", fork=fork, defer_apply=defer)[0])
-        res = fn(x) if paired else run_branch(x, fn)
+        res = run_branch(x, fn)
         return res, None
 
     def forward(self, x):
         fork = grad_fork(x)
-        # conv1 + projection shortcut in one launch on the native kernels
-        paired = self.downsample is not None and arm_conv_pair(
-            x, self.conv1, self.bn1, self.downsample[0], self.downsample[1])
         h, _ = conv_bn_act(x, self.conv1, self.bn1, "relu", fork=fork, private=True)
-        res, res_fork = self._res(x, fork, h, self.conv2, self.bn2, paired)  # after conv1: its backward runs first
+        res, res_fork = self._res(x, fork, h, self.conv2, self.bn2)  # after conv1: its backward runs first
         return conv_bn_act(h, self.conv2, self.bn2, "relu", residual=res,
                            want_preact=self.is_last and self._need_preact, res_fork=res_fork,
                            private=not (self.is_last and self._need_preact))

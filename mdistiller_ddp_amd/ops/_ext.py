@@ -43,6 +43,7 @@ SIGNATURES = {
     "mda_event_create": "p",
     "mda_event_destroy": "p",
     "mda_event_record": "pis",
+    "mda_clock_probe": "pis",
     "mda_stream_wait_event": "pis",
     # convolution (csrc/conv_igemm.hip)
     "mda_conv_fwd": "pppppppp" + "i" * 15 + "s",
@@ -75,10 +76,6 @@ SIGNATURES = {
     "mda_shuffle_tail_bwd": "ppppp" + "i" * 7 + "s",
     "mda_pack_conv_weights_pad": "pp" + "i" * 6 + "s",
     "mda_wgrad_plan": "iiiiiiiiiip",
-    "mda_bn_finish_compiled": "",
-    "mda_conv_dgrad_bnfin": "pppp" + "i" * 12 + "ppp" + "i" + "pp" + "pp" + "ii" + "ppppppp" + "p" + "s",
-    "mda_conv_fwd_bnfin": "pppp" + "i" * 12 + "ppppp" + "ff" + "p" + "ppp" + "i" + "pppppp" + "ff" + "p" + "p" + "s",
-    "mda_conv_fwd_bnacc_pair": "piiiiiiipppiiiipppiis",
     "mda_conv_dgrad_bnsum2": "pppiiiiiiiiiiiipppippppiis",
     "mda_pack_conv_weights": "ppp" + "i" * 6 + "s",
     "mda_pack_conv_weights_multi": "piiis",

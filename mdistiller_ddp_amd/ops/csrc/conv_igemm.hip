@@ -38,16 +38,6 @@
 #include <mutex>
 #include <unordered_map>
 
-// The in-kernel BN finishes (ConvParams::fin_on / bnf_on: a grid barrier in
-// the conv epilogue, then the BN finalize + apply or the BN backward) are
-// compiled only with -DMDA_BN_FINISH_KERNELS=1.  Measured (1x MI355X,
-// profiles/r5_ab.md): kept-row registers in the shared epilogues raised the
-// halo kernels from 146-185 to 225-256 VGPRs with spills, +0.14 ms on the
-// flagship step with the finishes off, and the barrier launches hung beside
-// the concurrently replayed look-ahead teacher graph.
-#ifndef MDA_BN_FINISH_KERNELS
-#define MDA_BN_FINISH_KERNELS 0
-#endif
 
 namespace {
 
@@ -59,20 +49,6 @@ constexpr int LDS_ROW = 72;  // bf16 elements per LDS row (64 + 8 pad = 144 B)
 
 enum { LOAD_FAST = 0, LOAD_VEC8 = 1, LOAD_SCALAR = 2, LOAD_DGRAD_FAST = 3, LOAD_DGRAD_VEC8 = 4 };
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_RELU6 = 2 };
-
-// BN-backward finish of a dgrad whose output is a training BN's output
-// gradient (mda_conv_dgrad_bnfin): after adding the layer's backward sums the
-// launch waits on a grid barrier over bnb_slot and writes the layer's input
-// gradient itself, dy = scale*(dz - (sum dz + xhat*sum dz*xhat)/M), plus
-// dres = dz when the layer has a residual; block 0 accumulates dgamma /
-// dbeta; rreg != null: the residual is a projection shortcut's raw BN input
-// (VirtualBN), whose backward sums of dres (with its input ry and [4][C]
-// stats) go into rreg -- so the separate bn_bwd_apply launch is gone.
-struct BnfArgs {
-  bf16_t* dy; bf16_t* dres; float* dg; float* db;
-  const bf16_t* ry; const float* rstats; BnRegion* rreg;
-  unsigned* err;
-};
 
 struct ConvParams {
   const bf16_t* x;       // [N, H, W, Cin]
@@ -155,24 +131,6 @@ struct ConvParams {
   const bf16_t* x2;
   const bf16_t* w2;
   int cin2, kp2, cls2, sh2;
-  // BN finish (training forward with stats_slot, mda_conv_fwd_bnfin): after
-  // adding its sums the launch waits on a grid barrier over stats_slot,
-  // finalizes the BN (fin; the blocks of the first M tile also store the
-  // [4][Cout] stats and update the running statistics) and writes
-  // fin_out = act(y*scale + shift (+ residual)) itself, so the separate apply
-  // launch (bn.hip mda_bn_apply_fin) is gone.  fin_rreg: fin_res is the RAW
-  // output of another training BN (a projection shortcut, VirtualBN) that is
-  // finalized and applied here too (rfin).  Served only when every block of
-  // the grid can be resident at once (fin_fits).
-  int fin_on, fin_act;
-  int bnf_on;  // BN-backward finish (dgrad with bnb_slot), see BnfArgs
-  BnfArgs bnf;
-  FinArgs fin, rfin;
-  BnRegion* fin_rreg;
-  const bf16_t* fin_res;
-  bf16_t* fin_out;
-  bf16_t* fin_pre;
-  unsigned* fin_err;
 };
 
 // n / d for 0 <= n < 2^31 with the host-made (mul, shr) of d
@@ -452,14 +410,8 @@ __device__ __forceinline__ void conv_epilogue_bnb(const ConvParams& p, float* Cs
   }
   float s1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, s2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float t1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, t2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#if MDA_BN_FINISH_KERNELS
-  uint4 dkeep[RPT];  // the stored dx rows, for the BN finish
-#endif
 #pragma unroll
   for (int k = 0; k < RPT; ++k) {
-#if MDA_BN_FINISH_KERNELS
-    dkeep[k] = make_uint4(0u, 0u, 0u, 0u);
-#endif
     if (mrow[k] < 0) continue;
     const bool set1 = mh > 0 && mrow[k] >= mh;
     const int r0 = rr + k * RPP;
@@ -491,9 +443,6 @@ __device__ __forceinline__ void conv_epilogue_bnb(const ConvParams& p, float* Cs
         if (set1) { t1[e] += d; t2[e] += xh; } else { s1[e] += d; s2[e] += xh; }
       }
     }
-#if MDA_BN_FINISH_KERNELS
-    dkeep[k] = make_uint4(ow[0], ow[1], ow[2], ow[3]);
-#endif
     *(uint4*)(p.y + (int64_t)mrow[k] * C + co) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
   }
   __syncthreads();  // every read of the C tile is done: reuse it for the reduction
@@ -519,103 +468,6 @@ __device__ __forceinline__ void conv_epilogue_bnb(const ConvParams& p, float* Cs
         acc_add(region_acc(slot, C, (int)blockIdx.x % slot_shards(C), q) + n0 + c, (double)(a0 + a1));
     }
   }
-#if MDA_BN_FINISH_KERNELS
-  if (!p.bnf_on || mh > 0) return;
-  // ---- BN finish (ConvParams::bnf_on): the shortcut BN's inputs are loaded
-  // before the barrier so their latency hides behind the wait
-  const BnfArgs& f = p.bnf;
-  uint4 ryv[RPT];
-#pragma unroll
-  for (int k = 0; k < RPT; ++k)
-    ryv[k] = (f.rreg != nullptr && mrow[k] >= 0) ? *(const uint4*)(f.ry + (int64_t)mrow[k] * C + co)
-                                                 : make_uint4(0u, 0u, 0u, 0u);
-  const unsigned nb = gridDim.x * gridDim.y * gridDim.z;
-  const unsigned bid = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-  region_grid_barrier_n(p.bnb_slot, f.err, nb, bid);  // (its first sync retires `red`)
-  float* sm = Cs;  // [2][BN]: sum dz / M, sum dz*xhat / M of the tile's channels
-  const float invM = 1.f / (float)p.M;
-  if (tid < BN) {
-    double a = 0.0, b = 0.0;
-    if (n0 + tid < C) region_channel<true>(p.bnb_slot, C, n0 + tid, a, b);
-    sm[tid] = (float)a * invM;
-    sm[BN + tid] = (float)b * invM;
-  }
-  if (bid == 0) {  // dgamma / dbeta of every channel (bn.hip bn_bwd_apply_reg order)
-    for (int c = tid; c < C; c += NT) {
-      double a, b;
-      region_channel<true>(p.bnb_slot, C, c, a, b);
-      if (f.db) f.db[c] += (float)a;
-      if (f.dg) f.dg[c] += (float)b;
-    }
-  }
-  __syncthreads();
-  float q0[8], q1[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) { q0[e] = sm[c8 * 8 + e]; q1[e] = sm[BN + c8 * 8 + e]; }
-  float r1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, r2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int k = 0; k < RPT; ++k) {
-    if (mrow[k] < 0) continue;
-    const uint32_t dw[4] = {dkeep[k].x, dkeep[k].y, dkeep[k].z, dkeep[k].w};
-    const uint32_t yw[4] = {yv[k].x, yv[k].y, yv[k].z, yv[k].w};
-    const uint32_t rw[4] = {rv[k].x, rv[k].y, rv[k].z, rv[k].w};
-    const uint32_t qw[4] = {ryv[k].x, ryv[k].y, ryv[k].z, ryv[k].w};
-    uint32_t go[4], ro[4];
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      float g[2], dzv[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int e = 2 * w + h;
-        auto bf = [&](uint32_t u) { return h ? __uint_as_float(u & 0xffff0000u) : __uint_as_float(u << 16); };
-        float dz = bf(dw[w]);
-        const float yf = bf(yw[w]);
-        if (p.bnb_act != ACT_NONE) {
-          float z = yf * sc[e] + sh[e];
-          if (zres) z += bf(rw[w]) * vsc[e] + vsh[e];
-          dz *= bnb_act_grad(z, p.bnb_act);
-        }
-        const float xhat = (yf - mu[e]) * rs[e];
-        g[h] = sc[e] * (dz - (q0[e] + xhat * q1[e]));
-        dzv[h] = dz;
-      }
-      go[w] = pack_bf16x2(g[0], g[1]);
-      ro[w] = pack_bf16x2(dzv[0], dzv[1]);
-    }
-    const int64_t o = (int64_t)mrow[k] * C + co;
-    *(uint4*)(f.dy + o) = make_uint4(go[0], go[1], go[2], go[3]);
-    if (f.dres) *(uint4*)(f.dres + o) = make_uint4(ro[0], ro[1], ro[2], ro[3]);
-    if (f.rreg) {  // the shortcut BN's sums of the stored dres
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int w = e >> 1;
-        const float d = (e & 1) ? __uint_as_float(ro[w] & 0xffff0000u) : __uint_as_float(ro[w] << 16);
-        const float yr = (e & 1) ? __uint_as_float(qw[w] & 0xffff0000u) : __uint_as_float(qw[w] << 16);
-        r1[e] += d;
-        r2[e] += d * ((yr - f.rstats[co + e]) * f.rstats[C + co + e]);
-      }
-    }
-  }
-  if (f.rreg == nullptr) return;
-  __syncthreads();  // every read of sm is done
-  float* red2 = Cs;  // [2][RPP][BN]
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    red2[(0 * RPP + rr) * BN + c8 * 8 + e] = r1[e];
-    red2[(1 * RPP + rr) * BN + c8 * 8 + e] = r2[e];
-  }
-  __syncthreads();
-  if (tid < 2 * BN) {
-    const int q = tid / BN, c = tid - q * BN;
-    float a0 = 0.f, a1 = 0.f;
-    for (int r = 0; r < RPP; r += 2) {
-      a0 += red2[(q * RPP + r) * BN + c];
-      a1 += red2[(q * RPP + r + 1) * BN + c];
-    }
-    if (n0 + c < C)
-      acc_add(region_acc(f.rreg, C, (int)(bid % (unsigned)slot_shards(C)), q) + n0 + c, (double)(a0 + a1));
-  }
-#endif
 }
 
 template <int BM, int BN>
@@ -629,95 +481,6 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, const f32x4 (
   conv_epilogue_rows<BM, BN, 256>(p, smem, m0, n0, rows, pc, has_pc, pre);
 }
 
-#if MDA_BN_FINISH_KERNELS
-// BN finish of a training forward (ConvParams::fin_on): every block's sums
-// are in the region once the grid barrier opens; each block finalizes the
-// channels of its N tile from the coherent region totals and applies
-// act(y*scale + shift (+ res)) to the rows it kept in registers.  The
-// residual rows are loaded before the barrier so their latency hides behind
-// the wait.
-template <int BM, int BN, int NT, int RPT>
-__device__ __forceinline__ void conv_bn_finish(const ConvParams& p, float* Cs, int m0, int n0,
-                                               int rows, const uint4 (&keep)[RPT]) {
-  constexpr int TPR = BN / 8;
-  constexpr int RPP = NT / TPR;
-  const int tid = threadIdx.x;
-  const int c8 = tid % TPR, rr = tid / TPR;
-  const int C = p.Cout;
-  const int co = n0 + c8 * 8;
-  const bool cok = co < C;
-  uint4 rv[RPT];
-#pragma unroll
-  for (int k = 0; k < RPT; ++k) {
-    const int r0 = rr + k * RPP;
-    const int m = m0 + r0;
-    const bool ok = cok && r0 < rows && m < p.M && p.fin_res != nullptr;
-    rv[k] = ok ? *(const uint4*)(p.fin_res + (int64_t)m * C + co) : make_uint4(0u, 0u, 0u, 0u);
-  }
-  const unsigned nb = gridDim.x * gridDim.y * gridDim.z;
-  const unsigned bid = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-  region_grid_barrier_n(p.stats_slot, p.fin_err, nb, bid);  // (its first sync retires `red`)
-  float* sf = Cs;  // [4][BN]: scale, shift, residual scale, residual shift
-  if (tid < BN) {
-    const int c = n0 + tid;
-    float sc = 0.f, sh = 0.f, rsc = 1.f, rsh = 0.f;
-    if (c < C) {
-      fin_channel_w<true>(p.stats_slot, p.M, C, c, p.fin, sc, sh, m0 == 0);
-      // (the shortcut's sums came from an earlier launch: plain loads)
-      if (p.fin_rreg) fin_channel_w<false>(p.fin_rreg, p.M, C, c, p.rfin, rsc, rsh, m0 == 0);
-    }
-    sf[tid] = sc;
-    sf[BN + tid] = sh;
-    sf[2 * BN + tid] = rsc;
-    sf[3 * BN + tid] = rsh;
-  }
-  if (bid == 0 && tid == 0) {
-    if (p.fin.nbt) p.fin.nbt[0] += 1;
-    if (p.fin_rreg && p.rfin.nbt) p.rfin.nbt[0] += 1;
-  }
-  __syncthreads();
-  if (!cok) return;
-  float sc[8], sh[8], rsc[8], rsh[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    sc[e] = sf[c8 * 8 + e];
-    sh[e] = sf[BN + c8 * 8 + e];
-    rsc[e] = sf[2 * BN + c8 * 8 + e];
-    rsh[e] = sf[3 * BN + c8 * 8 + e];
-  }
-  const bool has_res = p.fin_res != nullptr, vr = p.fin_rreg != nullptr;
-#pragma unroll
-  for (int k = 0; k < RPT; ++k) {
-    const int r0 = rr + k * RPP;
-    const int m = m0 + r0;
-    if (r0 >= rows || m >= p.M) continue;
-    const uint32_t yw[4] = {keep[k].x, keep[k].y, keep[k].z, keep[k].w};
-    const uint32_t rw[4] = {rv[k].x, rv[k].y, rv[k].z, rv[k].w};
-    uint32_t zo[4], oo[4];
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      float v0 = __uint_as_float(yw[w] << 16) * sc[2 * w] + sh[2 * w];
-      float v1 = __uint_as_float(yw[w] & 0xffff0000u) * sc[2 * w + 1] + sh[2 * w + 1];
-      if (has_res) {
-        const float q0 = __uint_as_float(rw[w] << 16), q1 = __uint_as_float(rw[w] & 0xffff0000u);
-        if (vr) {
-          v0 += q0 * rsc[2 * w] + rsh[2 * w];
-          v1 += q1 * rsc[2 * w + 1] + rsh[2 * w + 1];
-        } else {
-          v0 += q0;
-          v1 += q1;
-        }
-      }
-      zo[w] = pack_bf16x2(v0, v1);
-      oo[w] = pack_bf16x2(apply_act(v0, p.fin_act), apply_act(v1, p.fin_act));
-    }
-    const int64_t o = (int64_t)m * C + co;
-    *(uint4*)(p.fin_out + o) = make_uint4(oo[0], oo[1], oo[2], oo[3]);
-    if (p.fin_pre) *(uint4*)(p.fin_pre + o) = make_uint4(zo[0], zo[1], zo[2], zo[3]);
-  }
-}
-
-#endif
 
 // Phase 2: NT threads own 8 channels x rows of the C tile: bias / BN affine,
 // residual, activation, preact and bf16 stores, split-K partials, or the raw
@@ -746,27 +509,13 @@ __device__ __forceinline__ void conv_epilogue_rows(const ConvParams& p, char* sm
     // return before the barrier: threads past Cout just contribute zeros.
     float s1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, s2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     const bool cok = co < group_nlim(p, n0);
-#if MDA_BN_FINISH_KERNELS
-    constexpr int RPT = (BM + RPP - 1) / RPP;
-    uint4 keep[RPT];  // the stored rows, for the BN finish
-#pragma unroll
-    for (int k = 0; k < RPT; ++k) {
-      const int r0 = rr + k * RPP;
-      const int m = m0 + r0;
-      keep[k] = make_uint4(0u, 0u, 0u, 0u);
-      if (r0 >= rows || m >= mlim || !cok) continue;
-#else
     for (int r0 = rr; r0 < rows; r0 += RPP) {
       const int m = m0 + r0;
       if (m >= mlim || !cok) break;
-#endif
       const float4 lo = *(const float4*)&Cs[r0 * CS + c8 * 8];
       const float4 hi = *(const float4*)&Cs[r0 * CS + c8 * 8 + 4];
       const uint4 o = make_uint4(pack_bf16x2(lo.x, lo.y), pack_bf16x2(lo.z, lo.w),
                                  pack_bf16x2(hi.x, hi.y), pack_bf16x2(hi.z, hi.w));
-#if MDA_BN_FINISH_KERNELS
-      keep[k] = o;
-#endif
       *(uint4*)(p.y + (int64_t)m * p.Cout + co) = o;
       const uint32_t u[4] = {o.x, o.y, o.z, o.w};
 #pragma unroll
@@ -799,9 +548,6 @@ __device__ __forceinline__ void conv_epilogue_rows(const ConvParams& p, char* sm
           p.stats_part[((int64_t)(m0 / rows) * 2 + q) * p.Cout + n0 + c] = a0 + a1;
       }
     }
-#if MDA_BN_FINISH_KERNELS
-    if (p.fin_on) conv_bn_finish<BM, BN, NT, RPT>(p, Cs, m0, n0, rows, keep);
-#endif
     return;
   }
   if ((p.Cout & 7) == 0) {
@@ -1094,7 +840,6 @@ conv_fwd_kernel(const ConvParams p) {
 __device__ __attribute__((aligned(16))) uint32_t g_zero16[4] = {0u, 0u, 0u, 0u};
 
 constexpr int GLDS_NBUF = 3;
-constexpr int GLDS_DEEP = 6;  // (BM + BN) * 128 * 6 <= 144 KB for BN <= 64
 
 // RING = 1: single-stage blocks (K <= 64, e.g. the 1x1 expand convs of a
 // bottleneck): one LDS buffer, no dead prefetch stages, and a footprint of
@@ -1166,22 +911,6 @@ conv_glds_kernel(const ConvParams p) {
   int mt, nt;
   glds_tile(p.xcd != 0, mt, nt);
   glds_body<BM, BN, MODE, RING>(p, smem, mt, nt);
-}
-
-// Two GEMMs that share the output pixels in ONE launch: N tiles [0, ny1) run
-// conv p, the rest conv q (a block's tile is block-uniform, so each block is
-// entirely one conv).  The residual block's projection shortcut (1x1, stride
-// s) beside its conv1 (3x3, stride s, pad 1): both read the block input at
-// the same output pixels, so the XCD order puts a row tile's conv1 and
-// shortcut blocks on one L2, and the shortcut costs no launch of its own.
-template <int BM, int BN, int MODE, int RING = GLDS_NBUF>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GldsOcc<BM, BN, RING>::W)))
-conv_glds_pair_kernel(const ConvParams p, const ConvParams q, int ny1) {
-  __shared__ __attribute__((aligned(16))) char smem[GldsSmem<BM, BN, RING>::BYTES];
-  int mt, nt;
-  glds_tile(p.xcd != 0, mt, nt);
-  if (nt < ny1) glds_body<BM, BN, MODE, RING>(p, smem, mt, nt);
-  else glds_body<BM, BN, MODE, RING>(q, smem, mt, nt - ny1);
 }
 
 template <int BM, int BN, int MODE, int RING>
@@ -1403,8 +1132,7 @@ __device__ __forceinline__ void glds_body(const ConvParams& p, char* smem, int m
       compute(0);
     }
   } else {
-    // RING - 1 stages in flight: a deep ring (GLDS_DEEP) for grids of about one
-    // block per CU, whose per-step time is the DMA latency / (RING - 1)
+    // RING - 1 stages in flight
 #pragma unroll
     for (int s0 = 0; s0 < RING - 1; ++s0) issue(s_begin + s0, s0);
     stamp(p, 1);
@@ -2152,18 +1880,6 @@ int ring1_max() {
   return v;
 }
 
-// deep-ring glds (GLDS_DEEP stages) for grids of <= ~1 block per CU with a
-// long K loop: 0 off (default: measured +8 us/step on the flagship with the
-// parity dgrads on it, profiles/r5_ab.md), 1 strided-dgrad parity classes,
-// 2 also plain launches
-int glds_deep() {
-  static const int v = [] {
-    const char* e = getenv("MDA_GLDS_DEEP");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
 bool use_glds() {
   static const bool on = [] {
     const char* e = getenv("MDA_CONV_GLDS");
@@ -2172,50 +1888,7 @@ bool use_glds() {
   return on;
 }
 
-// BN finish (ConvParams::fin_on) runs a grid barrier: the launch is served
-// only if every block of the grid can be resident at once (occupancy x CUs;
-// other streams' kernels only delay residency, they do not depend on this one)
-int conv_num_cus() {
-  static const int n = [] {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
-      v = 256;
-    return v;
-  }();
-  return n;
-}
-
-bool fin_fits(const void* k, dim3 grid, dim3 block) {
-  static std::mutex mu;
-  static std::unordered_map<const void*, int> occ;
-  const int threads = (int)(block.x * block.y * block.z);
-  int per = 0;
-  {
-    std::lock_guard<std::mutex> g(mu);
-    auto it = occ.find(k);
-    if (it != occ.end()) {
-      per = it->second;
-    } else {
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, threads, 0) != hipSuccess) per = 0;
-      occ[k] = per;
-    }
-  }
-  static const int cap = [] {
-    const char* e = getenv("MDA_BN_FINISH_MAXB");
-    return e ? atoi(e) : 0;
-  }();
-  const int64_t nb = (int64_t)grid.x * grid.y * grid.z;
-  const int64_t lim = (int64_t)per * conv_num_cus();
-  return per > 0 && nb <= lim && (cap <= 0 || nb <= cap);
-}
-
-#define DLAUNCH(K, G, B, S, ST, P)                                                   \
-  do {                                                                               \
-    if (((P).fin_on || (P).bnf_on) && !fin_fits((const void*)(K), (G), (B)))         \
-      return MDA_NOT_SERVED;                                                         \
-    hipLaunchKernelGGL(K, G, B, S, ST, P);                                           \
-  } while (0)
+#define DLAUNCH(K, G, B, S, ST, P) hipLaunchKernelGGL(K, G, B, S, ST, P)
 
 template <int BM, int BN>
 int launch_tile(const ConvParams& p, int mode, int splits, hipStream_t st) {
@@ -2240,20 +1913,6 @@ int launch_tile(const ConvParams& p, int mode, int splits, hipStream_t st) {
     else
       DLAUNCH((conv_glds_kernel<BM, BN, LOAD_DGRAD_VEC8, 1>), grid, dim3(256), 0, st, p);
     return (int)hipGetLastError();
-  }
-  if constexpr (BN <= 64) {
-    if (mode != LOAD_SCALAR && use_glds() && !reg1x1 && glds_deep() >= 2 &&
-        (int64_t)grid.x * grid.y * grid.z <= 320 && p.steps_per_split >= 6) {
-      if (mode == LOAD_FAST)
-        DLAUNCH((conv_glds_kernel<BM, BN, LOAD_FAST, GLDS_DEEP>), grid, dim3(256), 0, st, p);
-      else if (mode == LOAD_VEC8)
-        DLAUNCH((conv_glds_kernel<BM, BN, LOAD_VEC8, GLDS_DEEP>), grid, dim3(256), 0, st, p);
-      else if (mode == LOAD_DGRAD_FAST)
-        DLAUNCH((conv_glds_kernel<BM, BN, LOAD_DGRAD_FAST, GLDS_DEEP>), grid, dim3(256), 0, st, p);
-      else
-        DLAUNCH((conv_glds_kernel<BM, BN, LOAD_DGRAD_VEC8, GLDS_DEEP>), grid, dim3(256), 0, st, p);
-      return (int)hipGetLastError();
-    }
   }
   if (mode != LOAD_SCALAR && use_glds() && !reg1x1) {
     if (mode == LOAD_FAST)
@@ -2346,7 +2005,7 @@ int dispatch(ConvParams& p, int mode, int64_t tile, int64_t splits, hipStream_t 
   // (conv1x1.hip) -- transposed MFMA, resident weights, stores straight from
   // the accumulators; -1 = shape not served, fall through
   if (p.KH == 1 && p.KW == 1 && p.pad == 0 && p.cout_g >= p.Cout && p.ldx == p.Cin &&
-      p.bnb_slot == nullptr && p.stats_part == nullptr && p.stamps == nullptr && !p.fin_on &&
+      p.bnb_slot == nullptr && p.stats_part == nullptr && p.stamps == nullptr &&
       (mode == LOAD_FAST || mode == LOAD_VEC8 ||
        ((mode == LOAD_DGRAD_FAST || mode == LOAD_DGRAD_VEC8) && p.stride == 1))) {
     // (K = Cin a multiple of 32 is enough there: LOAD_VEC8 covers K = 32 / 96 / ...)
@@ -2449,13 +2108,7 @@ int dispatch(ConvParams& p, int mode, int64_t tile, int64_t splits, hipStream_t 
     const int bm = (int)(tile / 1000), bn = (int)(tile % 1000);
     const int mc = p.N * ((p.Ho + p.par - 1) / p.par) * ((p.Wo + p.par - 1) / p.par);
     dim3 grid((mc + bm - 1) / bm, (p.Cout + bn - 1) / bn, s2 * (int)splits);
-    const bool deep = glds_deep() >= 1 && bn <= 64 && (int64_t)grid.x * grid.y * grid.z <= 320 &&
-                      p.steps_per_split >= 6;
-    if (deep && tile == 128064)
-      DLAUNCH((conv_glds_kernel<128, 64, LOAD_DGRAD_FAST, GLDS_DEEP>), grid, dim3(256), 0, st, p);
-    else if (deep && tile == 64064)
-      DLAUNCH((conv_glds_kernel<64, 64, LOAD_DGRAD_FAST, GLDS_DEEP>), grid, dim3(256), 0, st, p);
-    else switch (tile) {
+    switch (tile) {
       case 128128: DLAUNCH((conv_glds_kernel<128, 128, LOAD_DGRAD_FAST>), grid, dim3(256), 0, st, p); break;
       case 128064: DLAUNCH((conv_glds_kernel<128, 64, LOAD_DGRAD_FAST>), grid, dim3(256), 0, st, p); break;
       case 128032: DLAUNCH((conv_glds_kernel<128, 32, LOAD_DGRAD_FAST>), grid, dim3(256), 0, st, p); break;
@@ -2584,7 +2237,7 @@ static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, float* part
                            const void* bn_y, const void* bn_res, const float* bn_stats,
                            int64_t bn_act, void* region, int64_t groups, const float* bn_vres,
                            int64_t bn_mh, int64_t bn_rstride, const void* x2, const void* w2,
-                           int64_t cin2, int64_t kp2, const BnfArgs* bnf, hipStream_t st);
+                           int64_t cin2, int64_t kp2, hipStream_t st);
 
 MDA_API int mda_conv_dgrad_bnsum_g(const void* dy, const void* wt, void* dx, float* partial,
                                    const void* res, int64_t N, int64_t H, int64_t W, int64_t Cin,
@@ -2596,7 +2249,7 @@ MDA_API int mda_conv_dgrad_bnsum_g(const void* dy, const void* wt, void* dx, flo
                                    int64_t bn_rstride, hipStream_t st) {
   return conv_dgrad_impl(dy, wt, dx, partial, res, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride,
                          pad, Kp, tile, splits, bn_y, bn_res, bn_stats, bn_act, region, groups,
-                         bn_vres, bn_mh, bn_rstride, nullptr, nullptr, 0, 0, nullptr, st);
+                         bn_vres, bn_mh, bn_rstride, nullptr, nullptr, 0, 0, st);
 }
 
 // mda_conv_dgrad_bnsum_g of a stride-s conv with a 1 x 1 / stride-s / pad-0
@@ -2620,43 +2273,7 @@ MDA_API int mda_conv_dgrad_bnsum2(const void* dy, const void* wt, void* dx, int6
   if (splits != 1) return MDA_NOT_SERVED;
   return conv_dgrad_impl(dy, wt, dx, nullptr, nullptr, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride,
                          pad, Kp, tile, splits, bn_y, bn_res, bn_stats, bn_act, region, 1, bn_vres,
-                         0, 0, dy2, wt2, cin2, kp2, nullptr, st);
-}
-
-// mda_conv_dgrad_bnsum_g / mda_conv_dgrad_bnsum2 (dy2 != null) that also
-// FINISHES the BN layer's backward in the same launch (ConvParams::bnf_on,
-// BnfArgs): f_dy receives the layer's input gradient, f_dres its residual
-// gradient (null: no residual gradient wanted), dgamma / dbeta are
-// accumulated into f_dg / f_db, and f_rreg (with the shortcut BN's input f_ry
-// and stats f_rstats) receives the projection shortcut BN's backward sums.
-// dx (the BN output gradient) and the region sums are still produced, so a
-// consumer that cannot use the finished values falls back to the region.
-// MDA_NOT_SERVED (nothing launched): split-K plans, grids that cannot be
-// resident at once, MDA_BN_BWD_FINISH=0.
-MDA_API int mda_conv_dgrad_bnfin(const void* dy, const void* wt, void* dx, const void* res,
-                                 int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Ho,
-                                 int64_t Wo, int64_t Cout, int64_t KH, int64_t KW, int64_t stride,
-                                 int64_t pad, int64_t Kp, const void* bn_y, const void* bn_res,
-                                 const float* bn_stats, int64_t bn_act, void* region,
-                                 const float* bn_vres, const void* dy2, const void* wt2,
-                                 int64_t cin2, int64_t kp2, void* f_dy, void* f_dres, float* f_dg,
-                                 float* f_db, const void* f_ry, const float* f_rstats, void* f_rreg,
-                                 void* err, hipStream_t st) {
-  static const bool on = [] {
-    const char* e = getenv("MDA_BN_BWD_FINISH");
-    return !(e && e[0] == '0');
-  }();
-  if (!MDA_BN_FINISH_KERNELS || !on || region == nullptr) return MDA_NOT_SERVED;
-  if (dy2 != nullptr && (wt2 == nullptr || cin2 <= 0 || cin2 % BK || kp2 < cin2 || kp2 % BK))
-    return MDA_NOT_SERVED;
-  int64_t tile = 0, splits = 0;
-  mda_conv_plan(N * H * W, Cin, Kp, &tile, &splits);
-  if (splits != 1) return MDA_NOT_SERVED;
-  const BnfArgs f{(bf16_t*)f_dy, (bf16_t*)f_dres, f_dg, f_db, (const bf16_t*)f_ry, f_rstats,
-                  (BnRegion*)f_rreg, (unsigned*)err};
-  return conv_dgrad_impl(dy, wt, dx, nullptr, res, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
-                         Kp, tile, splits, bn_y, bn_res, bn_stats, bn_act, region, 1, bn_vres, 0, 0,
-                         dy2, wt2, cin2, kp2, &f, st);
+                         0, 0, dy2, wt2, cin2, kp2, st);
 }
 
 static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, float* partial,
@@ -2666,7 +2283,7 @@ static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, float* part
                            const void* bn_y, const void* bn_res, const float* bn_stats,
                            int64_t bn_act, void* region, int64_t groups, const float* bn_vres,
                            int64_t bn_mh, int64_t bn_rstride, const void* x2, const void* w2,
-                           int64_t cin2, int64_t kp2, const BnfArgs* bnf, hipStream_t st) {
+                           int64_t cin2, int64_t kp2, hipStream_t st) {
   if (Cout % 8 || groups < 1 || Cin % groups || Cout % groups) return (int)hipErrorInvalidValue;
   if (region != nullptr && (splits != 1 || Cin % 8 || Cin > SLOT_CMAX || bn_y == nullptr ||
                             bn_stats == nullptr))
@@ -2683,13 +2300,6 @@ static int conv_dgrad_impl(const void* dy, const void* wt, void* dx, float* part
   p.bnb_slot = (BnRegion*)region;
   p.bnb_act = (int)bn_act;
   p.bnb_vres = bn_res != nullptr ? bn_vres : nullptr;
-  if (bnf != nullptr) {
-    if (region == nullptr || bn_mh != 0 || groups != 1 || bnf->dy == nullptr ||
-        (bnf->rreg != nullptr && (bnf->ry == nullptr || bnf->rstats == nullptr || bnf->dres == nullptr)))
-      return MDA_NOT_SERVED;
-    p.bnf_on = 1;
-    p.bnf = *bnf;
-  }
   p.x2 = (const bf16_t*)x2;
   p.w2 = (const bf16_t*)w2;
   p.cin2 = (int)cin2;
@@ -2846,128 +2456,4 @@ MDA_API int mda_conv_fwd_bnacc_g(const void* x, const void* w, void* y, float* p
   return mda_bn_stats_acc(y, p.M, Cout, region, st);
 }
 
-// Training conv + its BN in ONE launch (ConvParams::fin_on): the conv
-// epilogue adds the BN batch sums, waits on a grid barrier, finalizes the BN
-// (running statistics, [4][Cout] stats) and stores out = act(y*scale +
-// shift (+ res)) and the pre-activation when pre != null; y (the raw conv
-// output, kept for the backward) is stored too.  rregion != null: res is the
-// RAW output of another training BN whose batch sums are complete (a
-// projection shortcut, VirtualBN), finalized and applied here as well.
-// Returns MDA_NOT_SERVED (nothing launched) for split-K plans, grouped convs,
-// grids that cannot be resident at once, or MDA_BN_FINISH=0; the caller then
-// runs mda_conv_fwd_bnacc_g + mda_bn_apply_fin(_vr).
-MDA_API int mda_conv_fwd_bnfin(const void* x, const void* w, void* y, void* region, int64_t N,
-                               int64_t H, int64_t W, int64_t Cin, int64_t Ho, int64_t Wo,
-                               int64_t Cout, int64_t KH, int64_t KW, int64_t stride, int64_t pad,
-                               int64_t Kp, const float* gamma, const float* beta,
-                               float* running_mean, float* running_var, float* stats,
-                               float momentum, float eps, int64_t* nbt, const void* res, void* out,
-                               void* pre, int64_t act, void* rregion, const float* rgamma,
-                               const float* rbeta, float* rrunning_mean, float* rrunning_var,
-                               float* rstats, float rmomentum, float reps, int64_t* rnbt,
-                               void* err, hipStream_t st) {
-  static const bool on = [] {
-    const char* e = getenv("MDA_BN_FINISH");
-    return !(e && e[0] == '0');
-  }();
-  if (!MDA_BN_FINISH_KERNELS || !on || Cout % 8 || Cout > SLOT_CMAX || region == nullptr ||
-      out == nullptr)
-    return MDA_NOT_SERVED;
-  if (rregion != nullptr && (res == nullptr || rstats == nullptr)) return (int)hipErrorInvalidValue;
-  ConvParams p{};
-  p.ldx = (int)Cin;
-  p.cout_g = (int)Cout;
-  p.x = (const bf16_t*)x; p.w = (const bf16_t*)w;
-  p.y = (bf16_t*)y;
-  p.N = N; p.H = H; p.W = W; p.Cin = Cin; p.Ho = Ho; p.Wo = Wo; p.Cout = Cout; p.KH = KH;
-  p.KW = KW; p.stride = stride; p.pad = pad; p.K = KH * KW * Cin; p.Kp = Kp; p.M = N * Ho * Wo;
-  p.zsplits = 1;
-  p.stamps = g_stamps;
-  const int mode = (Cin % BK == 0) ? LOAD_FAST : (Cin % 8 == 0 ? LOAD_VEC8 : LOAD_SCALAR);
-  int64_t tile = 0, splits = 0;
-  mda_conv_plan(p.M, p.Cout, p.Kp, &tile, &splits);
-  if (splits != 1) return MDA_NOT_SERVED;
-  p.stats_slot = (BnRegion*)region;
-  p.fin_on = 1;
-  p.fin_act = (int)act;
-  p.fin = FinArgs{gamma, beta, running_mean, running_var, stats, momentum, eps, nbt};
-  p.rfin = FinArgs{rgamma, rbeta, rrunning_mean, rrunning_var, rstats, rmomentum, reps, rnbt};
-  p.fin_rreg = (BnRegion*)rregion;
-  p.fin_res = (const bf16_t*)res;
-  p.fin_out = (bf16_t*)out;
-  p.fin_pre = (bf16_t*)pre;
-  p.fin_err = (unsigned*)err;
-  const int halo = halo_eligible(p) ? 1 : 0;
-  return dispatch(p, mode, tile, splits, st, halo);
-}
 
-// A residual block's conv1 (KH x KW, stride s, pad) and its projection shortcut
-// (1 x 1, stride s, pad 0) on the same input x, as ONE training launch
-// (conv_glds_pair_kernel): both raw bf16 outputs, each with its BN batch sums
-// in its own region.  Returns MDA_NOT_SERVED (nothing launched) when the pair is not served
-// -- different loader modes, a split-K or halo-kernel conv1, grouped convs --
-// and the caller launches the two convs on their own.
-MDA_API int mda_conv_fwd_bnacc_pair(const void* x, int64_t N, int64_t H, int64_t W, int64_t Cin,
-                                    int64_t Ho, int64_t Wo, int64_t stride, const void* w1,
-                                    void* y1, void* reg1, int64_t Cout1, int64_t K1, int64_t pad1,
-                                    int64_t Kp1, const void* w2, void* y2, void* reg2,
-                                    int64_t Cout2, int64_t Kp2, hipStream_t st) {
-  static const bool on = [] {
-    const char* e = getenv("MDA_CONV_PAIR");
-    return !(e && e[0] == '0');
-  }();
-  if (!on || !use_glds()) return MDA_NOT_SERVED;
-  auto mk = [&](ConvParams& p, const void* w, void* y, void* reg, int64_t Cout, int64_t K,
-                int64_t pad, int64_t Kp) {
-    p = ConvParams{};
-    p.ldx = (int)Cin;
-    p.cout_g = (int)Cout;
-    p.x = (const bf16_t*)x; p.w = (const bf16_t*)w; p.y = (bf16_t*)y;
-    p.N = N; p.H = H; p.W = W; p.Cin = Cin; p.Ho = Ho; p.Wo = Wo; p.Cout = Cout; p.KH = K;
-    p.KW = K; p.stride = stride; p.pad = pad; p.K = K * K * Cin; p.Kp = Kp; p.M = N * Ho * Wo;
-    p.zsplits = 1;
-    p.stats_slot = (BnRegion*)reg;
-    p.stamps = g_stamps;
-    p.x_bytes = (int)(N * H * W * Cin * 2);
-    p.w_bytes = (int)(Cout * Kp * 2);
-    glds_prep(p);
-  };
-  if (Cout1 % 8 || Cout2 % 8 || Cout1 > SLOT_CMAX || Cout2 > SLOT_CMAX || Cin % 8) return MDA_NOT_SERVED;
-  if (N * H * W * Cin * 2 >= ((int64_t)1 << 31) || N * Ho * Wo * std::max(Cout1, Cout2) >= ((int64_t)1 << 31))
-    return MDA_NOT_SERVED;
-  ConvParams p, q;
-  mk(p, w1, y1, reg1, Cout1, K1, pad1, Kp1);
-  mk(q, w2, y2, reg2, Cout2, 1, 0, Kp2);
-  if (p.Kp % BK || q.Kp % BK || p.Kp < p.K || q.Kp < q.K) return MDA_NOT_SERVED;
-  const int mode = (Cin % BK == 0) ? LOAD_FAST : LOAD_VEC8;
-  if (halo_eligible(p)) return MDA_NOT_SERVED;
-  int64_t tile = 0, splits = 0;
-  mda_conv_plan(p.M, p.Cout, p.Kp, &tile, &splits);
-  if (splits != 1 || (p.Kp / BK) <= ring1_max()) return MDA_NOT_SERVED;
-  p.steps_per_split = p.Kp / BK;
-  q.steps_per_split = q.Kp / BK;
-  const int bm = (int)(tile / 1000), bn = (int)(tile % 1000);
-  const int ny1 = (int)((Cout1 + bn - 1) / bn), ny2 = (int)((Cout2 + bn - 1) / bn);
-  dim3 grid((unsigned)((p.M + bm - 1) / bm), (unsigned)(ny1 + ny2), 1);
-#define PAIR_CASE(BM_, BN_)                                                                     \
-  case BM_ * 1000 + BN_:                                                                        \
-    if (mode == LOAD_FAST)                                                                      \
-      hipLaunchKernelGGL((conv_glds_pair_kernel<BM_, BN_, LOAD_FAST>), grid, dim3(256), 0, st, p, q, ny1); \
-    else                                                                                        \
-      hipLaunchKernelGGL((conv_glds_pair_kernel<BM_, BN_, LOAD_VEC8>), grid, dim3(256), 0, st, p, q, ny1); \
-    break;
-  switch (tile) {
-    PAIR_CASE(128, 128)
-    PAIR_CASE(128, 64)
-    PAIR_CASE(128, 32)
-    PAIR_CASE(64, 128)
-    PAIR_CASE(64, 64)
-    PAIR_CASE(64, 32)
-    default: return MDA_NOT_SERVED;
-  }
-#undef PAIR_CASE
-  return (int)hipGetLastError();
-}
-
-// 1 when the in-kernel BN finishes are compiled in (MDA_BN_FINISH_KERNELS).
-MDA_API int mda_bn_finish_compiled() { return MDA_BN_FINISH_KERNELS; }

@@ -49,3 +49,28 @@ MDA_API int mda_stream_wait_event(void* ev, int64_t mode, hipStream_t st) {
   if (mode == 2) return capture_node(st, false, (hipEvent_t)ev);
   return (int)hipStreamWaitEvent(st, (hipEvent_t)ev, mode == 1 ? hipEventWaitExternal : 0);
 }
+
+// Diagnostics: the shader clock at this point of a stream.  One wave reads
+// the core-clock counter (s_memtime) and the constant 100 MHz counter
+// (s_memrealtime) before and after a ~2 us spin and stores the ratio as MHz
+// into out[slot] (a float vector store).  scripts/replay_ramp.py puts one at
+// every step boundary of a timed window to see whether the first steps after
+// an idle GPU run at a lower clock.
+namespace {
+__global__ void clock_probe_kernel(float* out, int slot) {
+  if (threadIdx.x != 0) return;
+  const uint64_t c0 = __builtin_amdgcn_s_memtime();
+  const uint64_t r0 = __builtin_amdgcn_s_memrealtime();
+  uint64_t r1 = r0, c1 = c0;
+  while (r1 - r0 < 200) {  // 2 us of the 100 MHz clock
+    r1 = __builtin_amdgcn_s_memrealtime();
+    c1 = __builtin_amdgcn_s_memtime();
+  }
+  out[slot] = (float)((double)(c1 - c0) * 100.0 / (double)(r1 - r0));
+}
+}  // namespace
+
+MDA_API int mda_clock_probe(float* out, int64_t slot, hipStream_t st) {
+  hipLaunchKernelGGL(clock_probe_kernel, dim3(1), dim3(64), 0, st, out, (int)slot);
+  return (int)hipGetLastError();
+}

@@ -380,106 +380,31 @@ class BnLink:
     accumulates into it in place.
     """
 
-    __slots__ = ("y", "res", "stats", "act", "M", "C", "dout", "ver", "region", "vres", "gamma",
-                 "beta", "need_res", "rlink", "private", "done")
+    __slots__ = ("y", "res", "stats", "act", "M", "C", "dout", "ver", "region", "vres")
 
-    def __init__(self, y, res, stats, act, M, C, vres=None, gamma=None, beta=None, need_res=False,
-                 rlink=None, private=False):
+    def __init__(self, y, res, stats, act, M, C, vres=None):
         self.y, self.res, self.stats, self.act, self.M, self.C = y, res, stats, act, M, C
         self.vres = vres if res is not None else None  # res is a virtual residual (VirtualBN)
-        self.dout = self.region = self.done = None
+        self.dout = self.region = None
         self.ver = -1
-        # the layer's own backward operands, for a consumer dgrad that finishes
-        # it (mda_conv_dgrad_bnfin): its parameters, whether its residual needs
-        # a gradient, the projection-shortcut BN that residual came from, and
-        # whether the output is private to native consumers (no feature loss
-        # or other autograd consumer can add to its gradient)
-        self.gamma, self.beta, self.need_res, self.rlink = gamma, beta, need_res, rlink
-        self.private = private
 
-    def arm(self, dout, region, done=None) -> None:
-        self.dout, self.ver, self.region, self.done = dout, dout._version, region, done
-
-    def can_finish(self) -> bool:
-        """A consumer dgrad may finish this layer's backward in its launch: the
-        output is private, dgamma / dbeta go straight into bound flat views."""
-        return (self.private and _BNF_ON[0] and self.gamma is not None and _DUAL[0] is None
-                and self.gamma.grad is not None and self.beta.grad is not None)
+    def arm(self, dout, region) -> None:
+        self.dout, self.ver, self.region = dout, dout._version, region
 
     def take(self, dout):
-        return self.take_full(dout)[0]
-
-    def take_full(self, dout):
-        """(region, done): the dgrad-epilogue sums -- and, if that dgrad
-        finished the backward, its (dy, dres) -- when ``dout`` IS the armed
-        tensor, unmodified; else (None, None)."""
-        d, r, f = self.dout, self.region, self.done
-        self.dout = self.region = self.done = None
+        """The dgrad-epilogue sums' region when ``dout`` IS the armed tensor,
+        unmodified; else None."""
+        d, r = self.dout, self.region
+        self.dout = self.region = None
         if d is not None and d is dout and dout._version == self.ver:
             _BNB_COUNT[0] += 1
-            return r, f
+            return r
         if d is not None:
-            if f is not None:
-                # the finish accumulated dgamma / dbeta already: a private
-                # output must never receive another gradient
-                raise RuntimeError("a BN output marked private received an extra gradient")
             _BNB_COUNT[1] += 1
-        return None, None
+        return None
 
 
 _BNB_COUNT = [0, 0]  # BN backwards on dgrad-epilogue sums / armed links that fell back
-_BNF_ON = [os.environ.get("MDA_BN_BWD_FINISH", "1") != "0"]
-_BNF_COUNT = [0]  # BN backwards finished inside the consumer's dgrad launch
-
-
-def set_bn_bwd_finish(on: bool) -> None:
-    """BN backward finished in the consumer dgrad's launch (mda_conv_dgrad_bnfin) on / off."""
-    _BNF_ON[0] = bool(on)
-
-
-def bn_bwd_finish_count(reset: bool = False) -> int:
-    v = _BNF_COUNT[0]
-    if reset:
-        _BNF_COUNT[0] = 0
-    return v
-
-
-def _bnf_prepare(link, dev):
-    """Outputs of a dgrad that finishes ``link``'s BN backward, or None."""
-    if link is None or not link.can_finish():
-        return None
-    dy = torch.empty_like(link.y)
-    dres = torch.empty_like(link.y) if link.need_res else None
-    rl = link.rlink if link.need_res else None
-    rreg = _region(link.C, dev) if rl is not None else None
-    return dy, dres, rl, rreg
-
-
-def _bnf_dgrad(link, reg, dev, dy, wt, dx, other, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
-               KpT, fold):
-    """The consumer dgrad (optionally with a folded 1x1 shortcut dgrad,
-    ``fold`` = :class:`_DeferredDgrad`) that also finishes ``link``'s BN
-    backward in its launch; arms the link (and the shortcut BN's link) and
-    returns 0, or NOT_SERVED having launched nothing."""
-    if reg is None:
-        return _ext.NOT_SERVED
-    prep = _bnf_prepare(link, dev)
-    if prep is None:
-        return _ext.NOT_SERVED
-    fdy, fdres, rl, rreg = prep
-    rc = _ext.call("mda_conv_dgrad_bnfin", dy, wt, dx, other, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
-                   stride, pad, KpT, link.y, link.res, link.stats, link.act, reg, link.vres,
-                   fold.dy if fold is not None else None, fold.wt if fold is not None else None,
-                   fold.cin2 if fold is not None else 0, fold.kp2 if fold is not None else 0,
-                   fdy, fdres, link.gamma.grad, link.beta.grad, rl.y if rl is not None else None,
-                   rl.stats if rl is not None else None, rreg, _err_word(dev),
-                   ok=(0, _ext.NOT_SERVED))
-    if rc == 0:
-        link.arm(dx, reg, done=(fdy, fdres))
-        if rl is not None:
-            rl.arm(fdres, rreg)
-        _BNF_COUNT[0] += 1
-    return rc
 _LAST_VBN = [None]
 _BNB_ON = [os.environ.get("MDA_BN_DGRAD_SUMS", "1") != "0"]
 _LAST_LINK = [None]
@@ -511,12 +436,7 @@ def _bn_bwd(dout, dpre, y, res, stats, gamma, beta, M, C, act, need_res, direct_
     db = beta.grad if direct_gb else None
     dy = torch.empty_like(y)
     dres = torch.empty_like(y) if need_res else None
-    reg, done = link.take_full(dout) if link is not None else (None, None)
-    if done is not None:
-        # finished by the consumer's dgrad launch (mda_conv_dgrad_bnfin)
-        if dpre is not None or not direct_gb:
-            raise RuntimeError("a finished BN backward cannot take a pre-activation gradient")
-        return done[0], (done[1] if need_res else None), None
+    reg = link.take(dout) if link is not None else None
     # the residual's producer is a training BN without activation (a projection
     # shortcut): dres IS its output gradient, so this pass adds its sums too
     rl = res_link if (need_res and res_link is not None and 256 % (C // 8) == 0) else None
@@ -578,6 +498,10 @@ class PackCache:
         self._total = 0
         self._extra_key = None  # (zero fills, image) the table was built with
         self._img_pad = None
+        # the table / padded image a captured graph points at: an eager step
+        # after the capture (a partial batch) may rebuild the table, and the
+        # graph's copies must outlive that
+        self._graph_refs = None
 
     def lookup_pad(self, weight):
         """The channel-padded stem operand packed for this step, or None."""
@@ -711,6 +635,8 @@ class PackCache:
             self._build(device, zero, image)
         _ext.call("mda_pack_conv_weights_multi", self._table, self._table.shape[0], self._total,
                   self._khkw)
+        if capturing:
+            self._graph_refs = (self._table, self._img_pad)
         self.armed = True
         _PREPAD[0] = ((image, image._version, self._img_pad, torch.cuda.current_stream(device).cuda_stream)
                       if image is not None else None)
@@ -806,21 +732,17 @@ def set_deterministic(on: bool) -> None:
     pool + FC head) whose order varies run to run; here BN runs on per-block
     partial rows and a fixed-order finalize launch instead (the
     ``MDA_BN_FUSED=0`` kernels), and the fusions that exist only on the
-    regions (VirtualBN, BnLink sums, the depthwise fusions, the paired
-    forward) are off.  Everything else is fixed-order in both modes (split-K
+    regions (VirtualBN, BnLink sums, the depthwise fusions) are off.  Everything else is fixed-order in both modes (split-K
     combines, weight-gradient partial reduces, losses, optimizer, VID).
     Turning it off restores the switches as they were."""
     on = bool(on)
     if on == _DET["on"]:
         return
     if on:
-        _DET["saved"] = (_BN_FUSED[0], _BNB_ON[0], _VRES_ON[0], _DW_VIN_ON[0], _DW_BNB_ON[0],
-                         _PAIR_ON[0])
+        _DET["saved"] = (_BN_FUSED[0], _BNB_ON[0], _VRES_ON[0], _DW_VIN_ON[0], _DW_BNB_ON[0])
         _BN_FUSED[0] = _BNB_ON[0] = _VRES_ON[0] = _DW_VIN_ON[0] = _DW_BNB_ON[0] = False
-        _PAIR_ON[0] = False
     else:
-        (_BN_FUSED[0], _BNB_ON[0], _VRES_ON[0], _DW_VIN_ON[0], _DW_BNB_ON[0],
-         _PAIR_ON[0]) = _DET["saved"]
+        (_BN_FUSED[0], _BNB_ON[0], _VRES_ON[0], _DW_VIN_ON[0], _DW_BNB_ON[0]) = _DET["saved"]
     _DET["on"] = on
 
 
@@ -1010,6 +932,12 @@ def _fork_sum(fork, g):
     other = fork.take()
     if other is None:
         return g
+    if isinstance(other, _DeferredDgrad):
+        # a parked projection-shortcut dgrad whose fold partner has no dgrad
+        # of its own: compute it here
+        if _DUAL[0] is not None:
+            raise RuntimeError("a deferred shortcut dgrad reached the dual backward")
+        other = other.materialize(tuple(g.shape))
     if _DUAL[0] is not None:
         gf, of = dual_full(g), dual_full(other)
         full, half = dual_alloc(g.shape, g.dtype, g.device)
@@ -1083,65 +1011,6 @@ def can_defer_to_depthwise(x, dwconv, dwbn) -> bool:
             and dwbn is not None and dwbn.training and train_supported(x, dwconv, dwbn))
 
 
-# A residual block's conv1 and its projection shortcut read the same input at
-# the same output pixels: with both on the native kernels, conv1's forward
-# launches the two convs as ONE kernel (mda_conv_fwd_bnacc_pair) and the
-# shortcut's forward picks up its raw output and BN-sum region instead of
-# launching.  The block arms the pair right before conv1 (arm_conv_pair).
-# Opt-in: measured +6 us/step on the flagship (1x MI355X, 3 interleaved fresh
-# processes each, scripts/ab_env.sh: 0.8529 vs 0.8468 ms) -- the shortcut's
-# blocks share conv1's CUs and slow its critical blocks more than the saved
-# launch is worth.
-_FIN_ON = [os.environ.get("MDA_BN_FINISH", "1") != "0"]
-_FIN_COUNT = [0]
-
-
-def set_bn_finish(on: bool) -> None:
-    """Training conv + BN finalize + apply in one launch (mda_conv_fwd_bnfin) on / off."""
-    _FIN_ON[0] = bool(on)
-
-
-def bn_finish_count(reset: bool = False) -> int:
-    """Forward convs whose BN was finished inside the conv launch."""
-    v = _FIN_COUNT[0]
-    if reset:
-        _FIN_COUNT[0] = 0
-    return v
-
-
-_PAIR_ON = [os.environ.get("MDA_CONV_PAIR", "0") == "1"]
-_PAIR = [None]    # (x, conv1 weight, shortcut conv) armed by the block
-_PAIR_DONE = {}   # id(shortcut weight) -> (x, raw output, region) made by conv1's launch
-_PAIR_COUNT = [0]  # paired launches issued (tests)
-
-
-def set_conv_pair(on: bool) -> None:
-    """conv1 + projection shortcut forward in one launch on / off (A/B)."""
-    _PAIR_ON[0] = bool(on)
-
-
-def arm_conv_pair(x, conv1, bn1, conv_sc, bn_sc) -> bool:
-    """Arm the paired forward of ``conv1`` (+ ``bn1``) and the 1x1 projection
-    shortcut ``conv_sc`` (+ ``bn_sc``) on input ``x``; True when armed (the
-    caller then runs the shortcut inline, right after conv1)."""
-    _PAIR[0] = None
-    packs = _ACTIVE[0]
-    if not (_PAIR_ON[0] and _BN_FUSED[0] and packs is not None and packs.armed and _DUAL[0] is None):
-        return False
-    if not (isinstance(conv_sc, nn.Conv2d) and conv_sc.kernel_size == (1, 1)
-            and conv_sc.stride == conv1.stride and tuple(conv_sc.padding) == (0, 0)
-            and conv1.groups == 1 and conv_sc.groups == 1 and conv1.bias is None
-            and conv_sc.bias is None and conv1.in_channels == conv_sc.in_channels):
-        return False
-    if not (train_supported(x, conv1, bn1) and train_supported(x, conv_sc, bn_sc)):
-        return False
-    need_dx = x.requires_grad
-    if packs.lookup(conv1.weight, need_dx) is None or packs.lookup(conv_sc.weight, need_dx) is None:
-        return False
-    _PAIR[0] = (x, conv1.weight, conv_sc)
-    return True
-
-
 class _ConvBNActTrain(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, gamma, beta, residual, meta, bn, want_preact, forks=(None, None),
@@ -1172,7 +1041,6 @@ class _ConvBNActTrain(torch.autograd.Function):
         gc = G > 1 and cin_w % 8 == 0 and (weight.shape[0] // G) % 8 == 0 and _GROUPED_COMPACT[0]
         link_in = getattr(x, "_mda_bnlink", None) if (need_dx and (G == 1 or gc) and _BNB_ON[0]) else None
         chpad = G == 1 and (not need_dx) and needs_channel_pad(cin_w)
-        x_in = x
         x = pad_channels8(x) if chpad else _cl_bf16(x)
         N, Cin, H, W = x.shape
         Cout, _, KH, KW = weight.shape
@@ -1246,62 +1114,13 @@ class _ConvBNActTrain(torch.autograd.Function):
         ctx.vbn = None
         out = y if defer else torch.empty_like(y)
         pre = torch.empty_like(y) if want_preact else None
-        fin = False
         if _BN_FUSED[0] or gc:
             # conv whose epilogue adds the BN sums into the stream's slot, then
-            # apply with the finalize in its prologue (2 launches) -- or all of
-            # it in the conv launch (mda_conv_fwd_bnfin)
-            done = _PAIR_DONE.pop(id(weight), None)
-            pr, _PAIR[0] = _PAIR[0], None
-            if done is not None and done[0] is x_in and G == 1:
-                # this is a paired shortcut: conv1's launch produced y and its sums
-                y, reg = done[1], done[2]
-                out = y if defer else torch.empty_like(y)
-            else:
-                reg = _region(Cout, dev)
-                rc = _ext.NOT_SERVED
-                if (pr is not None and pr[0] is x_in and pr[1] is weight and ent is not None
-                        and G == 1 and not chpad and splits == 1 and residual is None):
-                    sc = pr[2]
-                    e2 = packs.lookup(sc.weight, need_dx)
-                    if e2 is not None:
-                        Cout2, Kp2 = sc.out_channels, e2["meta"][4]
-                        y2 = torch.empty((N, Cout2, Ho, Wo), dtype=torch.bfloat16, device=dev,
-                                         memory_format=torch.channels_last)
-                        reg2 = _region(Cout2, dev)
-                        rc = _ext.call("mda_conv_fwd_bnacc_pair", x, N, H, W, Cin, Ho, Wo, stride,
-                                       wf, y, reg, Cout, KH, pad, Kp, e2["wf"], y2, reg2, Cout2, Kp2,
-                                       ok=(0, _ext.NOT_SERVED))
-                        if rc == 0:
-                            _PAIR_DONE[id(sc.weight)] = (x_in, y2, reg2)
-                            _PAIR_COUNT[0] += 1
-                if rc != 0 and not defer and not gc and G == 1 and part is None and _FIN_ON[0]:
-                    # conv + BN finalize + apply in ONE launch (grid barrier in the
-                    # conv epilogue); not served -> the two launches below
-                    rvb = rv.bn if rv is not None else None
-                    rc = _ext.call(
-                        "mda_conv_fwd_bnfin", x, wf, y, reg, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
-                        stride, pad, Kp, gamma.detach(), beta.detach(), bn.running_mean,
-                        bn.running_var, stats, float(bn.momentum), float(bn.eps),
-                        bn.num_batches_tracked, res, out, pre, act,
-                        rv.reg if rv is not None else None, rv.gamma if rv is not None else None,
-                        rv.beta if rv is not None else None,
-                        rvb.running_mean if rvb is not None else None,
-                        rvb.running_var if rvb is not None else None,
-                        rv.stats if rv is not None else None,
-                        float(rvb.momentum) if rvb is not None else 0.0,
-                        float(rvb.eps) if rvb is not None else 0.0,
-                        rvb.num_batches_tracked if rvb is not None else None, _err_word(dev),
-                        ok=(0, _ext.NOT_SERVED))
-                    fin = rc == 0
-                    if fin:
-                        _FIN_COUNT[0] += 1
-                if rc != 0:
-                    _ext.call("mda_conv_fwd_bnacc_g", x, wf, y, part, reg, N, H, W, Cin, Ho, Wo,
-                              Cout, KH, KW, stride, pad, Kp, tile, splits, G if gc else 1)
-            if fin:
-                pass  # applied by the conv launch
-            elif defer:
+            # apply with the finalize in its prologue (2 launches)
+            reg = _region(Cout, dev)
+            _ext.call("mda_conv_fwd_bnacc_g", x, wf, y, part, reg, N, H, W, Cin, Ho, Wo,
+                      Cout, KH, KW, stride, pad, Kp, tile, splits, G if gc else 1)
+            if defer:
                 # no apply: the consumer's apply finalizes this BN (VirtualBN)
                 ctx.vbn = VirtualBN(reg, gamma.detach(), beta.detach(), bn, stats, act)
             elif rv is not None:
@@ -1340,9 +1159,7 @@ class _ConvBNActTrain(torch.autograd.Function):
         # output: its gradient would join dz after the consumer's epilogue)
         ctx.bnlink = None
         if not want_preact and Cout <= 2048:
-            ctx.bnlink = BnLink(y, res if act != 0 else None, stats, act, M, Cout, ctx.vres,
-                                gamma, beta, ctx.has_res and ctx.needs_input_grad[4], ctx.res_link,
-                                bool(private) and G == 1 and not ctx.gc)
+            ctx.bnlink = BnLink(y, res if act != 0 else None, stats, act, M, Cout, ctx.vres)
         _LAST_LINK[0] = ctx.bnlink
         _LAST_VBN[0] = ctx.vbn
         ctx.cbias = cbias is not None
@@ -1395,9 +1212,8 @@ class _ConvBNActTrain(torch.autograd.Function):
                 parks = False
             elif isinstance(other, _DeferredDgrad):
                 reg = _region(Cin, dev) if link is not None else None
-                rc = _bnf_dgrad(link, reg, dev, dy, wt, dx, None, N, H, W, Cin, Ho, Wo, Cout, KH,
-                                KW, stride, pad, KpT, other)
-                if rc != 0:
+                rc = _ext.NOT_SERVED
+                if other.stride == stride and tuple(other.dy.shape[2:]) == (Ho, Wo):
                     rc = _ext.call("mda_conv_dgrad_bnsum2", dy, wt, dx, N, H, W, Cin, Ho, Wo, Cout,
                                    KH, KW, stride, pad, KpT, link.y if reg is not None else None,
                                    link.res if reg is not None else None,
@@ -1405,8 +1221,8 @@ class _ConvBNActTrain(torch.autograd.Function):
                                    link.act if reg is not None else 0, reg,
                                    link.vres if reg is not None else None, other.dy, other.wt,
                                    other.cin2, other.kp2, ok=(0, _ext.NOT_SERVED))
-                    if rc == 0 and reg is not None:
-                        link.arm(dx, reg)
+                if rc == 0 and reg is not None:
+                    link.arm(dx, reg)
                 if rc == 0:
                     _MERGE_COUNT[0] += 1
                     folded = True
@@ -1425,15 +1241,12 @@ class _ConvBNActTrain(torch.autograd.Function):
                     link.arm(dx, reg)
             elif link is not None and not parks and splits == 1:
                 # dx is the whole output gradient of the BN layer that made x:
-                # its backward sums come out of this epilogue (BnLink) -- and,
-                # when the launch can finish that backward, its dy too
+                # its backward sums come out of this epilogue (BnLink)
                 reg = _region(Cin, dev)
-                if _bnf_dgrad(link, reg, dev, dy, wt, dx, other, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
-                              stride, pad, KpT, None) != 0:
-                    _ext.call("mda_conv_dgrad_bnsum_g", dy, wt, dx, part, other, N, H, W, Cin, Ho,
-                              Wo, Cout, KH, KW, stride, pad, KpT, tile, splits, link.y, link.res,
-                              link.stats, link.act, reg, 1, link.vres, 0, 0)
-                    link.arm(dx, reg)
+                _ext.call("mda_conv_dgrad_bnsum_g", dy, wt, dx, part, other, N, H, W, Cin, Ho,
+                          Wo, Cout, KH, KW, stride, pad, KpT, tile, splits, link.y, link.res,
+                          link.stats, link.act, reg, 1, link.vres, 0, 0)
+                link.arm(dx, reg)
             else:
                 _ext.call("mda_conv_dgrad_res", dy, wt, dx, part, other, N, H, W, Cin, Ho, Wo,
                           Cout, KH, KW, stride, pad, KpT, tile, splits)
@@ -1520,6 +1333,8 @@ def _conv_bn_backward_dual(ctx, dout, dpre):
         part = torch.empty(splits * 2 * N * H * W * Cin, dtype=torch.float32, device=dev) \
             if splits > 1 else None
         other = x_fork.take() if x_fork is not None else None
+        if isinstance(other, _DeferredDgrad):
+            raise RuntimeError("a deferred shortcut dgrad reached the dual backward")
         if other is not None:
             dual_full(other)
         parks = other is None and x_fork is not None and x_fork.armed

@@ -4,8 +4,8 @@ rounds of (arm A, arm B, ...) flagship runs (mdistiller_ddp_amd.benchmark.run),
 median ms/step per arm.  Box-to-box spread is ~1-2 %; this compares arms
 under the same clocks.
 
-    python scripts/ab_bench.py --arms pair=1,pair=0 [--rounds 3] [--steps 300]
-    knobs: pair (conv1 + shortcut launch), merge (shortcut dgrad merge)
+    python scripts/ab_bench.py --arms merge=1;merge=0 [--rounds 3] [--steps 300]
+    knobs: merge (shortcut dgrad merge)
 """
 import argparse
 import json
@@ -20,9 +20,7 @@ def apply(knobs):
     from mdistiller_ddp_amd.ops import hip_train as H
     for k, v in knobs.items():
         on = v not in ("0", "false", "off")
-        if k == "pair":
-            H.set_conv_pair(on)
-        elif k == "merge":
+        if k == "merge":
             H.set_dgrad_merge(on)
         else:
             raise SystemExit(f"unknown knob {k}")

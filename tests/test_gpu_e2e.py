@@ -255,7 +255,7 @@ def test_native_bf16_tracks_fp32_over_300_steps(typ, student):
 
 
 @pytest.mark.parametrize("typ,trainer,tgraph", [("DKD", "base", "split"), ("DKD", "base", "fork"),
-                                                 ("FITNET", "base", "split"),
+                                                 ("FITNET", "base", "split"), ("OFD", "base", "split"),
                                                  ("REVIEWKD", "base", "split"), ("KD", "dot", "split")])
 def test_teacher_lookahead_matches_inline_teacher(typ, trainer, tgraph):
     """The captured step with the teacher look-ahead (teacher of batch t+1 beside
@@ -342,3 +342,76 @@ def test_deterministic_mode_graph_runs_are_bitwise_equal():
     finally:
         hip_train.set_deterministic(False)
     assert torch.equal(out[0], out[1]), (out[0] - out[1]).abs().max()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("trainer", ["base", "dot"])
+def test_teacher_lookahead_deterministic_is_bitwise(trainer):
+    """EXPERIMENT.DETERMINISTIC: the look-ahead step (teacher of batch t+1 on
+    its own graph beside the student step t) gives bitwise the parameters of
+    the inline-teacher step.  The default mode's test above needs a 2e-4
+    allowance for the fp64-atomic BN sums; without them nothing may differ."""
+    from mdistiller_ddp_amd.ops import hip_train
+    torch.manual_seed(0)
+    cfg = _cfg("DKD" if trainer == "base" else "KD", trainer)
+    cfg.EXPERIMENT.DETERMINISTIC = True
+    d0 = build_distiller(cfg, 100, "cuda")
+    batches = list(SyntheticLoader("cifar100", 64, "cuda", steps_per_epoch=12, channels_last=True))
+    outs = []
+    try:
+        for la in (True, False):
+            d = copy.deepcopy(d0)
+            c = cfg.clone()
+            c.RUNTIME.TEACHER_LOOKAHEAD = "on" if la else "off"
+            d.train()
+            st = TrainStep(d, c, "cuda", trainer=trainer, use_graph=True, dtype=torch.bfloat16)
+            st.set_epoch(30.0)
+            for i, b in enumerate(batches):
+                st.step(b, next_batch=batches[i + 1] if i + 1 < len(batches) else None)
+            torch.cuda.synchronize()
+            assert (st._pipe is not None) == la
+            outs.append(st.flat.data.clone())
+    finally:
+        hip_train.set_deterministic(False)
+    assert torch.equal(outs[0], outs[1]), (outs[0] - outs[1]).abs().max()
+
+
+@pytest.mark.timeout(300)
+def test_partial_batch_between_replays_matches_eager():
+    """A partial batch (eager, other shapes) between hipGraph replays must not
+    disturb the captured step: the pack table / padded image the graph points
+    at stay alive and unchanged (ops/hip_train.py PackCache._graph_refs), so
+    graph replays before and after it train exactly like an eager run of the
+    same batches.  Deterministic mode on both sides: bitwise-close."""
+    from mdistiller_ddp_amd.ops import hip_train
+    torch.manual_seed(0)
+    cfg = _cfg("DKD")
+    cfg.EXPERIMENT.DETERMINISTIC = True
+    cfg.SOLVER.LR = 0.01
+    d0 = build_distiller(cfg, 100, "cuda")
+    full = list(SyntheticLoader("cifar100", 64, "cuda", steps_per_epoch=10, channels_last=True))
+    part = next(iter(SyntheticLoader("cifar100", 40, "cuda", steps_per_epoch=1, seed=5,
+                                     channels_last=True)))
+    seq = full[:6] + [part] + full[6:] + [part] + full[:2]
+    outs = []
+    try:
+        for g in (True, False):
+            d = copy.deepcopy(d0)
+            d.train()
+            st = TrainStep(d, cfg, "cuda", use_graph=g, dtype=torch.bfloat16)
+            st.set_epoch(30.0)
+            for i, b in enumerate(seq):
+                nb = seq[i + 1] if i + 1 < len(seq) else None
+                st.step(b, next_batch=nb)
+                # churn the caching allocator between steps: a freed block the
+                # graph still pointed at would be handed out and overwritten
+                junk = [torch.full((1 << 16,), float("nan"), device="cuda") for _ in range(8)]
+                del junk
+            torch.cuda.synchronize()
+            assert (st._graphs is not None) == g
+            outs.append(st.flat.data.clone())
+    finally:
+        hip_train.set_deterministic(False)
+    assert torch.isfinite(outs[0]).all()
+    rel = ((outs[0] - outs[1]).norm() / outs[1].norm()).item()
+    assert rel < 1e-4, rel

@@ -158,9 +158,6 @@ def test_pack_cache_matches_per_layer_packing(student):
     init = None
     det = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
     torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
-    # the paired conv1 + shortcut launch needs the cache: off on both sides so
-    # the two runs differ only in how the weights are packed
-    hip_train.set_conv_pair(False)
     out = []
     for d, use_cache in ((d1, True), (d2, False)):
         d.train()

@@ -44,6 +44,8 @@ SIGNATURES = {
     "mda_event_destroy": "p",
     "mda_event_record": "pis",
     "mda_clock_probe": "pis",
+    "mda_stream_create": "iiip",
+    "mda_stream_destroy": "p",
     "mda_stream_wait_event": "pis",
     # convolution (csrc/conv_igemm.hip)
     "mda_conv_fwd": "pppppppp" + "i" * 15 + "s",

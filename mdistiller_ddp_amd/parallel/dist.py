@@ -61,6 +61,9 @@ def init_distributed(backend: str = "auto", timeout_s: float = 600.0, device: st
                   timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":
             kw["device_id"] = dev
+            opts = nccl_options()
+            if opts is not None:
+                kw["pg_options"] = opts
         try:
             dist.init_process_group(**kw)
         except TypeError:  # older torch without device_id
@@ -69,6 +72,19 @@ def init_distributed(backend: str = "auto", timeout_s: float = 600.0, device: st
     _INFO = DistInfo(rank, local, world, backend if world > 1 else "none", dev)
     os.environ["IS_MASTER_NODE"] = "1" if rank == 0 else "0"
     return _INFO
+
+
+def nccl_options():
+    """RCCL process-group options: the collectives run on HIGH-priority
+    internal streams, so a bucket's all-reduce is dispatched ahead of the
+    teacher / student kernels queued on the same device (docs/DESIGN.md 4).
+    None when this torch build has no ProcessGroupNCCL."""
+    pg = getattr(dist, "ProcessGroupNCCL", None)
+    if pg is None or not hasattr(pg, "Options"):
+        return None
+    o = pg.Options()
+    o.is_high_priority_stream = True
+    return o
 
 
 def info() -> DistInfo:

@@ -361,7 +361,10 @@ class GradReducer:
             # never one of the step's other live streams (teacher, branch,
             # wgrad, capture): the bucket all-reduces would queue behind them
             avoid = [S._streams.get(idx), S._branch_streams.get(idx)] + list(self.avoid_streams)
-            self._comm = S._fresh_stream(idx, avoid)
+            # high priority: a bucket's wait + all-reduce never queues behind the
+            # teacher's or the student's kernels on a shared hardware queue
+            # (docs/DESIGN.md 4, stream -> queue map)
+            self._comm = S._fresh_stream(idx, avoid, priority=-1)
         # (no wait on the current stream: that would wait for the whole replay;
         # each all-reduce waits only for its bucket's event)
         self._works = {}

@@ -33,6 +33,13 @@ def _free_port():
 
 def _worker(rank, world, port, scenario, outdir):
     comm = "split"
+    det = scenario.endswith("_det")
+    if det:
+        scenario = scenario[:-len("_det")]
+    wire = "fp32"
+    for w in ("_bf16wire", "_fp32wire"):
+        if scenario.endswith(w):
+            scenario, wire = scenario[:-len(w)], w[1:5]
     if scenario.endswith("_events"):
         scenario, comm = scenario[:-len("_events")], "events"
     elif scenario.endswith("_default"):  # every DIST knob at its default
@@ -65,6 +72,12 @@ def _worker(rank, world, port, scenario, outdir):
         if scenario == "dot":
             cfg.DIST.GRAD_DTYPE = "bf16"
     cfg.CRD.NCE.K = 256
+    cfg.EXPERIMENT.DETERMINISTIC = det
+    if wire == "bf16":
+        cfg.DIST.GRAD_DTYPE = "bf16"
+    nsteps = int(os.environ.get("MDA_TEST_STEPS", "20"))
+    if nsteps > 20:
+        cfg.SOLVER.LR = 0.05
     torch.manual_seed(1000 + rank)  # different init per rank
     d = build_distiller(cfg, 100, dev, num_data=1000)
     d.train()
@@ -77,7 +90,7 @@ def _worker(rank, world, port, scenario, outdir):
     out = {"init_equal": all(torch.equal(allc[0], a) for a in allc)}
     st.set_epoch(1.0)
     init = st.flat.data.clone()
-    ld = SyntheticLoader("cifar100", 32, dev, steps_per_epoch=20, channels_last=True, seed=rank,
+    ld = SyntheticLoader("cifar100", 32, dev, steps_per_epoch=nsteps, channels_last=True, seed=rank,
                          crd_k=256, num_data=1000)
     if typ == "CRD":  # distinct dataset indices across ranks (a sharded sampler's guarantee)
         for i, b in enumerate(ld.batches):
@@ -86,7 +99,11 @@ def _worker(rank, world, port, scenario, outdir):
     mem0 = None
     if typ == "CRD":
         mem0 = torch.cat([d.contrast.memory_v1.reshape(-1), d.contrast.memory_v2.reshape(-1)]).clone()
+    curve = []
     for i, b in enumerate(ld):
+        if nsteps > 20 and i in (50, nsteps - 50):
+            curve.append(st.meters.summary(reduce=True)["loss"])
+            st.meters.reset()
         st.step(b)
         if typ == "CRD" and i == 10:
             # an epoch's partial last batch between graph replays:
@@ -112,6 +129,7 @@ def _worker(rank, world, port, scenario, outdir):
     out["moved"] = float((flat - init).norm() / init.norm())
     m = st.meters.summary(reduce=True)
     out["loss"] = m["loss"]
+    out["curve"] = [curve[0], m["loss"]] if curve else []  # steps 0-49, the last 50
     if typ == "CRD":  # the memory banks stay identical: the exchange ran between the graphs
         mem = torch.cat([d.contrast.memory_v1.reshape(-1), d.contrast.memory_v2.reshape(-1)])
         allm = [torch.empty_like(mem) for _ in range(world)]
@@ -170,6 +188,43 @@ def test_events_overlap_matches_split():
         return ((a["flat"] - b["flat"]).norm() / b["flat"].norm()).item()
     spread = rel(sp2[0], sp[0])
     assert rel(ev[0], sp[0]) <= 3.0 * spread + 2e-3, (rel(ev[0], sp[0]), spread)
+
+
+@pytest.mark.timeout(600)
+def test_events_matches_split_bitwise_deterministic():
+    """EXPERIMENT.DETERMINISTIC (fixed-order BN reductions): the events path
+    (each bucket's all-reduce behind its event of the replayed backward) and
+    the split path (all-reduce after the backward graph) give bitwise the same
+    parameters after 20 steps -- same buckets, same sums, only the launch time
+    of the collectives differs."""
+    os.environ["MDA_TEST_BUCKET_MB"] = "0.5"
+    try:
+        ev = _spawn("dkd_events_det")
+        sp = _spawn("dkd_det")
+    finally:
+        os.environ.pop("MDA_TEST_BUCKET_MB", None)
+    assert ev[0]["early"] > 0 and ev[0]["events"], ev[0]
+    for r in ev + sp:
+        assert r["params_equal"] and r["finite"], r
+    assert torch.equal(ev[0]["flat"], sp[0]["flat"]), (ev[0]["flat"] - sp[0]["flat"]).abs().max()
+
+
+@pytest.mark.timeout(900)
+def test_bf16_wire_tracks_fp32_wire_over_300_steps():
+    """DIST.GRAD_DTYPE=bf16 (gradients all-reduced as bf16, half the bytes on
+    the wire) vs the fp32 wire over 300 two-rank steps: both learn and the
+    loss of the last 50 steps agrees within 3 %."""
+    os.environ["MDA_TEST_STEPS"] = "300"
+    try:
+        b16 = _spawn("dkd_default_bf16wire")
+        f32 = _spawn("dkd_default_fp32wire")
+    finally:
+        os.environ.pop("MDA_TEST_STEPS", None)
+    for r in b16 + f32:
+        assert r["params_equal"] and r["finite"], r
+    (first16, last16), (first32, last32) = b16[0]["curve"], f32[0]["curve"]
+    assert last16 < 0.8 * first16 and last32 < 0.8 * first32, (b16[0]["curve"], f32[0]["curve"])
+    assert abs(last16 - last32) / abs(last32) < 0.03, (b16[0]["curve"], f32[0]["curve"])
 
 
 @pytest.mark.timeout(400)

@@ -104,7 +104,8 @@ def main():
                    "ms_per_step": round(r["ms_per_step"], 3), "per_gpu_batch": bs,
                    "n_gpus": r["n_gpus"], "graph": r["graph"], "dtype": r["dtype"],
                    "final_loss": round(r["final_loss"], 4),
-                   "host_ms_per_step": round(r["host_ms_per_step"], 3)}
+                   "host_ms_per_step": round(r["host_ms_per_step"], 3),
+                   "host_idle_ms_per_step": round(r["host_idle_ms_per_step"], 3)}
             if name in BASELINE_MS and r["n_gpus"] == 1 and bs == 64:
                 row["baseline_ms"] = BASELINE_MS[name]
                 row["speedup_vs_baseline"] = round(BASELINE_MS[name] / r["ms_per_step"], 2)

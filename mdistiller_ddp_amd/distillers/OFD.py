@@ -91,9 +91,8 @@ class ConnectorConvBN(nn.Module):
         return nn.Sequential(conv, bn)
 
     def forward(self, g_s):
-        # conv + training BN on the native fused kernels (nn.Sequential's
-        # MIOpen conv + train-mode BN inside the captured step went non-finite
-        # on its second replay with the look-ahead teacher: scripts/debug/ofd_nan.py)
+        # conv + training BN on the native fused kernels (one BN-sum region
+        # per call from the step's arena; no MIOpen train-mode BN in the graph)
         from ..ops.nn import conv_bn_act
         return [conv_bn_act(f, c[0], c[1], "none")[0] for c, f in zip(self.connectors, g_s)]
 

@@ -668,12 +668,11 @@ class TrainStep:
         both sides already fill the GPU and it costs 6 %: ``auto`` skips that case."""
         if self.lookahead != "auto":
             return bool(self.lookahead)
-        if getattr(self.distiller, "_teacher_train_bn", False):
-            # a train-mode teacher (OFD.TEACHER_TRAIN_BN) runs inline: with the
-            # look-ahead its second replayed step computed different teacher
-            # features (non-finite loss_kd in 2-3 of 3 runs, prefetch or not;
-            # scripts/debug/ofd_nan.py) -- inline it matches eager exactly
-            return False
+        # (a train-mode teacher, OFD.TEACHER_TRAIN_BN, is served too: its
+        # round-5 non-finite losses under the look-ahead were the step's arena
+        # zero fill racing the teacher graph's BN regions, fixed by closing the
+        # arena window at the step capture (_bn_end); the look-ahead test
+        # covers OFD, tests/test_gpu_e2e.py)
         img = static.get("image")
         big = img is not None and img.dim() == 4 and min(img.shape[-2:]) >= 128
         needs = tuple(getattr(self.distiller, "teacher_needs", ("logits",)))

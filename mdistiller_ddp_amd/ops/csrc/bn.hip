@@ -636,7 +636,6 @@ _Pragma("unroll")
 // of the region's sums in the prologue.  Grid stride is a multiple of C/8
 // when C/8 is a power of two (power-of-two grid) so every thread keeps one
 // channel group.
-constexpr int APPLY_V = 4;  // 16-byte vectors per thread, all loads issued before any math
 
 __device__ __forceinline__ void apply8(const uint4& yv, const uint4& rv, bool has_res, const float* sc,
                                        const float* sh, int act, uint4& out, uint4& z,
@@ -673,27 +672,34 @@ __device__ __forceinline__ void fin_channel(BnRegion* reg, int64_t M, int C, int
 }
 
 // z = y*scale + shift (+ res); out = act(z); preact = z -- with the finalize
-// of the region's sums in the prologue.  The thread's APPLY_V vectors of y
+// of the region's sums in the prologue.  The thread's V vectors of y
 // (and res) are loaded BEFORE the prologue, so their latency overlaps the
-// region loads; grids past APPLY_V vectors per thread loop.
+// region loads; grids past V vectors per thread loop.
 // rreg != null: `res` is the RAW output of another training conv whose BN
 // (no activation: a projection shortcut) is applied here too -- its batch
 // statistics are finalized from rreg in the same prologue (rf: its affine,
 // running stats and [4][C] stats) and res contributes res*rscale + rshift, so
 // that BN never runs an apply pass of its own.
+// The per-channel operands live in dynamic LDS sized to C (2C or 4C floats):
+// a static SLOT_CMAX-channel array held 16-32 KB whatever the layer's width.
+// V = 16-byte vectors per thread (apply_vpt).
+template <int V>
 __global__ void __launch_bounds__(256)
 bn_apply_fin_kernel(const bf16_t* __restrict__ y, BnRegion* __restrict__ reg, int64_t M, int C,
                     FinArgs f, const bf16_t* __restrict__ res, bf16_t* __restrict__ out,
                     bf16_t* __restrict__ preact, int act, BnRegion* __restrict__ rreg, FinArgs rf) {
-  __shared__ float s_scale[SLOT_CMAX], s_shift[SLOT_CMAX];
-  __shared__ float s_rscale[SLOT_CMAX], s_rshift[SLOT_CMAX];
+  extern __shared__ float s_dyn[];
+  float* const s_scale = s_dyn;
+  float* const s_shift = s_dyn + C;
+  float* const s_rscale = s_dyn + 2 * C;  // (rreg only)
+  float* const s_rshift = s_dyn + 3 * C;
   const int64_t total = M * C / 8;
   const int c8 = C / 8;
   const int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  uint4 yv[APPLY_V], rv[APPLY_V];
+  uint4 yv[V], rv[V];
 #pragma unroll
-  for (int k = 0; k < APPLY_V; ++k) {
+  for (int k = 0; k < V; ++k) {
     const int64_t i = i0 + k * stride;
     const int64_t ii = i < total ? i : 0;
     yv[k] = ((const uint4*)y)[ii];
@@ -711,7 +717,7 @@ bn_apply_fin_kernel(const bf16_t* __restrict__ y, BnRegion* __restrict__ reg, in
   float sc[8], sh[8], rsc[8], rsh[8];
   const bool vr = rreg != nullptr;
 #pragma unroll
-  for (int k = 0; k < APPLY_V; ++k) {
+  for (int k = 0; k < V; ++k) {
     const int64_t i = i0 + k * stride;
     if (i < total) {
       const int cc = (int)(i % c8) * 8;
@@ -726,7 +732,7 @@ bn_apply_fin_kernel(const bf16_t* __restrict__ y, BnRegion* __restrict__ reg, in
       if (preact) ((uint4*)preact)[i] = z;
     }
   }
-  for (int64_t i = i0 + APPLY_V * stride; i < total; i += stride) {
+  for (int64_t i = i0 + V * stride; i < total; i += stride) {
     const int cc = (int)(i % c8) * 8;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -1012,22 +1018,28 @@ _Pragma("unroll")
 // mda_conv_dgrad_bnsum): one streaming pass, no reduction and no grid
 // barrier.  dz = dout * act'(z) (+ dpre), dy = scale*(dz - (sum dz +
 // xhat*sum dz*xhat)/M), dres = dz; block 0 accumulates dgamma / dbeta (and
-// writes sums).  The thread's APPLY_V vectors are loaded before the
+// writes sums).  The thread's V vectors are loaded before the
 // prologue reads the region, so both latencies overlap.
+template <int V>
 __global__ void __launch_bounds__(256)
 bn_bwd_apply_reg_kernel(BwdArgs a) {
   dual_shift(a);
-  // per-channel operands in LDS: a thread's channel group changes along the
-  // grid stride when C / 8 is not a power of two (MobileNetV2 widths)
-  __shared__ float s_m0[SLOT_CMAX], s_m1[SLOT_CMAX], s_st[4][SLOT_CMAX], s_vr[2][SLOT_CMAX];
+  // per-channel operands in LDS (dynamic, 8C floats): a thread's channel group
+  // changes along the grid stride when C / 8 is not a power of two
+  // (MobileNetV2 widths)
+  extern __shared__ float s_dyn[];
   const int C = a.C;
+  float* const s_m0 = s_dyn;
+  float* const s_m1 = s_dyn + C;
+  float* const s_st0 = s_dyn + 2 * C;  // [4][C] mean, rstd, scale, shift
+  float* const s_vr0 = s_dyn + 6 * C;  // [2][C] virtual-residual scale, shift
   const int c8 = C / 8;
   const int64_t total = (int64_t)a.M * c8;
   const int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  Raw8 raw[APPLY_V];
+  Raw8 raw[V];
 #pragma unroll
-  for (int k = 0; k < APPLY_V; ++k) {
+  for (int k = 0; k < V; ++k) {
     const int64_t i = i0 + k * stride;
     bwd_load8(a, (i < total ? i : 0) * 8, raw[k]);
   }
@@ -1040,9 +1052,9 @@ bn_bwd_apply_reg_kernel(BwdArgs a) {
       s_m0[c] = t0 * invM;
       s_m1[c] = t1 * invM;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) s_st[q][c] = a.stats[q * C + c];
-      s_vr[0][c] = a.vres ? a.vres[2 * C + c] : 1.f;
-      s_vr[1][c] = a.vres ? a.vres[3 * C + c] : 0.f;
+      for (int q = 0; q < 4; ++q) s_st0[q * C + c] = a.stats[q * C + c];
+      s_vr0[c] = a.vres ? a.vres[2 * C + c] : 1.f;
+      s_vr0[C + c] = a.vres ? a.vres[3 * C + c] : 0.f;
       if (blockIdx.x == 0) {
         if (a.sums) { a.sums[c] = t0; a.sums[C + c] = t1; }
         if (a.dbeta) a.dbeta[c] += t0;
@@ -1057,9 +1069,9 @@ bn_bwd_apply_reg_kernel(BwdArgs a) {
     float sc[8], sh[8], mu[8], rs[8], dz[8], vsc[8], vsh[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      mu[e] = s_st[0][c0 + e]; rs[e] = s_st[1][c0 + e];
-      sc[e] = s_st[2][c0 + e]; sh[e] = s_st[3][c0 + e];
-      vsc[e] = s_vr[0][c0 + e]; vsh[e] = s_vr[1][c0 + e];
+      mu[e] = s_st0[c0 + e]; rs[e] = s_st0[C + c0 + e];
+      sc[e] = s_st0[2 * C + c0 + e]; sh[e] = s_st0[3 * C + c0 + e];
+      vsc[e] = s_vr0[c0 + e]; vsh[e] = s_vr0[C + c0 + e];
     }
     bwd_dz8(a, v, sc, sh, dz, vsc, vsh);
     const uint32_t yw[4] = {v.y.x, v.y.y, v.y.z, v.y.w};
@@ -1082,11 +1094,11 @@ bn_bwd_apply_reg_kernel(BwdArgs a) {
     if (a.rreg) rsum_add8(a, i * 8, c0, ro, r1, r2);  // (the host checks: fixed channel group)
   };
 #pragma unroll
-  for (int k = 0; k < APPLY_V; ++k) {
+  for (int k = 0; k < V; ++k) {
     const int64_t i = i0 + k * stride;
     if (i < total) emit(i, raw[k]);
   }
-  for (int64_t i = i0 + APPLY_V * stride; i < total; i += stride) {
+  for (int64_t i = i0 + V * stride; i < total; i += stride) {
     Raw8 v;
     bwd_load8(a, i * 8, v);
     emit(i, v);
@@ -1114,6 +1126,25 @@ inline int apply_blocks(int64_t n8, int vpt) {
   int64_t b = 1;
   while (b < want && b < 1024) b <<= 1;
   return (int)b;
+}
+
+// Vectors per thread of a streaming apply launch.  Fewer vectors and more
+// blocks for small layers (>= 2 blocks per CU) measured the same on the
+// flagship and 2 % slower on R50 -> MV1 (profiles/r6_ab.md): kept at 4.
+inline int apply_vpt(int64_t) { return 4; }
+
+template <typename... A>
+int launch_apply_fin(int v, dim3 g, size_t lds, hipStream_t st, A... args) {
+  if (v != 4) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_apply_fin_kernel<4>, g, dim3(256), lds, st, args...);
+  return (int)hipGetLastError();
+}
+
+int launch_bwd_apply(int v, dim3 g, int C, hipStream_t st, const BwdArgs& a) {
+  if (v != 4) return (int)hipErrorInvalidValue;
+  const size_t lds = (size_t)8 * C * sizeof(float);
+  hipLaunchKernelGGL(bn_bwd_apply_reg_kernel<4>, g, dim3(256), lds, st, a);
+  return (int)hipGetLastError();
 }
 
 }  // namespace
@@ -1144,11 +1175,12 @@ MDA_API int mda_bn_apply_fin_vr(const void* y, void* region, int64_t M, int64_t 
   if (rregion != nullptr && (res == nullptr || rstats == nullptr)) return (int)hipErrorInvalidValue;
   FinArgs f{gamma, beta, running_mean, running_var, stats, momentum, eps, nbt};
   FinArgs rf{rgamma, rbeta, rrunning_mean, rrunning_var, rstats, rmomentum, reps, rnbt};
-  const int nb = apply_blocks(M * C / 8, APPLY_V);
-  hipLaunchKernelGGL(bn_apply_fin_kernel, dim3(nb), dim3(256), 0, st, (const bf16_t*)y,
-                     (BnRegion*)region, M, (int)C, f, (const bf16_t*)res, (bf16_t*)out,
-                     (bf16_t*)preact, (int)act, (BnRegion*)rregion, rf);
-  MDA_CHECK_LAUNCH();
+  const int v = apply_vpt(M * C / 8);
+  const int nb = apply_blocks(M * C / 8, v);
+  const size_t lds = (size_t)(rregion != nullptr ? 4 : 2) * C * sizeof(float);
+  return launch_apply_fin(v, dim3(nb), lds, st, (const bf16_t*)y, (BnRegion*)region, M, (int)C, f,
+                          (const bf16_t*)res, (bf16_t*)out, (bf16_t*)preact, (int)act,
+                          (BnRegion*)rregion, rf);
 }
 
 MDA_API int mda_bn_apply_fin(const void* y, void* region, int64_t M, int64_t C, const float* gamma,
@@ -1203,8 +1235,8 @@ MDA_API int mda_bn_bwd_fused(const void* dout, const void* dout2, const void* dp
     hipLaunchKernelGGL(bn_bwd_sums_kernel, dim3(nbr, ns), dim3(256), 0, st, a);
     { const int rc_ = (int)hipGetLastError(); if (rc_) return rc_; }
     a.err = nullptr;
-    hipLaunchKernelGGL(bn_bwd_apply_reg_kernel, dim3(apply_blocks(M * C / 8, APPLY_V), ns), dim3(256), 0, st, a);
-    MDA_CHECK_LAUNCH();
+    const int v = apply_vpt(M * C / 8);
+    return launch_bwd_apply(v, dim3(apply_blocks(M * C / 8, v), ns), (int)C, st, a);
   }
   if (per <= 1) hipLaunchKernelGGL((bn_bwd_fused_kernel<1, true>), dim3(nb, ns), dim3(256), 0, st, a);
   else if (per <= 2) hipLaunchKernelGGL((bn_bwd_fused_kernel<2, true>), dim3(nb, ns), dim3(256), 0, st, a);
@@ -1228,10 +1260,9 @@ MDA_API int mda_bn_bwd_apply_reg(const void* dout, const void* dpre, const void*
             (const bf16_t*)res, stats, (bf16_t*)dy, (bf16_t*)dres, dgamma, dbeta, sums,
             (BnRegion*)region, nullptr, (int)M, (int)C, (int)act, (const bf16_t*)ry, rstats,
             (BnRegion*)rregion, vres, dd, dg, dr};
-  const int nb = apply_blocks(M * C / 8, APPLY_V);
   if (rregion != nullptr && (dres == nullptr || ry == nullptr || rstats == nullptr ||
                              256 % (C / 8) != 0))
     return (int)hipErrorInvalidValue;  // a thread must keep one channel group
-  hipLaunchKernelGGL(bn_bwd_apply_reg_kernel, dim3(nb, (unsigned)nsets), dim3(256), 0, st, a);
-  MDA_CHECK_LAUNCH();
+  const int v = apply_vpt(M * C / 8);
+  return launch_bwd_apply(v, dim3(apply_blocks(M * C / 8, v), (unsigned)nsets), (int)C, st, a);
 }

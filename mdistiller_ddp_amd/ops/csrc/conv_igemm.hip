@@ -1554,183 +1554,6 @@ conv_halo1_kernel(const ConvParams p) {
   conv_epilogue<BM, BN>(p, acc, smem, m0, n0, PB, ParClass{}, false, pre, p8);
 }
 
-// Single-chunk (Cin == 64) halo conv with a 256-pixel block: two groups of
-// four waves (512 threads) own 128 output pixels each and share ONE patch
-// and ONE copy of all nine weight tiles, resident in LDS for the whole
-// block.  The 128-pixel kernels spent most of their time streaming the same
-// 72 KB of weights into every block (512 blocks x 72 KB = 37 MB of L2->LDS
-// traffic per 4.8 GFLOP conv, vs 13 MB of activations); a 256-pixel block
-// halves that, and with every load issued up front each tap waits only for
-// its own tile.  DMA layout: 64-row slabs (8 waves x 8 rows); weight tiles
-// use 64-row slots whatever BN is (rows >= BN read the zero page).
-constexpr int HALO2_CAP = 256;
-constexpr int HALO2_PIECES = 6;                        // 6 x 64 = 384 patch rows
-constexpr int HALO2_PROWS = HALO2_PIECES * 64;
-
-template <int BN>
-struct Halo2Smem {
-  static constexpr int PATCH = HALO2_PROWS * 128;      // 48 KB
-  static constexpr int BT = 64 * 128;                  // one tap's weight slot
-  static constexpr int PIPE = PATCH + 9 * BT;          // 120 KB
-  static constexpr int CTILE = ConvSmem<HALO2_CAP, BN>::CTILE;
-  static constexpr int BYTES = PIPE > CTILE ? PIPE : CTILE;
-};
-
-template <int BN, bool FLIP>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
-conv_halo2_kernel(const ConvParams p) {
-  constexpr int BMG = 128;                    // pixels per group
-  constexpr int MI = BMG / 32, NI = BN / 32;
-  constexpr int PATCH = Halo2Smem<BN>::PATCH;
-  constexpr int BT = Halo2Smem<BN>::BT;
-
-  __shared__ __attribute__((aligned(16))) char smem[Halo2Smem<BN>::BYTES];
-  typedef __attribute__((address_space(3))) char lds_char;
-  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_char*)smem;
-
-  stamp(p, 0);
-  const int gtid = threadIdx.x;                                   // 0..511
-  const int grp = __builtin_amdgcn_readfirstlane(gtid >> 8);     // pixel group
-  const int tid = gtid & 255, lane = tid & 63, wid = tid >> 6;   // within the group
-  const int wm = wid >> 1, wn = wid & 1;
-  const int PB = p.hpb;
-  const int m0 = blockIdx.x * PB;
-  const int n0 = blockIdx.y * BN;
-  const uint32_t wave_off = (uint32_t)__builtin_amdgcn_readfirstlane(gtid >> 6) * 1024u;
-  const bf16_t* const zero = (const bf16_t*)g_zero16;
-
-  const int W = p.W, H = p.H;
-  const int IMGS = p.himgs, RH = p.hrows;
-  const int PW = W + 2, PH = RH + 2;
-  const int grow0 = hdiv(m0, p.dv_W);
-  const int img0 = hdiv(grow0, p.dv_H);
-  const int oh0 = grow0 - img0 * H;
-  EpiPre<HALO2_CAP, BN, 512> pre;
-  epi_prefetch(p, pre, m0, n0, PB, false);
-
-  // DMA lanes: 64 rows (8 per wave) x 8 sixteen-byte chunks, XOR-swizzled
-  const int trow = gtid >> 3;
-  const int chunk = (gtid & 7) ^ (trow & 6);
-  int p_src[HALO2_PIECES];
-  {
-    const int P = IMGS * PH * PW;
-#pragma unroll
-    for (int j = 0; j < HALO2_PIECES; ++j) {
-      const int pr = 64 * j + trow;
-      int off = -1;
-      if (pr < P) {
-        const int img = hdiv(pr, p.dv_PHPW);
-        const int rem = pr - img * PH * PW;
-        const int ir = hdiv(rem, p.dv_PW), ic = rem - ir * PW;
-        const int n = img0 + img;
-        const int ih = oh0 + ir - 1, iw = ic - 1;
-        if (n < p.N && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
-          off = ((n * H + ih) * W + iw) * p.Cin;
-      }
-      p_src[j] = off;
-    }
-  }
-  const int co = n0 + trow;
-  const bool b_ok = trow < BN && co < p.Cout;
-  const bf16_t* const b_row = p.w + (int64_t)(b_ok ? co : 0) * p.Kp + chunk * 8;
-
-  // every DMA up front: the patch, then the nine weight taps in order
-#pragma unroll
-  for (int j = 0; j < HALO2_PIECES; ++j) {
-    const bf16_t* src = p_src[j] >= 0 ? p.x + p_src[j] + chunk * 8 : zero;
-    glds16(src, lds0 + (uint32_t)(j * 64 * 128) + wave_off);
-  }
-#pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    const int wtap = FLIP ? 8 - t : t;
-    glds16(b_ok ? b_row + wtap * p.Cin : zero, lds0 + PATCH + (uint32_t)(t * BT) + wave_off);
-  }
-  stamp(p, 1);
-
-  f32x4 acc[MI][NI];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NI; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  const int frow = lane & 15;
-  const bool p8 = W == 8 && p.perm8 != 0;  // (see perm8)
-  const int g4 = lane >> 4;
-  int a_prow[MI];
-#pragma unroll
-  for (int i = 0; i < MI; ++i) {
-    int ml = grp * BMG + wm * (BMG / 2) + i * 16 + (p8 ? perm8(frow) : frow);
-    if (ml >= PB) ml = 0;                       // idle MFMA row (masked at the store)
-    const int lr = hdiv(ml, p.dv_W), c = ml - lr * W;
-    const int img = hdiv(lr, p.dv_RH), r = lr - img * RH;
-    a_prow[i] = (img * PH + r) * PW + c;
-  }
-  const int bswz = frow & 6;
-
-  // A fragments (patch rows) of tap t+1 are read during tap t: the patch is
-  // resident from tap 0 on, only the weight tile of a tap needs its own wait
-  bf16x8 af[2][2][MI];  // [buffer][kk][i]
-  auto load_a = [&](int tap, int buf) {
-    const int kh = tap / 3, kw = tap - (tap / 3) * 3;
-    const int toff = kh * PW + kw;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int q = kk * 4 + g4;
-#pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        const int pr = a_prow[i] + toff;
-        af[buf][kk][i] = *(const bf16x8*)(smem + pr * 128 + ((q ^ (pr & 6)) * 16));
-      }
-    }
-  };
-#pragma unroll
-  for (int tap = 0; tap < 9; ++tap) {
-    // the patch and weight taps 0..tap have landed: 8 - tap younger DMAs
-    switch (tap) {  // (the loop is unrolled: each case folds to one wait)
-      case 0: vm_wait_barrier<8>(); break;
-      case 1: vm_wait_barrier<7>(); break;
-      case 2: vm_wait_barrier<6>(); break;
-      case 3: vm_wait_barrier<5>(); break;
-      case 4: vm_wait_barrier<4>(); break;
-      case 5: vm_wait_barrier<3>(); break;
-      case 6: vm_wait_barrier<2>(); break;
-      case 7: vm_wait_barrier<1>(); break;
-      default: vm_wait_barrier<0>(); break;
-    }
-    if (tap == 0) {
-      stamp(p, 2);
-      load_a(0, 0);
-    }
-    const char* Bs = smem + PATCH + tap * BT;
-    bf16x8 bfr[2][NI];
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int q = kk * 4 + g4;
-#pragma unroll
-      for (int j = 0; j < NI; ++j)
-        bfr[kk][j] = *(const bf16x8*)(Bs + (wn * (BN / 2) + j * 16 + frow) * 128 + ((q ^ bswz) * 16));
-    }
-    if (tap + 1 < 9) load_a(tap + 1, (tap + 1) & 1);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[tap & 1][kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
-  }
-  __syncthreads();  // every LDS read of the patch / weights done: the C tile aliases them
-  stamp(p, 3);
-  store_c_tile<BMG, BN>((float*)smem, ConvSmem<HALO2_CAP, BN>::CS, acc, grp * BMG, wid, lane, p8);
-  __syncthreads();
-  conv_epilogue_rows<HALO2_CAP, BN, 512>(p, smem, m0, n0, PB, ParClass{}, false, pre);
-  if (p.stamps != nullptr) {
-    __syncthreads();
-    stamp(p, 4);
-  }
-}
-
 // Split-K combine: y = epilogue(sum_z partial[z]) in fixed z order.
 // Cout % 8 == 0: one thread per 8 channels (16-byte traffic).
 __global__ void __launch_bounds__(256) conv_splitk_epilogue(const ConvParams p, int splits) {
@@ -1803,19 +1626,14 @@ bool halo_eligible(ConvParams& p) {
   return halo_geometry(p, p.Cin == BK ? HALO1_PROWS : HALO_PROWS);
 }
 
-// MDA_CONV_HALO2=0: single-chunk convs on the 128-pixel kernel
-bool use_halo2() {
-  static const bool on = [] {
-    const char* e = getenv("MDA_CONV_HALO2");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
+// Halving the channel tile of an 8 x 8 halo conv that has fewer blocks than
+// CUs: off by default since round 6 -- beside the look-ahead teacher the
+// extra blocks cost more than the idle CUs they fill (flagship 0.820 ->
+// 0.810 ms/step without it, profiles/r6_ab.md).  MDA_HALO_NARROW=1: on.
 bool halo_narrow() {
   static const bool on = [] {
     const char* e = getenv("MDA_HALO_NARROW");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return on;
 }
@@ -2039,21 +1857,6 @@ int dispatch(ConvParams& p, int mode, int64_t tile, int64_t splits, hipStream_t 
     if (!(nchunks == 1 && splits == 1 && use_halo1()) &&
         p.himgs * (p.hrows + 2) * (p.W + 2) > HALO_PROWS)
       halo = 0;
-  }
-  if (halo && p.Cin == BK && splits == 1 && use_halo2()) {
-    ConvParams q = p;
-    if (halo_geometry(q, HALO2_PROWS, HALO2_CAP)) {
-      const int bn = q.Cout <= 32 ? 32 : 64;
-      dim3 grid((q.M + q.hpb - 1) / q.hpb, (q.Cout + bn - 1) / bn, 1);
-      if (bn == 32) {
-        if (halo == 2) DLAUNCH((conv_halo2_kernel<32, true>), grid, dim3(512), 0, st, q);
-        else DLAUNCH((conv_halo2_kernel<32, false>), grid, dim3(512), 0, st, q);
-      } else {
-        if (halo == 2) DLAUNCH((conv_halo2_kernel<64, true>), grid, dim3(512), 0, st, q);
-        else DLAUNCH((conv_halo2_kernel<64, false>), grid, dim3(512), 0, st, q);
-      }
-      return (int)hipGetLastError();  // single chunk: no split-K combine
-    }
   }
   if (halo) {  // halo kernel: split over 64-channel chunks, hpb pixels per block
     const int nchunks = p.Cin / BK;
@@ -2381,10 +2184,7 @@ MDA_API int mda_conv_fwd_bnstats(const void* x, const void* w, void* y, float* p
   const int halo = halo_eligible(p) ? 1 : 0;
   // M-blocks of the launch that will run (see dispatch)
   int64_t nblk;
-  ConvParams q2 = p;
-  if (halo && p.Cin == BK && splits == 1 && use_halo2() && halo_geometry(q2, HALO2_PROWS, HALO2_CAP))
-    nblk = (p.M + q2.hpb - 1) / q2.hpb;
-  else if (halo && !(!((Cin / BK) == 1 && splits == 1 && use_halo1()) &&
+  if (halo && !(!((Cin / BK) == 1 && splits == 1 && use_halo1()) &&
                      p.himgs * (p.hrows + 2) * (p.W + 2) > HALO_PROWS))
     nblk = (p.M + p.hpb - 1) / p.hpb;
   else

@@ -92,8 +92,6 @@ CFG.RUNTIME.TEACHER_GRAPH = "split"  # split | fork: the look-ahead teacher as i
                                      # replayed on the teacher stream (split), or forked inside the step graph
 CFG.RUNTIME.TEACHER_FIRST = True     # split: enqueue the teacher graph before the student's
 CFG.RUNTIME.WGRAD_DEFER = True       # captured backward: all layers' wgrad split reductions in one launch
-CFG.RUNTIME.WGRAD_XGRAPH = 0         # >0: captured backward's wgrads as that many small graphs on their own
-                                     # stream, each behind an event node of the step graph (two queues)
 CFG.RUNTIME.WGRAD_STREAM = "auto"    # auto | on | off: captured-backward wgrads on a forked stream (auto: >= 128 px inputs)
 CFG.RUNTIME.FOLD_TEACHER_BN = True   # fold frozen teacher BN into conv weights
 CFG.RUNTIME.PROFILE = False          # torch.profiler trace + hipEvent step times of a window
@@ -110,10 +108,9 @@ CFG.DIST.BUCKET_MB = 0.0             # gradient bucket size (MB of fp32); 0 = au
                                      # total / 4 clamped to [0.5, 8] MB (parallel/grad_reducer.py)
 CFG.DIST.TIMEOUT_S = 600
 CFG.DIST.GRAD_DTYPE = "fp32"         # fp32 | bf16 wire format for gradient all-reduce
-CFG.DIST.GRAPH_COMM = "auto"         # events | split | capture | auto (= events):
+CFG.DIST.GRAPH_COMM = "auto"         # events | split | auto (= events):
                                      # per-bucket all-reduce behind events of the captured backward
-                                     # (events), eager between the fwd+bwd and update graphs (split),
-                                     # or inside one multi-branch graph (capture)
+                                     # (events), or eager between the fwd+bwd and update graphs (split)
 CFG.DIST.BROADCAST_INIT = True       # rank-0 broadcast of all params/buffers at step construction (C2)
 
 # Distillation methods -----------------------------------------------------

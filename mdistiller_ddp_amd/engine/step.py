@@ -15,9 +15,9 @@ This is the hot loop of the reference (`engine/trainer.py:257-321` base,
   GPU a CIFAR distillation step is ~300-600 small kernels, so this removes
   the dominant (launch-bound) cost.  With world > 1 the collectives stay
   outside the captured graphs (forward/backward graph -> RCCL all-reduce ->
-  optimizer graph) unless ``DIST.GRAPH_COMM`` captures them: with RCCL the
-  bucketed all-reduces are recorded inside the single step graph, issued
-  from the backward hooks, so they overlap the remaining backward kernels.
+  optimizer graph); with ``DIST.GRAPH_COMM=events`` (the default) each
+  bucket's all-reduce is launched right after the replay, behind an event
+  node of the captured backward, so it overlaps the remaining backward.
 * **Flat parameters** (:mod:`.optim`) -> one all-reduce, one optimizer launch.
 * **DOT** runs its two backwards into the two halves of one ``[2, n]``
   gradient buffer and reduces both with one collective (fixes SURVEY D4).
@@ -268,33 +268,27 @@ class TrainStep:
         self._wg_auto = False
         self._wg_stream = None
         self.wgrad_defer = self.device.type == "cuda" and bool(cfg.RUNTIME.get("WGRAD_DEFER", True))
-        self.wgrad_xgraph = int(cfg.RUNTIME.get("WGRAD_XGRAPH", 0)) if self.device.type == "cuda" else 0
-        self._wgraph = None     # (wgrad graph, its stream, queued launches) of the two-graph backward
 
     def _graph_comm_mode(self, cfg):
         """How the gradient all-reduce meets the captured step at world > 1.
 
         ``False`` (split): fwd+bwd graph -> eager bucketed all-reduce -> optimizer
-        graph.  ``"events"``: the same two graphs, but the captured backward
-        records one external event per gradient bucket and the all-reduces are
-        enqueued right after the replay launch on a comm stream, each behind
-        its bucket's event, so they overlap the rest of the backward
-        (GradReducer.arm_capture).  ``True`` (capture): the all-reduce inside
-        the single step graph (a multi-branch graph, slow on ROCm's executor).
-        ``auto`` = events (DOT with its two backward graphs: split).
+        graph.  ``"events"`` (auto): the same two graphs, but the captured
+        backward records one external event per gradient bucket and the
+        all-reduces are enqueued right after the replay launch on a comm
+        stream, each behind its bucket's event, so they overlap the rest of the
+        backward (GradReducer.arm_capture).  (An all-reduce captured inside the
+        step graph needs a multi-branch graph, slow on ROCm's executor: not
+        offered.)
         """
         if self.world <= 1 or not self.use_graph:
             return False
         mode = str(cfg.DIST.get("GRAPH_COMM", "auto")).lower()
-        import torch.distributed as dist
-        rccl = dist.get_backend() == "nccl"
-        if mode == "capture":
-            if not rccl:
-                raise ValueError("DIST.GRAPH_COMM=capture needs the RCCL (nccl) backend")
-            return True
         if mode in ("events", "auto"):
             return "events"
-        return False  # split
+        if mode == "split":
+            return False
+        raise ValueError(f"DIST.GRAPH_COMM={mode!r}: expected auto | events | split")
 
     # ------------------------------------------------------------------
     def set_epoch(self, epoch: float) -> None:
@@ -460,8 +454,7 @@ class TrainStep:
         """While a backward is being captured (and the wgrads stay on the main
         stream), defer every layer's split reduction to one multi-layer launch
         at the end of the backward (``hip_train.set_wgrad_defer``)."""
-        if not (self.wgrad_defer and torch.cuda.is_current_stream_capturing()) or \
-                self.graph_comm is True:
+        if not (self.wgrad_defer and torch.cuda.is_current_stream_capturing()):
             return False
         from ..ops import hip_train
         hip_train.set_wgrad_defer(True)
@@ -554,9 +547,9 @@ class TrainStep:
     def _reduce(self, replay: bool = False):
         """The step's collectives: the gradient all-reduce, then any exchange the
         distiller staged after its backward (CRD's memory-update all-gather).
-        Eager between the fwd+bwd and update graphs (split mode), captured in
-        the one graph in ``DIST.GRAPH_COMM=capture`` mode; after a replay in
-        ``events`` mode each bucket's all-reduce waits only for its event."""
+        Eager between the fwd+bwd and update graphs (split mode); after a
+        replay in ``events`` mode each bucket's all-reduce waits only for its
+        event."""
         if self.world <= 1:
             return
         if replay and self.graph_comm == "events" and self.reducer.graph_events is not None:
@@ -621,7 +614,7 @@ class TrainStep:
             # back to MIOpen on some layer): stay eager for good
             self.use_graph = False
             return out
-        if self.is_dot and self.dot_dual and not self.dot_single and self.graph_comm is not True:
+        if self.is_dot and self.dot_dual and not self.dot_single:
             try:
                 return self._capture_dot_dual(static, pool, s, out)
             finally:
@@ -713,20 +706,9 @@ class TrainStep:
 
     def _capture_step(self, static, pool, s):
         g1 = torch.cuda.CUDAGraph()
-        if self.wgrad_xgraph and not self.is_dot and self.graph_comm is not True:
-            return self._capture_step_xgraph(static, pool, s)
         if self.world <= 1:
             with torch.cuda.graph(g1, pool=pool, stream=s):
                 preds, losses = self._fwd_bwd(static, overlap_comm=False)
-                self._update(preds, static["target"], losses)
-            g2 = None
-        elif self.graph_comm is True:
-            # one graph: bucket all-reduces are issued from the backward hooks
-            # while the rest of backward is being captured, so the replayed
-            # DAG overlaps them with the remaining gradient kernels
-            with torch.cuda.graph(g1, pool=pool, stream=s):
-                preds, losses = self._fwd_bwd(static, overlap_comm=True)
-                self._reduce()
                 self._update(preds, static["target"], losses)
             g2 = None
         else:
@@ -740,66 +722,11 @@ class TrainStep:
         self._graphs = (g1, g2)
         self._static = (static, preds.detach(), {k: v.detach() for k, v in losses.items()})
 
-    def _capture_step_xgraph(self, static, pool, s):
-        """Two-queue backward (RUNTIME.WGRAD_XGRAPH = G > 0 groups): the step
-        graph without the weight-gradient GEMMs -- each conv backward adds an
-        event-record node once its dy exists -- then the queued wgrad launches
-        captured as G small graphs on their own stream and memory pool.  A
-        replay enqueues, on that stream, "wait for the last event of group g,
-        replay group g's graph" for every group (a wait on a node of a replayed
-        graph from outside it works on this ROCm; a wait NODE in another graph
-        does not, scripts/graph_external_event_probe.py), then the update graph
-        once both streams are done."""
-        from ..ops import hip_train
-        from ..runtime.streams import _fresh_stream
-        g1, g_u = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g1, pool=pool, stream=s):
-            hip_train.set_wgrad_xgraph(True)
-            try:
-                preds, losses = self._fwd_bwd(static, overlap_comm=False)
-            finally:
-                items = hip_train.take_wgrad_xgraph()
-        ws = self._wg_stream = self._wg_stream or _fresh_stream(self.device.index or 0, (s,))
-        ws.wait_stream(s)
-        G = max(1, min(int(self.wgrad_xgraph), len(items)))
-        bounds = [round(i * len(items) / G) for i in range(G + 1)]
-        wpool = torch.cuda.graph_pool_handle()
-        groups = []
-        hip_train.set_wgrad_defer(True)
-        try:
-            for gi in range(G):
-                part = items[bounds[gi]:bounds[gi + 1]]
-                if not part:
-                    continue
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=wpool, stream=ws):
-                    for _, fn, _ in part:
-                        fn()
-                    if gi == G - 1:
-                        hip_train.flush_wgrad_reduces()  # every layer's split reduction
-                groups.append((part[-1][0], g))
-        finally:
-            hip_train.set_wgrad_defer(False)
-        s.wait_stream(ws)
-        with torch.cuda.graph(g_u, pool=pool, stream=s):
-            self._update(preds, static["target"], losses)
-        self._bn_end()
-        self._graphs = (g1, g_u)
-        self._wgraph = (groups, ws, items)
-        self._static = (static, preds.detach(), {k: v.detach() for k, v in losses.items()})
-
     def _replay_main(self):
-        """Replay the captured step graph(s) on the current stream (+ the wgrad
-        graph on its stream, + the eager collectives between graphs)."""
+        """Replay the captured step graph(s) on the current stream (+ the eager
+        collectives between graphs)."""
         g1, g2 = self._graphs
         g1.replay()
-        if self._wgraph is not None:
-            groups, ws, _ = self._wgraph
-            for ev, g in groups:
-                ev.wait(ws)  # the replay has reached this group's last dy
-                with torch.cuda.stream(ws):
-                    g.replay()
-            torch.cuda.current_stream().wait_stream(ws)
         if g2 is not None:
             self._reduce(replay=True)
             g2.replay()
@@ -1055,7 +982,6 @@ class TrainStep:
     def invalidate_graph(self) -> None:
         """Drop captured graphs (shape change, e.g. the last partial batch)."""
         self._graphs = None
-        self._wgraph = None
         self._static = None
         self._dual = None
         self._drop_feed()

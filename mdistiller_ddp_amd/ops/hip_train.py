@@ -314,36 +314,10 @@ def _conv_wgrad(x, dy, target, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, 
               pad, Kp, sp, 1.0, 1 if direct else 0, cin_keep, groups, nsets, gstride)
 
 
-_WG_XG = [None]  # [(event, launch fn, inputs)] while a backward is captured for a wgrad graph
-
-
-def set_wgrad_xgraph(on: bool) -> None:
-    """Arm / disarm the two-graph backward (``RUNTIME.WGRAD_XGRAPH``): while
-    armed, each native conv backward captured into the step graph records an
-    EXTERNAL event once its dy exists and queues its weight-gradient launch
-    instead of issuing it; the training step then captures the queued
-    launches, each behind its event, as a second single-chain graph replayed
-    on its own stream beside the step graph (a fork inside one graph costs
-    ROCm's executor several us per kernel, scripts/launch_floor_probe.py)."""
-    _WG_XG[0] = [] if on else None
-
-
-def take_wgrad_xgraph():
-    items, _WG_XG[0] = _WG_XG[0], None
-    return items or []
-
-
 def _wgrad_launch(fn, direct, *tensors):
     """Run ``fn`` (a wgrad launch sequence) on the armed side stream when its
     result goes straight into the flat gradient; inputs are recorded as used
     there so the allocator does not hand their memory out early."""
-    xg = _WG_XG[0]
-    if xg is not None and direct:
-        from ..runtime.streams import HipEvent
-        ev = HipEvent()
-        ev.record(external=True)
-        xg.append((ev, fn, tensors))  # the refs keep x / dy out of the pool's reuse
-        return
     s = _WG_SIDE[0]
     if s is None or not direct:
         fn()

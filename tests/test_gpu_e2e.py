@@ -132,10 +132,9 @@ def test_validation_sees_updated_weights(tmp_path):
     assert abs(v2[0] - v2_ref[0]) <= 3.0, (v2, v2_ref)
 
 
-@pytest.mark.parametrize("trainer,student,xgraph", [("base", "resnet8x4", False), ("dot", "resnet8x4", False),
-                                                    ("base", "MobileNetV2", False), ("base", "ShuffleV1", False),
-                                                    ("base", "resnet8x4", True), ("base", "MobileNetV2", True)])
-def test_native_bf16_graph_matches_eager(trainer, student, xgraph):
+@pytest.mark.parametrize("trainer,student", [("base", "resnet8x4"), ("dot", "resnet8x4"),
+                                             ("base", "MobileNetV2"), ("base", "ShuffleV1")])
+def test_native_bf16_graph_matches_eager(trainer, student):
     """20 steps of the NATIVE bf16 path (HIP conv/BN/loss/optimizer kernels):
     hipGraph replay vs eager launches of the same kernels (the captured step
     defers every dense and depthwise weight-gradient reduction into one
@@ -144,8 +143,6 @@ def test_native_bf16_graph_matches_eager(trainer, student, xgraph):
     torch.manual_seed(0)
     cfg = _cfg("DKD" if trainer == "base" else "KD", trainer)
     cfg.DISTILLER.STUDENT = student
-    # xgraph: the weight gradients as a second graph behind external events
-    cfg.RUNTIME.WGRAD_XGRAPH = 3 if xgraph else 0
     d1 = build_distiller(cfg, 100, "cuda")
     d2 = copy.deepcopy(d1)
     outs = []
@@ -158,8 +155,6 @@ def test_native_bf16_graph_matches_eager(trainer, student, xgraph):
             st.step(b)
         torch.cuda.synchronize()
         assert (st._graphs is not None) == g
-        if g:
-            assert (st._wgraph is not None) == xgraph
         outs.append(st.flat.data.clone())
     rel = (outs[0] - outs[1]).norm() / outs[1].norm()
     assert rel < 1e-2, rel

@@ -576,6 +576,7 @@ MDA_API int mda_bn_finalize(const float* partial, int64_t nblk, int64_t M, int64
 // apply) launches per layer before; dout2 folds the gradient add of a
 // residual fork (two consumers of one activation) into the same pass.
 #include "bnslot.h"
+#include "bnbwd.h"
 #include <cstdlib>
 
 namespace {
@@ -748,100 +749,10 @@ bn_apply_fin_kernel(const bf16_t* __restrict__ y, BnRegion* __restrict__ reg, in
   }
 }
 
-struct BwdArgs {
-  const bf16_t* dout; const bf16_t* dout2; const bf16_t* dpre;
-  const bf16_t* y; const bf16_t* res;
-  const float* stats;    // [4][C] mean, rstd, scale, shift
-  bf16_t* dy; bf16_t* dres;
-  float* dgamma; float* dbeta; float* sums;   // accumulated / written by block 0 (each may be null)
-  BnRegion* reg;
-  unsigned* err;
-  int M, C, act;
-  // optional: the residual came from another training BN with no activation
-  // (a projection shortcut): its dout IS dres, so this pass also adds that
-  // layer's sum dres and sum dres*xhat_r (ry = its BN input, rstats = its
-  // [4][C] stats) into rreg -- its backward is then one streaming pass too
-  const bf16_t* ry; const float* rstats; BnRegion* rreg;
-  // optional: `res` is the RAW input of another training BN (a projection
-  // shortcut whose apply was folded into this layer's, mda_bn_apply_fin_vr):
-  // the residual value is res * vres[2C + c] + vres[3C + c] (vres = that
-  // layer's [4][C] stats)
-  const float* vres;
-  // DOT single-pass backward (two stacked cotangents): gridDim.y = 2 sets;
-  // set 1's dout / dout2 / dpre / dy / dres start dd elements later, its
-  // dgamma / dbeta / sums dg floats later (the other gradient set of the flat
-  // buffer, may be negative) and its reg / rreg dr bytes later.  y, res, ry
-  // and every stats operand are the forward's, shared by both sets.
-  int64_t dd, dg, dr;
-};
-
-__device__ __forceinline__ void dual_shift(BwdArgs& a) {
-  if (blockIdx.y == 0) return;
-  if (a.dout) a.dout += a.dd;
-  if (a.dout2) a.dout2 += a.dd;
-  if (a.dpre) a.dpre += a.dd;
-  if (a.dy) a.dy += a.dd;
-  if (a.dres) a.dres += a.dd;
-  if (a.dgamma) a.dgamma += a.dg;
-  if (a.dbeta) a.dbeta += a.dg;
-  if (a.sums) a.sums += a.dg;
-  if (a.reg) a.reg = (BnRegion*)((char*)a.reg + a.dr);
-  if (a.rreg) a.rreg = (BnRegion*)((char*)a.rreg + a.dr);
-}
-
-// res-producer sums of one 8-channel vector (dz = the stored dres values)
-__device__ __forceinline__ void rsum_add8(const BwdArgs& a, int64_t o, int c0, const uint32_t (&ro)[4],
-                                          float (&r1)[8], float (&r2)[8]) {
-  const uint4 yv = *(const uint4*)(a.ry + o);
-  const uint32_t yw[4] = {yv.x, yv.y, yv.z, yv.w};
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int w = e >> 1;
-    const float d = (e & 1) ? __uint_as_float(ro[w] & 0xffff0000u) : __uint_as_float(ro[w] << 16);
-    const float yf = (e & 1) ? __uint_as_float(yw[w] & 0xffff0000u) : __uint_as_float(yw[w] << 16);
-    r1[e] += d;
-    r2[e] += d * ((yf - a.rstats[c0 + e]) * a.rstats[a.C + c0 + e]);
-  }
-}
-
-struct Raw8 { uint4 y, d, d2, p, r; };
-
-__device__ __forceinline__ void bwd_load8(const BwdArgs& a, int64_t o, Raw8& v) {
-  v.y = *(const uint4*)(a.y + o);
-  v.d = a.dout ? *(const uint4*)(a.dout + o) : make_uint4(0, 0, 0, 0);
-  v.d2 = a.dout2 ? *(const uint4*)(a.dout2 + o) : make_uint4(0, 0, 0, 0);
-  v.p = a.dpre ? *(const uint4*)(a.dpre + o) : make_uint4(0, 0, 0, 0);
-  v.r = (a.res && a.act != ACT_NONE) ? *(const uint4*)(a.res + o) : make_uint4(0, 0, 0, 0);
-}
-
-// dz of 8 channels (z recomputed from y: no stored mask)
-__device__ __forceinline__ void bwd_dz8(const BwdArgs& a, const Raw8& v, const float* sc,
-                                        const float* sh, float (&dz)[8], const float* vsc,
-                                        const float* vsh) {
-  const uint32_t yw[4] = {v.y.x, v.y.y, v.y.z, v.y.w}, dw[4] = {v.d.x, v.d.y, v.d.z, v.d.w};
-  const uint32_t d2w[4] = {v.d2.x, v.d2.y, v.d2.z, v.d2.w}, pw[4] = {v.p.x, v.p.y, v.p.z, v.p.w};
-  const uint32_t rw[4] = {v.r.x, v.r.y, v.r.z, v.r.w};
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int w = k >> 1;
-    const bool hi = k & 1;
-    auto f = [&](uint32_t u) { return hi ? __uint_as_float(u & 0xffff0000u) : __uint_as_float(u << 16); };
-    float d = f(dw[w]);
-    if (a.dout2) d += f(d2w[w]);
-    if (a.act != ACT_NONE) {
-      float z = f(yw[w]) * sc[k] + sh[k];
-      if (a.res) z += a.vres ? f(rw[w]) * vsc[k] + vsh[k] : f(rw[w]);
-      d *= act_grad(z, a.act);
-    }
-    if (a.dpre) d += f(pw[w]);
-    dz[k] = d;
-  }
-}
-
 template <int VPT, bool HOLD>
 __global__ void __launch_bounds__(256)
 bn_bwd_fused_kernel(BwdArgs a) {
-  dual_shift(a);
+  dual_shift(a, blockIdx.y);
   __shared__ float s_m0[SLOT_CMAX], s_m1[SLOT_CMAX];
   const int C = a.C, M = a.M;
   const int C8 = C / 8;
@@ -980,7 +891,7 @@ bn_bwd_fused_kernel(BwdArgs a) {
 // re-read y / dout with 4 waves per CU (70 us for a 64 x 112^2 x 64 layer).
 __global__ void __launch_bounds__(256)
 bn_bwd_sums_kernel(BwdArgs a) {
-  dual_shift(a);
+  dual_shift(a, blockIdx.y);
   const int C = a.C, M = a.M;
   const int C8 = C / 8;
   const int rpi = 256 / C8;
@@ -1015,95 +926,13 @@ _Pragma("unroll")
 
 // BN backward whose channel sums a producer already added into the region
 // (the dgrad epilogue of the consuming conv, conv_igemm.hip
-// mda_conv_dgrad_bnsum): one streaming pass, no reduction and no grid
-// barrier.  dz = dout * act'(z) (+ dpre), dy = scale*(dz - (sum dz +
-// xhat*sum dz*xhat)/M), dres = dz; block 0 accumulates dgamma / dbeta (and
-// writes sums).  The thread's V vectors are loaded before the
-// prologue reads the region, so both latencies overlap.
+// mda_conv_dgrad_bnsum): one streaming pass (bnbwd.h bn_bwd_apply_body).
 template <int V>
 __global__ void __launch_bounds__(256)
 bn_bwd_apply_reg_kernel(BwdArgs a) {
-  dual_shift(a);
-  // per-channel operands in LDS (dynamic, 8C floats): a thread's channel group
-  // changes along the grid stride when C / 8 is not a power of two
-  // (MobileNetV2 widths)
   extern __shared__ float s_dyn[];
-  const int C = a.C;
-  float* const s_m0 = s_dyn;
-  float* const s_m1 = s_dyn + C;
-  float* const s_st0 = s_dyn + 2 * C;  // [4][C] mean, rstd, scale, shift
-  float* const s_vr0 = s_dyn + 6 * C;  // [2][C] virtual-residual scale, shift
-  const int c8 = C / 8;
-  const int64_t total = (int64_t)a.M * c8;
-  const int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  Raw8 raw[V];
-#pragma unroll
-  for (int k = 0; k < V; ++k) {
-    const int64_t i = i0 + k * stride;
-    bwd_load8(a, (i < total ? i : 0) * 8, raw[k]);
-  }
-  {
-    const float invM = 1.f / (float)a.M;
-    for (int c = threadIdx.x; c < C; c += blockDim.x) {
-      double d0, d1;
-      region_channel<false>(a.reg, C, c, d0, d1);
-      const float t0 = (float)d0, t1 = (float)d1;
-      s_m0[c] = t0 * invM;
-      s_m1[c] = t1 * invM;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) s_st0[q * C + c] = a.stats[q * C + c];
-      s_vr0[c] = a.vres ? a.vres[2 * C + c] : 1.f;
-      s_vr0[C + c] = a.vres ? a.vres[3 * C + c] : 0.f;
-      if (blockIdx.x == 0) {
-        if (a.sums) { a.sums[c] = t0; a.sums[C + c] = t1; }
-        if (a.dbeta) a.dbeta[c] += t0;
-        if (a.dgamma) a.dgamma[c] += t1;
-      }
-    }
-  }
-  __syncthreads();
-  float r1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, r2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  auto emit = [&](int64_t i, const Raw8& v) {
-    const int c0 = (int)(i % c8) * 8;
-    float sc[8], sh[8], mu[8], rs[8], dz[8], vsc[8], vsh[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      mu[e] = s_st0[c0 + e]; rs[e] = s_st0[C + c0 + e];
-      sc[e] = s_st0[2 * C + c0 + e]; sh[e] = s_st0[3 * C + c0 + e];
-      vsc[e] = s_vr0[c0 + e]; vsh[e] = s_vr0[C + c0 + e];
-    }
-    bwd_dz8(a, v, sc, sh, dz, vsc, vsh);
-    const uint32_t yw[4] = {v.y.x, v.y.y, v.y.z, v.y.w};
-    uint32_t go[4], ro[4];
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      float g[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int e = 2 * w + h;
-        const float yf = h ? __uint_as_float(yw[w] & 0xffff0000u) : __uint_as_float(yw[w] << 16);
-        const float xhat = (yf - mu[e]) * rs[e];
-        g[h] = sc[e] * (dz[e] - (s_m0[c0 + e] + xhat * s_m1[c0 + e]));
-      }
-      go[w] = pack_bf16x2(g[0], g[1]);
-      ro[w] = pack_bf16x2(dz[2 * w], dz[2 * w + 1]);
-    }
-    *(uint4*)(a.dy + i * 8) = make_uint4(go[0], go[1], go[2], go[3]);
-    if (a.dres) *(uint4*)(a.dres + i * 8) = make_uint4(ro[0], ro[1], ro[2], ro[3]);
-    if (a.rreg) rsum_add8(a, i * 8, c0, ro, r1, r2);  // (the host checks: fixed channel group)
-  };
-#pragma unroll
-  for (int k = 0; k < V; ++k) {
-    const int64_t i = i0 + k * stride;
-    if (i < total) emit(i, raw[k]);
-  }
-  for (int64_t i = i0 + V * stride; i < total; i += stride) {
-    Raw8 v;
-    bwd_load8(a, i * 8, v);
-    emit(i, v);
-  }
-  if (a.rreg) region_block_add(a.rreg, r1, r2, C, 256 / c8);
+  dual_shift(a, blockIdx.y);
+  bn_bwd_apply_body<V>(a, s_dyn, (int)blockIdx.x, (int)gridDim.x);
 }
 
 int g_num_cus = 0;
@@ -1120,13 +949,6 @@ int num_cus() {
   return g_num_cus;
 }
 
-// power-of-two block count for the apply kernels
-inline int apply_blocks(int64_t n8, int vpt) {
-  const int64_t want = (n8 + 256 * (int64_t)vpt - 1) / (256 * (int64_t)vpt);
-  int64_t b = 1;
-  while (b < want && b < 1024) b <<= 1;
-  return (int)b;
-}
 
 // Vectors per thread of a streaming apply launch.  Fewer vectors and more
 // blocks for small layers (>= 2 blocks per CU) measured the same on the
@@ -1142,7 +964,7 @@ int launch_apply_fin(int v, dim3 g, size_t lds, hipStream_t st, A... args) {
 
 int launch_bwd_apply(int v, dim3 g, int C, hipStream_t st, const BwdArgs& a) {
   if (v != 4) return (int)hipErrorInvalidValue;
-  const size_t lds = (size_t)8 * C * sizeof(float);
+  const size_t lds = (size_t)bn_apply_lds_bytes(C, 256, a.rreg != nullptr);
   hipLaunchKernelGGL(bn_bwd_apply_reg_kernel<4>, g, dim3(256), lds, st, a);
   return (int)hipGetLastError();
 }

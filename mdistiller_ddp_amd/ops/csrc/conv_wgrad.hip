@@ -18,6 +18,8 @@
 //         optionally, bf16 [Cin][KpT] with k = (kh*KW+kw)*Cout + co (dgrad
 //         operand), in one launch per conv per step.
 #include "common.h"
+#include "bnslot.h"
+#include "bnbwd.h"
 
 extern uint64_t* g_stamps;  // csrc/conv_igemm.hip (mda_conv_set_stamps)
 
@@ -69,11 +71,25 @@ struct WgParams {
   uint64_t* stamps;  // diagnostics: per-block phase stamps (mda_conv_set_stamps), else null
 };
 
-__device__ __forceinline__ void wg_stamp(const WgParams& p, int k) {
-  if (p.stamps != nullptr && threadIdx.x == 0) {
-    const int b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-    p.stamps[(int64_t)b * 8 + k] = __builtin_amdgcn_s_memrealtime();
-  }
+// A GEMM block's position in its (co tile, k tile, split) grid.  The
+// stand-alone kernels take it from blockIdx; the fused launches
+// (wgrad + BN-backward apply, mda_conv_wgrad_nored_bn) from the block's
+// linear index, in the same x-fastest order.
+struct VB {
+  int x, y, z, gx, gy, gz;
+  __device__ int lin() const { return x + gx * (y + gy * z); }
+};
+__device__ __forceinline__ VB vb_hw() {
+  return VB{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z,
+            (int)gridDim.x, (int)gridDim.y, (int)gridDim.z};
+}
+__device__ __forceinline__ VB vb_lin(int b, int gx, int gy, int gz) {
+  return VB{b % gx, (b / gx) % gy, b / (gx * gy), gx, gy, gz};
+}
+
+__device__ __forceinline__ void wg_stamp(const WgParams& p, int k, const VB& vb) {
+  if (p.stamps != nullptr && threadIdx.x == 0)
+    p.stamps[(int64_t)vb.lin() * 8 + k] = __builtin_amdgcn_s_memrealtime();
 }
 
 constexpr uint32_t OOB = 0x80000000u;
@@ -108,17 +124,18 @@ __device__ __forceinline__ bf16x8 tr_frag(const bf16_t* tile, int r0, int c0, in
   return out;
 }
 
+constexpr int WG_REG_SMEM = 4 * TM * ROW * 2;  // Ds[2] + Xs[2] bf16 tiles
+
 template <int MODE>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
-conv_wgrad_kernel(const WgParams p) {
-  __shared__ __attribute__((aligned(16))) bf16_t Ds[2][TM * ROW];  // dy tile [m][co]
-  __shared__ __attribute__((aligned(16))) bf16_t Xs[2][TM * ROW];  // im2col tile [m][k]
+__device__ __forceinline__ void wgrad_reg_body(const WgParams& p, char* smem, const VB& vb) {
+  bf16_t (*Ds)[TM * ROW] = (bf16_t (*)[TM * ROW])smem;                  // dy tile [m][co]
+  bf16_t (*Xs)[TM * ROW] = (bf16_t (*)[TM * ROW])(smem + 2 * TM * ROW * 2);  // im2col tile [m][k]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  const int co0 = blockIdx.x * TC;
-  const int k0 = blockIdx.y * TK;
-  const int zset = (int)blockIdx.z / p.zsp;
-  const int m_begin = ((int)blockIdx.z - zset * p.zsp) * p.m_per_split;
+  const int co0 = vb.x * TC;
+  const int k0 = vb.y * TK;
+  const int zset = vb.z / p.zsp;
+  const int m_begin = (vb.z - zset * p.zsp) * p.m_per_split;
   const int m_end = min(p.M, m_begin + p.m_per_split);
   const int chunk = tid & 7, row = tid >> 3;  // 32 rows x 8 chunks per pass, 2 passes
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(p.x, p.x_bytes);
@@ -240,8 +257,15 @@ conv_wgrad_kernel(const WgParams p) {
         const int oc = co0 + wm * 32 + i * 16 + erow + r;
         const int k = k0 + wn * 32 + j * 16 + ecol;
         if (oc < p.Cout && k < p.Kp)
-          p.partial[((int64_t)blockIdx.z * p.Cout + oc) * p.Kp + k] = acc[i][j][r];
+          p.partial[((int64_t)vb.z * p.Cout + oc) * p.Kp + k] = acc[i][j][r];
       }
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+conv_wgrad_kernel(const WgParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[WG_REG_SMEM];
+  wgrad_reg_body<MODE>(p, smem, vb_hw());
 }
 
 // ---------------------------------------------------------------------------
@@ -289,23 +313,24 @@ template <int TCo, int TKk>
 struct WgOcc { static constexpr int W = (TCo * TKk >= 16384) ? 1 : 3; };
 
 template <int TCo, int TKk>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WgOcc<TCo, TKk>::W)))
-conv_wgrad_glds_kernel(const WgParams p) {
+struct WgGlds { static constexpr int BYTES = WG_NBUF * (TCo / 64 + TKk / 64) * 64 * 128; };
+
+template <int TCo, int TKk>
+__device__ __forceinline__ void wgrad_glds_body(const WgParams& p, char* smem, const VB& vb) {
   constexpr int SC = TCo / 64, SK = TKk / 64;  // 64-wide subtiles of dy / im2col(x)
   constexpr int SUB = 64 * 128;                // bytes per [64 px][64 ch] subtile
   constexpr int STAGE = (SC + SK) * SUB;
   constexpr int NL = 2 * (SC + SK);            // DMA instructions per wave per stage
   constexpr int MI = TCo / 32, NI = TKk / 32;  // 16x16 tiles per wave (wave tile TCo/2 x TKk/2)
-  __shared__ __attribute__((aligned(16))) char smem[WG_NBUF * STAGE];
   typedef __attribute__((address_space(3))) char lds_char;
   const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_char*)smem;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  const int co0 = blockIdx.x * TCo;
-  const int k0 = blockIdx.y * TKk;
-  const int zset = (int)blockIdx.z / p.zsp;
-  const int m_begin = ((int)blockIdx.z - zset * p.zsp) * p.m_per_split;
+  const int co0 = vb.x * TCo;
+  const int k0 = vb.y * TKk;
+  const int zset = vb.z / p.zsp;
+  const int m_begin = (vb.z - zset * p.zsp) * p.m_per_split;
   const int m_end = min(p.M, m_begin + p.m_per_split);
   const bf16_t* const dyp = p.dy + (int64_t)zset * p.M * p.Cout;
   const uint32_t wave_off = (uint32_t)__builtin_amdgcn_readfirstlane(wid) * 1024u;
@@ -440,8 +465,15 @@ conv_wgrad_glds_kernel(const WgParams p) {
         const int oc = co0 + wm * (TCo / 2) + i * 16 + erow + r;
         const int k = k0 + wn * (TKk / 2) + j * 16 + ecol;
         if (oc < p.Cout && k < p.Kp)
-          p.partial[((int64_t)blockIdx.z * p.Cout + oc) * p.Kp + k] = acc[i][j][r];
+          p.partial[((int64_t)vb.z * p.Cout + oc) * p.Kp + k] = acc[i][j][r];
       }
+}
+
+template <int TCo, int TKk>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WgOcc<TCo, TKk>::W)))
+conv_wgrad_glds_kernel(const WgParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[WgGlds<TCo, TKk>::BYTES];
+  wgrad_glds_body<TCo, TKk>(p, smem, vb_hw());
 }
 
 // ---------------------------------------------------------------------------
@@ -477,9 +509,7 @@ __device__ __forceinline__ int wgh_swz(int ir, int ic) {
   return (((ic >> 1) & 1) | ((((ic >> 3) ^ ir) & 1) << 1)) << 1;
 }
 
-__global__ void __launch_bounds__(WGH_NT)
-conv_wgrad_halo_kernel(const WgParams p) {
-  __shared__ __attribute__((aligned(16))) char smem[WGH_RING * WGH_STAGE];
+__device__ __forceinline__ void wgrad_halo_body(const WgParams& p, char* smem, const VB& vb) {
   typedef __attribute__((address_space(3))) char lds_char;
   const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_char*)smem;
 
@@ -489,9 +519,9 @@ conv_wgrad_halo_kernel(const WgParams p) {
   // XCD-aware block order: hardware block b runs on XCD b % 8; each XCD gets a
   // contiguous run of (co tile, ci tile, split) in that order, so the blocks
   // that read the same x chunk / dy chunk of a split share an L2
-  const int gx = gridDim.x, gy = gridDim.y;
-  const int nwg = gx * gy * gridDim.z;
-  const int bid = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const int gx = vb.gx, gy = vb.gy;
+  const int nwg = gx * gy * vb.gz;
+  const int bid = vb.lin();
   int wg = bid;
   {
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
@@ -507,7 +537,7 @@ conv_wgrad_halo_kernel(const WgParams p) {
   const bf16_t* const zero = (const bf16_t*)g_wg_zero16;
   const int W = p.W, H = p.H, HW = H * W;
   const int RH = p.h_rh, PW = W + 2, PHPW = (RH + 2) * PW, P = p.h_img * PHPW;
-  wg_stamp(p, 0);
+  wg_stamp(p, 0, vb);
 
   // Stage layout: patch rows [0, 160) (byte 0), dy rows after (byte WGH_XB).
   // A DMA instruction writes 8 rows of 128 B (lane-linear);
@@ -629,21 +659,21 @@ conv_wgrad_halo_kernel(const WgParams p) {
   const int n = (m_end - m_begin + 63) / 64;
 #pragma unroll
   for (int s0 = 0; s0 < WGH_RING - 1; ++s0) issue(m_begin + s0 * 64, s0);
-  wg_stamp(p, 1);
+  wg_stamp(p, 1, vb);
   int cbuf = 0;
   for (int t = 0; t < n; ++t) {
     // loaders: stage t landed (the 7 DMAs of each of the RING - 2 younger
     // stages still in flight); the barrier publishes it and retires every
     // wave's reads of the slot stage t + RING - 1 overwrites (stage t - 1's)
     wg_wait_barrier<7 * (WGH_RING - 2)>();
-    if (t == 0) wg_stamp(p, 2);
+    if (t == 0) wg_stamp(p, 2, vb);
     const int ibuf = cbuf == 0 ? WGH_RING - 1 : cbuf - 1;  // (t + RING - 1) % RING
     issue(m_begin + (t + WGH_RING - 1) * 64, ibuf);
     compute(smem + cbuf * WGH_STAGE);
     cbuf = cbuf == WGH_RING - 1 ? 0 : cbuf + 1;
   }
   wg_wait_barrier<0>();  // zero-page prefetches drained, every fragment read retired
-  wg_stamp(p, 3);
+  wg_stamp(p, 3, vb);
 
   // partials: round kw stages the three taps (kh, kw) of all groups, then
   // 16-byte stores along k (partial[z][co][tap * Cin + ci])
@@ -669,8 +699,48 @@ conv_wgrad_halo_kernel(const WgParams p) {
   }
   if (p.stamps != nullptr) {
     __syncthreads();
-    wg_stamp(p, 4);
+    wg_stamp(p, 4, vb);
   }
+}
+
+__global__ void __launch_bounds__(WGH_NT)
+conv_wgrad_halo_kernel(const WgParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[WGH_RING * WGH_STAGE];
+  wgrad_halo_body(p, smem, vb_hw());
+}
+
+// ---------------------------------------------------------------------------
+// A weight-gradient GEMM and the streaming BN-backward apply of the layer
+// below it in ONE launch (mda_conv_wgrad_nored_bn).  Neither depends on the
+// other -- the GEMM reads this conv's dy and x, the apply reads the dgrad
+// output of this conv -- and back to back each left most CUs idle (the
+// flagship's backward: 128-512-block applies after 16-288-block GEMMs).
+// Blocks [0, nw) are the GEMM's (x-fastest order of its 3-D grid), the rest
+// the apply's; the apply runs with the GEMM's block size and reuses its LDS.
+template <int MODE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+wgrad_reg_bn_kernel(const WgParams p, const BwdArgs a, int gx, int gy, int gz) {
+  __shared__ __attribute__((aligned(16))) char smem[WG_REG_SMEM];
+  const int nw = gx * gy * gz, b = blockIdx.x;
+  if (b < nw) wgrad_reg_body<MODE>(p, smem, vb_lin(b, gx, gy, gz));
+  else bn_bwd_apply_body<4>(a, (float*)smem, b - nw, (int)gridDim.x - nw);
+}
+
+template <int TCo, int TKk>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WgOcc<TCo, TKk>::W)))
+wgrad_glds_bn_kernel(const WgParams p, const BwdArgs a, int gx, int gy, int gz) {
+  __shared__ __attribute__((aligned(16))) char smem[WgGlds<TCo, TKk>::BYTES];
+  const int nw = gx * gy * gz, b = blockIdx.x;
+  if (b < nw) wgrad_glds_body<TCo, TKk>(p, smem, vb_lin(b, gx, gy, gz));
+  else bn_bwd_apply_body<4>(a, (float*)smem, b - nw, (int)gridDim.x - nw);
+}
+
+__global__ void __launch_bounds__(WGH_NT)
+wgrad_halo_bn_kernel(const WgParams p, const BwdArgs a, int gx, int gy, int gz) {
+  __shared__ __attribute__((aligned(16))) char smem[WGH_RING * WGH_STAGE];
+  const int nw = gx * gy * gz, b = blockIdx.x;
+  if (b < nw) wgrad_halo_body(p, smem, vb_lin(b, gx, gy, gz));
+  else bn_bwd_apply_body<4>(a, (float*)smem, b - nw, (int)gridDim.x - nw);
 }
 
 // grad[co][ci][kh][kw] (+)= scale * sum_s partial[s][co][(kh*KW+kw)*Cin+ci]
@@ -1163,8 +1233,9 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* partial, float*
                            int64_t KH, int64_t KW, int64_t stride, int64_t pad, int64_t Kp,
                            int64_t splits, float scale, int64_t accumulate, int64_t cin_keep,
                            int64_t groups, hipStream_t st, bool reduce, int64_t nsets,
-                           int64_t gstride) {
+                           int64_t gstride, const BwdArgs* fuse = nullptr) {
   if (Cout % 8 || Kp % TK || nsets < 1 || nsets > 2) return (int)hipErrorInvalidValue;
+  if (fuse != nullptr && (reduce || nsets != 1)) return MDA_NOT_SERVED;
   if (cin_keep <= 0 || cin_keep > Cin) cin_keep = Cin;
   if (groups > 1 && (Cin % groups || Cout % groups)) return (int)hipErrorInvalidValue;
   WgParams p;
@@ -1185,12 +1256,54 @@ static int conv_wgrad_impl(const void* x, const void* dy, float* partial, float*
   dim3 grid((int)((Cout + TC - 1) / TC), (int)(Kp / TK), (int)(splits * nsets));
   const int tile = mode == WG_SCALAR ? 0 : wg_tile(p.M, Cout, Cin, KH, KW, Kp);
   int64_t hrh = 0, himg = 0;
+  // fused launch (fuse != null): the GEMM's blocks, then nbn apply blocks
+  // of the next BN backward, if its operands fit the GEMM's LDS
+  const int nbn = fuse ? apply_blocks((int64_t)fuse->M * fuse->C / 8, 4) : 0;
+  auto fits = [&](int64_t lds, int nt) {
+    return bn_apply_lds_bytes(fuse->C, nt, fuse->rreg != nullptr) <= lds;
+  };
   if (groups <= 1 && cin_keep == Cin && Kp == 9 * Cin &&
       wg_halo_ok(p.M, Cout, Cin, KH, KW, H, W, stride, pad) && wg_halo_geom(H, W, &hrh, &himg)) {
     p.h_rh = (int)hrh;
     p.h_img = (int)himg;
     dim3 gh((int)(Cout / 64), (int)(Cin / 64), (int)(splits * nsets));
+    if (fuse) {
+      if (!fits(WGH_RING * WGH_STAGE, WGH_NT)) return MDA_NOT_SERVED;
+      const int nw = (int)(gh.x * gh.y * gh.z);
+      hipLaunchKernelGGL(wgrad_halo_bn_kernel, dim3(nw + nbn), dim3(WGH_NT), 0, st, p, *fuse,
+                         (int)gh.x, (int)gh.y, (int)gh.z);
+      return (int)hipGetLastError();
+    }
     hipLaunchKernelGGL(conv_wgrad_halo_kernel, gh, dim3(WGH_NT), 0, st, p);
+  } else if (tile != 0 && fuse) {
+    const int tc = tile / 1000, tk = tile % 1000;
+    dim3 g2((int)((Cout + tc - 1) / tc), (int)((Kp + tk - 1) / tk), (int)(splits * nsets));
+    const int nw = (int)(g2.x * g2.y * g2.z);
+#define WG_FUSED_GLDS(TC_, TK_)                                                                  \
+  if (!fits(WgGlds<TC_, TK_>::BYTES, 256)) return MDA_NOT_SERVED;                               \
+  hipLaunchKernelGGL((wgrad_glds_bn_kernel<TC_, TK_>), dim3(nw + nbn), dim3(256), 0, st, p, *fuse, \
+                     (int)g2.x, (int)g2.y, (int)g2.z);
+    switch (tile) {
+      case 128128: { WG_FUSED_GLDS(128, 128) break; }
+      case 128064: { WG_FUSED_GLDS(128, 64) break; }
+      case 64128: { WG_FUSED_GLDS(64, 128) break; }
+      default: { WG_FUSED_GLDS(64, 64) break; }
+    }
+#undef WG_FUSED_GLDS
+    return (int)hipGetLastError();
+  } else if (fuse) {
+    if (!fits(WG_REG_SMEM, 256)) return MDA_NOT_SERVED;
+    const int nw = (int)(grid.x * grid.y * grid.z);
+    if (mode == WG_FAST)
+      hipLaunchKernelGGL(wgrad_reg_bn_kernel<WG_FAST>, dim3(nw + nbn), dim3(256), 0, st, p, *fuse,
+                         (int)grid.x, (int)grid.y, (int)grid.z);
+    else if (mode == WG_VEC8)
+      hipLaunchKernelGGL(wgrad_reg_bn_kernel<WG_VEC8>, dim3(nw + nbn), dim3(256), 0, st, p, *fuse,
+                         (int)grid.x, (int)grid.y, (int)grid.z);
+    else
+      hipLaunchKernelGGL(wgrad_reg_bn_kernel<WG_SCALAR>, dim3(nw + nbn), dim3(256), 0, st, p, *fuse,
+                         (int)grid.x, (int)grid.y, (int)grid.z);
+    return (int)hipGetLastError();
   } else if (tile != 0) {
     const int tc = tile / 1000, tk = tile % 1000;
     dim3 g2((int)((Cout + tc - 1) / tc), (int)((Kp + tk - 1) / tk), (int)(splits * nsets));
@@ -1242,6 +1355,34 @@ MDA_API int mda_conv_wgrad_nored(const void* x, const void* dy, float* partial, 
                                  int64_t nsets, hipStream_t st) {
   return conv_wgrad_impl(x, dy, partial, grad, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
                          Kp, splits, scale, accumulate, cin_keep, groups, st, false, nsets, 0);
+}
+
+// mda_conv_wgrad_nored and the streaming BN-backward apply of the next layer
+// (csrc/bn.hip mda_bn_bwd_apply_reg's operands, b_*, one gradient set, no
+// pre-activation gradient) in ONE launch.  MDA_NOT_SERVED (nothing launched)
+// when the apply's LDS does not fit the GEMM kernel's or the shapes are not
+// served; the caller then launches the two on their own.
+MDA_API int mda_conv_wgrad_nored_bn(const void* x, const void* dy, float* partial, float* grad,
+                                    int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Ho,
+                                    int64_t Wo, int64_t Cout, int64_t KH, int64_t KW,
+                                    int64_t stride, int64_t pad, int64_t Kp, int64_t splits,
+                                    int64_t cin_keep, int64_t groups, const void* b_dout,
+                                    const void* b_y, const void* b_res, const float* b_stats,
+                                    int64_t b_M, int64_t b_C, int64_t b_act, void* b_region,
+                                    void* b_dy, void* b_dres, float* b_dgamma, float* b_dbeta,
+                                    float* b_sums, const void* b_ry, const float* b_rstats,
+                                    void* b_rregion, const float* b_vres, hipStream_t st) {
+  if (b_C % 8 || b_C > SLOT_CMAX || b_M <= 0 || b_M >= ((int64_t)1 << 31) || b_region == nullptr)
+    return MDA_NOT_SERVED;
+  if (b_rregion != nullptr && (b_dres == nullptr || b_ry == nullptr || b_rstats == nullptr ||
+                               256 % (b_C / 8) != 0))
+    return MDA_NOT_SERVED;  // a thread must keep one channel group
+  const BwdArgs a{(const bf16_t*)b_dout, nullptr, nullptr, (const bf16_t*)b_y,
+                  (const bf16_t*)b_res, b_stats, (bf16_t*)b_dy, (bf16_t*)b_dres, b_dgamma, b_dbeta,
+                  b_sums, (BnRegion*)b_region, nullptr, (int)b_M, (int)b_C, (int)b_act,
+                  (const bf16_t*)b_ry, b_rstats, (BnRegion*)b_rregion, b_vres, 0, 0, 0};
+  return conv_wgrad_impl(x, dy, partial, grad, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
+                         Kp, splits, 1.f, 1, cin_keep, groups, st, false, 1, 0, &a);
 }
 
 // rows: n x 11 int64 {partial, grad, splits, Cout, Cin, KH, KW, Kp, accumulate, cin_keep,

@@ -284,9 +284,37 @@ def set_wgrad_defer(on: bool) -> None:
     instead of one reduce kernel per layer on the backward's critical path."""
     _WG_DEFER[0] = [] if on else None
     _WG_KEEP.clear()
+    _WG_PEND[0] = None
+
+
+# A deferred weight-gradient GEMM waiting to ride in the launch of the next
+# BN-backward apply on the same stream (mda_conv_wgrad_nored_bn): the GEMM
+# reads dy and x of its conv, the apply the dgrad output below it, so the two
+# are independent and one launch fills the CUs either leaves idle.  At most
+# one is parked; it holds its operands (the allocator cannot reuse them) and
+# is launched on its own by the next park, the next flush, or when the apply
+# is not served.  Only while the reductions are deferred (captured backward).
+_WG_PEND = [None]   # (stream, wgrad args, keep-alive tensors)
+_WG_FUSE_ON = [os.environ.get("MDA_WGRAD_BN_FUSE", "1") != "0"]
+_WG_FUSE_COUNT = [0]  # fused launches issued (tests)
+
+
+def set_wgrad_bn_fuse(on: bool) -> None:
+    """Weight-gradient GEMM + next BN-backward apply in one launch on / off (A/B)."""
+    _WG_FUSE_ON[0] = bool(on)
+
+
+def _launch_pending_wgrad() -> None:
+    pend, _WG_PEND[0] = _WG_PEND[0], None
+    if pend is None:
+        return
+    stream, args, _ = pend
+    with torch.cuda.stream(stream):
+        _ext.call("mda_conv_wgrad_nored", *args)
 
 
 def flush_wgrad_reduces() -> None:
+    _launch_pending_wgrad()
     rows = _WG_DEFER[0]
     if rows:
         t = torch.tensor(rows, dtype=torch.int64)
@@ -302,8 +330,14 @@ def _conv_wgrad(x, dy, target, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, 
     set 1's gradient goes ``gstride`` floats past ``target`` -- one launch."""
     part = torch.empty(nsets * sp * Cout * Kp, dtype=torch.float32, device=x.device)
     if direct and _WG_DEFER[0] is not None:
-        _ext.call("mda_conv_wgrad_nored", x, dy, part, target, N, H, W, Cin, Ho, Wo, Cout, KH, KW,
-                  stride, pad, Kp, sp, 1.0, 1, cin_keep, groups, nsets)
+        args = (x, dy, part, target, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, Kp, sp, 1.0, 1,
+                cin_keep, groups, nsets)
+        _launch_pending_wgrad()
+        if nsets == 1 and _WG_FUSE_ON[0] and _WG_SIDE[0] is None and _DUAL[0] is None:
+            # park it: the next BN-backward apply on this stream launches it too
+            _WG_PEND[0] = (torch.cuda.current_stream(), args, (x, dy))
+        else:
+            _ext.call("mda_conv_wgrad_nored", *args)
         for k in range(nsets):
             _WG_DEFER[0].append([part.data_ptr() + 4 * k * sp * Cout * Kp,
                                  target.data_ptr() + 4 * k * gstride, sp, Cout, Cin, KH, KW, Kp, 1,
@@ -418,8 +452,20 @@ def _bn_bwd(dout, dpre, y, res, stats, gamma, beta, M, C, act, need_res, direct_
     ry, rst = (rl.y, rl.stats) if rl is not None else (None, None)
     if reg is not None and dpre is None:
         sums = None if direct_gb else torch.empty(2, C, dtype=torch.float32, device=dev)
-        _ext.call("mda_bn_bwd_apply_reg", dout, None, y, res, stats, M, C, act, reg, dy, dres,
-                  dg, db, sums, ry, rst, rreg, vres, 1, 0, 0, 0)
+        pend = _WG_PEND[0]
+        rc = _ext.NOT_SERVED
+        if pend is not None and pend[0] == torch.cuda.current_stream():
+            # the parked weight-gradient GEMM and this apply in one launch
+            a = pend[1]
+            rc = _ext.call("mda_conv_wgrad_nored_bn", *a[:17], *a[19:21], dout, y, res, stats, M, C,
+                           act, reg, dy, dres, dg, db, sums, ry, rst, rreg, vres,
+                           ok=(0, _ext.NOT_SERVED))
+            if rc == 0:
+                _WG_PEND[0] = None
+                _WG_FUSE_COUNT[0] += 1
+        if rc != 0:
+            _ext.call("mda_bn_bwd_apply_reg", dout, None, y, res, stats, M, C, act, reg, dy, dres,
+                      dg, db, sums, ry, rst, rreg, vres, 1, 0, 0, 0)
         if rl is not None:
             rl.arm(dres, rreg)
         return dy, dres, sums

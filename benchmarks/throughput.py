@@ -68,6 +68,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--out", default=None, help="append JSON rows to this file")
+    ap.add_argument("--opts", nargs="*", default=[], help="extra KEY VALUE config overrides for every row")
     ap.add_argument("--in-process", action="store_true",
                     help="run every config in THIS process (default: one child process each)")
     args = ap.parse_args()
@@ -85,6 +86,8 @@ def main():
                 cmd.append("--no-graph")
             if args.out:
                 cmd += ["--out", args.out]
+            if args.opts:
+                cmd += ["--opts"] + list(args.opts)
             r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
             rows = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
             print(rows[-1] if rows else json.dumps({"config": name, "error": f"exit {r.returncode}"}),
@@ -94,7 +97,8 @@ def main():
     for name in names:
         yaml, bs, opts, ds = CONFIGS[name]
         try:
-            r = benchmark.run(os.path.join(ROOT, yaml), bs, args.steps, args.warmup, opts=opts,
+            r = benchmark.run(os.path.join(ROOT, yaml), bs, args.steps, args.warmup,
+                              opts=list(opts) + list(args.opts),
                               use_graph=not args.no_graph, dataset=ds)
         except Exception as e:  # report and continue with the other configs
             print(json.dumps({"config": name, "error": f"{type(e).__name__}: {e}"[:300]}), flush=True)

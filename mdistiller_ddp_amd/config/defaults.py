@@ -92,7 +92,6 @@ CFG.RUNTIME.TEACHER_GRAPH = "split"  # split | fork: the look-ahead teacher as i
                                      # replayed on the teacher stream (split), or forked inside the step graph
 CFG.RUNTIME.TEACHER_FIRST = True     # split: enqueue the teacher graph before the student's
 CFG.RUNTIME.WGRAD_DEFER = True       # captured backward: all layers' wgrad split reductions in one launch
-CFG.RUNTIME.WGRAD_STREAM = "auto"    # auto | on | off: captured-backward wgrads on a forked stream (auto: >= 128 px inputs)
 CFG.RUNTIME.FOLD_TEACHER_BN = True   # fold frozen teacher BN into conv weights
 CFG.RUNTIME.PROFILE = False          # torch.profiler trace + hipEvent step times of a window
 CFG.RUNTIME.PROFILE_START = 20       #   first profiled iteration of epoch 1

@@ -244,11 +244,6 @@ class TrainStep:
         self._dual = None  # DOT: (fwd, kd-bwd, ce-bwd, opt, upd graphs, side stream, event)
         self.dot_dual = self.is_dot and bool(cfg.RUNTIME.get("DOT_DUAL_STREAM", True))
         self.dot_single = self.is_dot and self._dot_single_ok(cfg)
-        # measured (profiles/r2_wgrad_stream_ab.md): the forked wgrads pay off on ImageNet-sized
-        # students (-4 %) and cost 5-9 % on the CIFAR ones, whose steps are too short for the
-        # extra graph edges; "auto" = on for inputs of >= 128 px
-        ws = cfg.RUNTIME.get("WGRAD_STREAM", "auto")
-        ws = ws.lower() if isinstance(ws, str) else bool(ws)
         la = cfg.RUNTIME.get("TEACHER_LOOKAHEAD", "auto")
         la = la.lower() if isinstance(la, str) else bool(la)
         self.lookahead = "auto" if la == "auto" else la in (True, "true", "1", "on")
@@ -263,10 +258,6 @@ class TrainStep:
         self.teacher_first = bool(cfg.RUNTIME.get("TEACHER_FIRST", True))
         self._tsplit = None     # (graph, T list, X list, stream, teacher-done event, copy-done event)
         self._tp_inflight = False
-        self.wgrad_side = (False if self.device.type != "cuda" else
-                           "auto" if ws == "auto" else ws in (True, "true", "1", "on"))
-        self._wg_auto = False
-        self._wg_stream = None
         self.wgrad_defer = self.device.type == "cuda" and bool(cfg.RUNTIME.get("WGRAD_DEFER", True))
 
     def _graph_comm_mode(self, cfg):
@@ -398,8 +389,7 @@ class TrainStep:
 
     def _fwd_bwd(self, b: dict, overlap_comm):
         preds, losses = self._fwd(b)
-        armed = self._arm_wgrad_stream()
-        deferred = (not armed) and self._arm_wgrad_defer()
+        deferred = self._arm_wgrad_defer()
         # DOT's single pass writes both gradient sets of a parameter together:
         # its buckets launch both sets from the same events
         events = overlap_comm == "events" and (not self.is_dot or self.dot_single)
@@ -440,7 +430,6 @@ class TrainStep:
             if self.is_dot and self.dot_single and events != "armed":
                 self.reducer.end_calibration()
             self._flush_wgrad_defer(deferred)
-            self._join_wgrad_stream(armed)
             join_branches()
         if events == "armed":
             self.reducer.finish_capture()
@@ -451,9 +440,10 @@ class TrainStep:
         return preds, losses
 
     def _arm_wgrad_defer(self) -> bool:
-        """While a backward is being captured (and the wgrads stay on the main
-        stream), defer every layer's split reduction to one multi-layer launch
-        at the end of the backward (``hip_train.set_wgrad_defer``)."""
+        """While a backward is being captured, defer every layer's split
+        reduction to one multi-layer launch at the end of the backward
+        (``hip_train.set_wgrad_defer``); each weight-gradient GEMM then rides
+        in the launch of the next BN-backward apply (mda_conv_wgrad_nored_bn)."""
         if not (self.wgrad_defer and torch.cuda.is_current_stream_capturing()):
             return False
         from ..ops import hip_train
@@ -467,31 +457,6 @@ class TrainStep:
                 hip_train.flush_wgrad_reduces()
             finally:
                 hip_train.set_wgrad_defer(False)
-
-    def _arm_wgrad_stream(self) -> bool:
-        """While a backward is being captured, fork the native weight-gradient
-        GEMMs onto a side stream (``hip_train.set_wgrad_stream``): the captured
-        DAG then runs them beside the dgrad / BN-backward chain.  Not with the
-        all-reduce captured in the same graph (its bucket hooks assume the
-        gradients are complete on the main stream)."""
-        if not (self.wgrad_side and torch.cuda.is_current_stream_capturing()) or self.graph_comm:
-            return False  # (events mode too: its bucket events assume one stream)
-        if self.is_dot and self.dot_dual:
-            return False  # measured: the forks serialise the two concurrently replayed passes
-        if self.wgrad_side == "auto" and not self._wg_auto:
-            return False
-        from ..ops import hip_train
-        if self._wg_stream is None:
-            self._wg_stream = torch.cuda.Stream(device=self.device)
-            self.reducer.avoid_streams.append(self._wg_stream)
-        hip_train.set_wgrad_stream(self._wg_stream)
-        return True
-
-    def _join_wgrad_stream(self, armed: bool) -> None:
-        if armed:
-            from ..ops import hip_train
-            hip_train.join_wgrad_stream()
-            hip_train.set_wgrad_stream(None)
 
     def _post_backward(self):
         post = getattr(self.distiller, "post_backward", None)
@@ -598,7 +563,6 @@ class TrainStep:
         """
         static = {k: v.clone() for k, v in b.items()}
         img = self._static_img = static.get("image")
-        self._wg_auto = img is not None and img.dim() == 4 and min(img.shape[-2:]) >= 128
         pool = torch.cuda.graph_pool_handle()
         s = self._cap_stream = torch.cuda.Stream()
         self.reducer.avoid_streams = [s]
@@ -758,13 +722,11 @@ class TrainStep:
             preds, losses = self._fwd(static)
         with torch.cuda.graph(g_kd, pool=pool, stream=s):
             self.flat.bind_grads(1)
-            armed = self._arm_wgrad_stream()
-            deferred = (not armed) and self._arm_wgrad_defer()
+            deferred = self._arm_wgrad_defer()
             try:
                 losses["loss_kd"].backward(retain_graph=True)
             finally:
                 self._flush_wgrad_defer(deferred)
-                self._join_wgrad_stream(armed)
                 join_branches()
         hip_train.set_ws_tag("dot_ce")
         try:
@@ -775,13 +737,11 @@ class TrainStep:
                     with _autocast(self.device, self.dtype):
                         feed.prefetch(self.distiller.teacher)
                 self.flat.bind_grads(0)
-                armed = self._arm_wgrad_stream()
-                deferred = (not armed) and self._arm_wgrad_defer()
+                deferred = self._arm_wgrad_defer()
                 try:
                     losses["loss_ce"].backward()
                 finally:
                     self._flush_wgrad_defer(deferred)
-                    self._join_wgrad_stream(armed)
                     join_branches()
                 if in_graph:
                     # join only: the KD-backward graph may still be replaying on the

@@ -250,28 +250,6 @@ def _ws(device):
     return w
 
 
-_WG_SIDE = [None]
-
-
-def set_wgrad_stream(stream) -> None:
-    """Arm (a stream) or disarm (None) the weight-gradient side stream.
-
-    While armed, every native backward launches its weight-gradient GEMM and
-    split reduction on ``stream``, forked from the current stream once dy is
-    ready: the dgrad / BN-backward chain that carries the backward forward no
-    longer waits for them, and they fill the CUs the chain leaves idle.  Only
-    for gradients written straight into the flat buffer; the caller joins the
-    side stream (:func:`join_wgrad_stream`) before anything reads the grads.
-    """
-    _WG_SIDE[0] = stream
-
-
-def join_wgrad_stream() -> None:
-    s = _WG_SIDE[0]
-    if s is not None:
-        torch.cuda.current_stream().wait_stream(s)
-
-
 _WG_DEFER = [None]  # rows of deferred split reductions while armed (a list), else None
 _WG_KEEP: list = []  # their partial buffers, alive until the flush has been queued
 
@@ -333,7 +311,7 @@ def _conv_wgrad(x, dy, target, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, 
         args = (x, dy, part, target, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, Kp, sp, 1.0, 1,
                 cin_keep, groups, nsets)
         _launch_pending_wgrad()
-        if nsets == 1 and _WG_FUSE_ON[0] and _WG_SIDE[0] is None and _DUAL[0] is None:
+        if nsets == 1 and _WG_FUSE_ON[0] and _DUAL[0] is None:
             # park it: the next BN-backward apply on this stream launches it too
             _WG_PEND[0] = (torch.cuda.current_stream(), args, (x, dy))
         else:
@@ -346,22 +324,6 @@ def _conv_wgrad(x, dy, target, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, 
         return
     _ext.call("mda_conv_wgrad", x, dy, part, target, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride,
               pad, Kp, sp, 1.0, 1 if direct else 0, cin_keep, groups, nsets, gstride)
-
-
-def _wgrad_launch(fn, direct, *tensors):
-    """Run ``fn`` (a wgrad launch sequence) on the armed side stream when its
-    result goes straight into the flat gradient; inputs are recorded as used
-    there so the allocator does not hand their memory out early."""
-    s = _WG_SIDE[0]
-    if s is None or not direct:
-        fn()
-        return
-    s.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(s):
-        fn()
-    for t in tensors:
-        if t is not None:
-            t.record_stream(s)
 
 
 def _bn_bwd_reduce(dout, dpre, y, res, stats, M, C, act, ws, sums, dg, db):
@@ -1282,7 +1244,7 @@ class _ConvBNActTrain(torch.autograd.Function):
             def wg():
                 _conv_wgrad(x, dy, target, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, Kw, sp,
                             direct_w, ctx.cin_keep, ctx.groups)
-            _wgrad_launch(wg, direct_w, x, dy)
+            wg()
             dw = None if direct_w else target
             if direct_w:
                 notify_grad(weight)
@@ -1380,7 +1342,7 @@ def _conv_bn_backward_dual(ctx, dout, dpre):
         def wg():  # both sets in one launch (x read by both)
             _conv_wgrad(x, dy, target, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, Kw, sp,
                         True, ctx.cin_keep, 1, 2, _DUAL[0].gstride)
-        _wgrad_launch(wg, True, x, dy)
+        wg()
         notify_grad(weight)
     notify_grad(gamma, beta)
     return dx, None, None, None, dres, None, None, None, None, None, None, None
@@ -1520,7 +1482,7 @@ def _dw_backward(ctx, dout, dpre):
                 return
             _ext.call("mda_dw_wgrad", x, dy, part, target, N, H, W, C, Ho, Wo, 3, 3, stride, pad,
                       nblk, 1 if direct_w else 0, vst, vact)
-        _wgrad_launch(wg, direct_w, x, dy)
+        wg()
         dw = None if direct_w else target
         if direct_w:
             notify_grad(weight)
@@ -1709,7 +1671,7 @@ class _ConvTrain(torch.autograd.Function):
             def wg():
                 _conv_wgrad(x, dz, target, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, Kp, sp,
                             direct_w, ctx.cin_keep, 1)
-            _wgrad_launch(wg, direct_w, x, dz)
+            wg()
             dw = None if direct_w else target
             if direct_w:
                 notify_grad(weight)

@@ -625,11 +625,15 @@ class TrainStep:
         both sides already fill the GPU and it costs 6 %: ``auto`` skips that case."""
         if self.lookahead != "auto":
             return bool(self.lookahead)
-        # (a train-mode teacher, OFD.TEACHER_TRAIN_BN, is served too: its
-        # round-5 non-finite losses under the look-ahead were the step's arena
-        # zero fill racing the teacher graph's BN regions, fixed by closing the
-        # arena window at the step capture (_bn_end); the look-ahead test
-        # covers OFD, tests/test_gpu_e2e.py)
+        if getattr(self.distiller, "_teacher_train_bn", False):
+            # a train-mode teacher (OFD.TEACHER_TRAIN_BN) runs inline under
+            # auto.  With every step handed its next batch the look-ahead is
+            # exact for it (tests/test_gpu_e2e.py look-ahead test, OFD case;
+            # the round-5 arena race is fixed), but a caller that passes no
+            # next batch takes the priming-graph / recapture fallback, which
+            # still gives non-finite losses with a train-mode teacher
+            # (test_distiller_graph_steps[OFD]); cause not found in round 6
+            return False
         img = static.get("image")
         big = img is not None and img.dim() == 4 and min(img.shape[-2:]) >= 128
         needs = tuple(getattr(self.distiller, "teacher_needs", ("logits",)))

@@ -1186,10 +1186,15 @@ static bool wg_halo_ok(int64_t M, int64_t Cout, int64_t Cin, int64_t KH, int64_t
 }
 
 // halo kernel splits: MDA_WGH_BLOCKS (default 128) blocks, >= 2 stages each
+// Target GEMM blocks of a halo wgrad: 64 since round 6.  Its GEMM now shares
+// a launch with a BN-backward apply (mda_conv_wgrad_nored_bn), so fewer,
+// longer blocks (half the split partials for the deferred reduce) won:
+// flagship 0.7707 -> 0.7605 ms/step (0.7678 -> 0.7614 in a second set); the
+// student alone 0.6130 -> 0.6208 (profiles/r6_ab.md).  MDA_WGH_BLOCKS: A/B.
 static int64_t wg_halo_splits(int64_t M, int64_t Cout, int64_t Cin) {
   static const int64_t target = [] {
     const char* e = getenv("MDA_WGH_BLOCKS");
-    return e ? (int64_t)atoi(e) : (int64_t)128;
+    return e ? (int64_t)atoi(e) : (int64_t)64;
   }();
   const int64_t tiles = (Cout / 64) * (Cin / 64), stages = M / 64;
   int64_t sp = (target + tiles - 1) / tiles;

@@ -13,7 +13,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ...ops.nn import conv_bn_act, grad_fork, pool_linear
-from ...ops.hip_train import can_defer_residual
+from ...ops.hip_train import arm_apply_ride, can_defer_residual, finish_apply_ride
 from ...runtime.streams import run_branch
 from .._base import ModelBase, PreactStage
 
@@ -45,7 +45,10 @@ class BasicBlock(nn.Module):
         # x feeds conv1 and the shortcut: their input gradients are summed in
         # the second one's dgrad epilogue (GradFork), not by an autograd add
         fork = grad_fork(x)
-        # h feeds conv2 only: conv2's dgrad may finish bn1's backward
+        if self.downsample is not None:
+            # conv1's BN apply rides in the projection shortcut's conv launch
+            # (ops/hip_train.py arm_apply_ride); nothing reads h before it
+            arm_apply_ride(x)
         h, _ = conv_bn_act(x, self.conv1, self.bn1, "relu", fork=fork, private=True)
         if self.downsample is None:
             res = x
@@ -58,6 +61,7 @@ class BasicBlock(nn.Module):
             # (ops/hip_train.py VirtualBN)
             defer = can_defer_residual(h, self.conv2, self.bn2)
             res = run_branch(x, lambda t: self._shortcut(t, fork, defer))
+            finish_apply_ride()
             fork = None
         # the block output is a stage feature only when features are consumed
         return conv_bn_act(h, self.conv2, self.bn2, "relu", residual=res,

@@ -17,7 +17,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ...ops.nn import MaxPool2d, conv_bn_act, grad_fork, pool_linear
-from ...ops.hip_train import can_defer_residual
+from ...ops.hip_train import arm_apply_ride, can_defer_residual, finish_apply_ride
 from ...runtime.streams import run_branch
 from .._base import ModelBase, PreactStage
 from ..cifar.resnet import Stage
@@ -58,8 +58,11 @@ class BasicBlock(nn.Module):
 
     def forward(self, x):
         fork = grad_fork(x)
+        if self.downsample is not None:
+            arm_apply_ride(x)  # conv1's BN apply rides in the shortcut's launch
         h, _ = conv_bn_act(x, self.conv1, self.bn1, "relu", fork=fork, private=True)
         res, res_fork = self._res(x, fork, h, self.conv2, self.bn2)  # after conv1: its backward runs first
+        finish_apply_ride()
         return conv_bn_act(h, self.conv2, self.bn2, "relu", residual=res,
                            want_preact=self.is_last and self._need_preact, res_fork=res_fork,
                            private=not (self.is_last and self._need_preact))

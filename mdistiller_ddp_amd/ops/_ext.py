@@ -68,6 +68,7 @@ SIGNATURES = {
     "mda_nst_bwd": "p" + "ii" + "pp" + "s",
     "mda_conv_wgrad": "pppp" + "i" * 13 + "fiii" + "ii" + "s",
     "mda_conv_wgrad_nored": "pppp" + "i" * 13 + "fiii" + "i" + "s",
+    "mda_conv1x1_bnacc_apply": "pppp" + "i" * 9 + "pp" + "ii" + "ppppp" + "ff" + "p" + "ppp" + "i" + "s",
     "mda_conv_wgrad_nored_bn": "pppp" + "i" * 15 + "pppp" + "iii" + "pppppp" + "pppp" + "s",
     "mda_wgrad_reduce_multi": "pis",
     "mda_pack_conv_weights_grouped": "ppp" + "i" * 7 + "s",

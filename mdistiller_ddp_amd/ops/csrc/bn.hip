@@ -638,39 +638,7 @@ _Pragma("unroll")
 // when C/8 is a power of two (power-of-two grid) so every thread keeps one
 // channel group.
 
-__device__ __forceinline__ void apply8(const uint4& yv, const uint4& rv, bool has_res, const float* sc,
-                                       const float* sh, int act, uint4& out, uint4& z,
-                                       const float* rsc = nullptr, const float* rsh = nullptr) {
-  const uint32_t yw[4] = {yv.x, yv.y, yv.z, yv.w};
-  const uint32_t rw[4] = {rv.x, rv.y, rv.z, rv.w};
-  uint32_t zo[4], oo[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    float v0 = __uint_as_float(yw[k] << 16) * sc[2 * k] + sh[2 * k];
-    float v1 = __uint_as_float(yw[k] & 0xffff0000u) * sc[2 * k + 1] + sh[2 * k + 1];
-    if (has_res) {
-      const float r0 = __uint_as_float(rw[k] << 16), r1 = __uint_as_float(rw[k] & 0xffff0000u);
-      if (rsc) {  // virtual residual: the raw input of another BN, applied here
-        v0 += r0 * rsc[2 * k] + rsh[2 * k];
-        v1 += r1 * rsc[2 * k + 1] + rsh[2 * k + 1];
-      } else {
-        v0 += r0;
-        v1 += r1;
-      }
-    }
-    zo[k] = pack_bf16x2(v0, v1);
-    oo[k] = pack_bf16x2(act_f(v0, act), act_f(v1, act));
-  }
-  out = make_uint4(oo[0], oo[1], oo[2], oo[3]);
-  z = make_uint4(zo[0], zo[1], zo[2], zo[3]);
-}
 
-// Batch statistics of channel c from a region -> scale / shift (block 0
-// writes the [4][C] stats and the running statistics; bnslot.h fin_channel_w).
-__device__ __forceinline__ void fin_channel(BnRegion* reg, int64_t M, int C, int c, const FinArgs& f,
-                                            float& sc, float& sh) {
-  fin_channel_w<false>(reg, M, C, c, f, sc, sh, blockIdx.x == 0);
-}
 
 // z = y*scale + shift (+ res); out = act(z); preact = z -- with the finalize
 // of the region's sums in the prologue.  The thread's V vectors of y
@@ -690,63 +658,8 @@ bn_apply_fin_kernel(const bf16_t* __restrict__ y, BnRegion* __restrict__ reg, in
                     FinArgs f, const bf16_t* __restrict__ res, bf16_t* __restrict__ out,
                     bf16_t* __restrict__ preact, int act, BnRegion* __restrict__ rreg, FinArgs rf) {
   extern __shared__ float s_dyn[];
-  float* const s_scale = s_dyn;
-  float* const s_shift = s_dyn + C;
-  float* const s_rscale = s_dyn + 2 * C;  // (rreg only)
-  float* const s_rshift = s_dyn + 3 * C;
-  const int64_t total = M * C / 8;
-  const int c8 = C / 8;
-  const int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  uint4 yv[V], rv[V];
-#pragma unroll
-  for (int k = 0; k < V; ++k) {
-    const int64_t i = i0 + k * stride;
-    const int64_t ii = i < total ? i : 0;
-    yv[k] = ((const uint4*)y)[ii];
-    rv[k] = res ? ((const uint4*)res)[ii] : make_uint4(0, 0, 0, 0);
-  }
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    fin_channel(reg, M, C, c, f, s_scale[c], s_shift[c]);
-    if (rreg) fin_channel(rreg, M, C, c, rf, s_rscale[c], s_rshift[c]);
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    if (f.nbt) f.nbt[0] += 1;
-    if (rreg && rf.nbt) rf.nbt[0] += 1;
-  }
-  __syncthreads();
-  float sc[8], sh[8], rsc[8], rsh[8];
-  const bool vr = rreg != nullptr;
-#pragma unroll
-  for (int k = 0; k < V; ++k) {
-    const int64_t i = i0 + k * stride;
-    if (i < total) {
-      const int cc = (int)(i % c8) * 8;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        sc[e] = s_scale[cc + e]; sh[e] = s_shift[cc + e];
-        rsc[e] = vr ? s_rscale[cc + e] : 1.f; rsh[e] = vr ? s_rshift[cc + e] : 0.f;
-      }
-      uint4 o, z;
-      apply8(yv[k], rv[k], res != nullptr, sc, sh, act, o, z, vr ? rsc : nullptr, vr ? rsh : nullptr);
-      ((uint4*)out)[i] = o;
-      if (preact) ((uint4*)preact)[i] = z;
-    }
-  }
-  for (int64_t i = i0 + V * stride; i < total; i += stride) {
-    const int cc = (int)(i % c8) * 8;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      sc[e] = s_scale[cc + e]; sh[e] = s_shift[cc + e];
-      rsc[e] = vr ? s_rscale[cc + e] : 1.f; rsh[e] = vr ? s_rshift[cc + e] : 0.f;
-    }
-    const uint4 y1 = ((const uint4*)y)[i];
-    const uint4 r1 = res ? ((const uint4*)res)[i] : make_uint4(0, 0, 0, 0);
-    uint4 o, z;
-    apply8(y1, r1, res != nullptr, sc, sh, act, o, z, vr ? rsc : nullptr, vr ? rsh : nullptr);
-    ((uint4*)out)[i] = o;
-    if (preact) ((uint4*)preact)[i] = z;
-  }
+  bn_apply_fin_body<V>(FwdApply{y, reg, M, C, f, res, out, preact, act, rreg, rf}, s_dyn,
+                       (int)blockIdx.x, (int)gridDim.x);
 }
 
 template <int VPT, bool HOLD>

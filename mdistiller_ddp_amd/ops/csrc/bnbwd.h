@@ -1,6 +1,9 @@
-// Training-BN backward pieces shared by csrc/bn.hip (the BN backward kernels)
-// and csrc/conv_wgrad.hip (a weight-gradient GEMM and the NEXT layer's BN
-// backward apply in one launch, mda_conv_wgrad_nored_bn).
+// Training-BN streaming passes shared by csrc/bn.hip (the BN kernels) and the
+// fused launches that run them beside another kernel's blocks:
+// csrc/conv_wgrad.hip (a weight-gradient GEMM and the NEXT layer's BN
+// backward apply, mda_conv_wgrad_nored_bn) and csrc/conv1x1.hip (a residual
+// block's projection-shortcut conv and conv1's BN forward apply,
+// mda_conv1x1_bnacc_apply).
 //
 // bn_bwd_apply_body is the streaming pass of a BN backward whose channel sums
 // a producer already added into the region (the consuming conv's dgrad
@@ -244,6 +247,111 @@ inline int apply_blocks(int64_t n8, int vpt) {
   int64_t b = 1;
   while (b < want && b < 1024) b <<= 1;
   return (int)b;
+}
+
+// ---------------------------------------------------------------------------
+// Forward apply: z = y*scale + shift (+ res); out = act(z); preact = z, with
+// the finalize of the region's sums in the prologue (every block finalizes
+// the channels; block 0 also writes the [4][C] stats and the running
+// statistics).  rreg != null: `res` is the RAW output of another training
+// conv whose BN (no activation: a projection shortcut) is applied here too
+// (VirtualBN).  V vectors per thread loaded BEFORE the prologue.
+struct FwdApply {
+  const bf16_t* y; BnRegion* reg; int64_t M; int C; FinArgs f;
+  const bf16_t* res; bf16_t* out; bf16_t* preact; int act;
+  BnRegion* rreg; FinArgs rf;
+};
+
+__device__ __forceinline__ float bw_act_f(float v, int act) {
+  if (act == 1) return fmaxf(v, 0.f);
+  if (act == 2) return fminf(fmaxf(v, 0.f), 6.f);
+  return v;
+}
+
+__device__ __forceinline__ void apply8(const uint4& yv, const uint4& rv, bool has_res, const float* sc,
+                                       const float* sh, int act, uint4& out, uint4& z,
+                                       const float* rsc = nullptr, const float* rsh = nullptr) {
+  const uint32_t yw[4] = {yv.x, yv.y, yv.z, yv.w};
+  const uint32_t rw[4] = {rv.x, rv.y, rv.z, rv.w};
+  uint32_t zo[4], oo[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float v0 = __uint_as_float(yw[k] << 16) * sc[2 * k] + sh[2 * k];
+    float v1 = __uint_as_float(yw[k] & 0xffff0000u) * sc[2 * k + 1] + sh[2 * k + 1];
+    if (has_res) {
+      const float r0 = __uint_as_float(rw[k] << 16), r1 = __uint_as_float(rw[k] & 0xffff0000u);
+      if (rsc) {  // virtual residual: the raw input of another BN, applied here
+        v0 += r0 * rsc[2 * k] + rsh[2 * k];
+        v1 += r1 * rsc[2 * k + 1] + rsh[2 * k + 1];
+      } else {
+        v0 += r0;
+        v1 += r1;
+      }
+    }
+    zo[k] = pack_bf16x2(v0, v1);
+    oo[k] = pack_bf16x2(bw_act_f(v0, act), bw_act_f(v1, act));
+  }
+  out = make_uint4(oo[0], oo[1], oo[2], oo[3]);
+  z = make_uint4(zo[0], zo[1], zo[2], zo[3]);
+}
+
+// LDS floats bn_apply_fin_body needs for C channels
+__host__ __device__ __forceinline__ int64_t bn_fin_lds_bytes(int C, bool rreg) {
+  return (int64_t)(rreg ? 4 : 2) * C * 4;
+}
+
+template <int V>
+__device__ __forceinline__ void bn_apply_fin_body(const FwdApply& a, float* s_dyn, int bid, int nblk) {
+  const int C = a.C;
+  float* const s_scale = s_dyn;
+  float* const s_shift = s_dyn + C;
+  float* const s_rscale = s_dyn + 2 * C;  // (rreg only)
+  float* const s_rshift = s_dyn + 3 * C;
+  const int64_t total = a.M * C / 8;
+  const int c8 = C / 8;
+  const int64_t i0 = bid * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)nblk * blockDim.x;
+  uint4 yv[V], rv[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const int64_t i = i0 + k * stride;
+    const int64_t ii = i < total ? i : 0;
+    yv[k] = ((const uint4*)a.y)[ii];
+    rv[k] = a.res ? ((const uint4*)a.res)[ii] : make_uint4(0, 0, 0, 0);
+  }
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    fin_channel_w<false>(a.reg, a.M, C, c, a.f, s_scale[c], s_shift[c], bid == 0);
+    if (a.rreg) fin_channel_w<false>(a.rreg, a.M, C, c, a.rf, s_rscale[c], s_rshift[c], bid == 0);
+  }
+  if (bid == 0 && threadIdx.x == 0) {
+    if (a.f.nbt) a.f.nbt[0] += 1;
+    if (a.rreg && a.rf.nbt) a.rf.nbt[0] += 1;
+  }
+  __syncthreads();
+  float sc[8], sh[8], rsc[8], rsh[8];
+  const bool vr = a.rreg != nullptr;
+  auto emit = [&](int64_t i, const uint4& y1, const uint4& r1) {
+    const int cc = (int)(i % c8) * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      sc[e] = s_scale[cc + e]; sh[e] = s_shift[cc + e];
+      rsc[e] = vr ? s_rscale[cc + e] : 1.f; rsh[e] = vr ? s_rshift[cc + e] : 0.f;
+    }
+    uint4 o, z;
+    apply8(y1, r1, a.res != nullptr, sc, sh, a.act, o, z, vr ? rsc : nullptr, vr ? rsh : nullptr);
+    ((uint4*)a.out)[i] = o;
+    if (a.preact) ((uint4*)a.preact)[i] = z;
+  };
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const int64_t i = i0 + k * stride;
+    if (i < total) emit(i, yv[k], rv[k]);
+  }
+  for (int64_t i = i0 + V * stride; i < total; i += stride) {
+    const uint4 y1 = ((const uint4*)a.y)[i];
+    const uint4 r1 = a.res ? ((const uint4*)a.res)[i] : make_uint4(0, 0, 0, 0);
+    emit(i, y1, r1);
+  }
 }
 
 }  // namespace

@@ -27,6 +27,7 @@
 // forward; dgrad stride 1.
 #include "common.h"
 #include "bnslot.h"
+#include "bnbwd.h"
 #include <stdlib.h>
 
 namespace {
@@ -56,18 +57,24 @@ __device__ __forceinline__ float s1_act(float v, int act) {
 
 // CI 16-channel subtiles per wave (block: 4 waves x 16*CI channels), KK
 // 32-wide k slices (K = 32*KK)
+template <int KK>
+struct S1Smem { static constexpr int BYTES = 2 * S_BM * (32 * KK + 8) * 2; };
+
+// Block (bx, by) of a (gx, gy) grid: bx strides the pixel tiles (persistent),
+// by picks the channel slice.  The stand-alone kernel passes blockIdx /
+// gridDim; the fused launch (mda_conv1x1_bnacc_apply) a linear block index.
 template <int CI, int KK>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
-conv1x1_stream_kernel(const S1Params p) {
+__device__ __forceinline__ void conv1x1_body(const S1Params& p, char* smem, int bx, int by, int gx,
+                                             int gy) {
   constexpr int K = 32 * KK;
   constexpr int ROW = K + 8;                  // LDS row (bf16): 16-byte pad, conflict-free b128 reads
   constexpr int CH = S_BM * K / 8 / 256;      // 16-byte X chunks per thread per tile
   static_assert(S_BM * K / 8 % 256 == 0, "tile load");
-  __shared__ __attribute__((aligned(16))) bf16_t xs[2][S_BM * ROW];
+  bf16_t (*xs)[S_BM * ROW] = (bf16_t (*)[S_BM * ROW])smem;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int q = lane >> 4, r16 = lane & 15;
-  const int ch0 = blockIdx.y * (64 * CI) + wid * (16 * CI);   // this wave's first channel
+  const int ch0 = by * (64 * CI) + wid * (16 * CI);   // this wave's first channel
 
   // resident A fragments: W[ch0 + 16 ci + r16][32 kk + 8 q .. + 8]
   bf16x8 af[CI][KK];
@@ -124,7 +131,7 @@ conv1x1_stream_kernel(const S1Params p) {
     }
   };
 
-  int t = blockIdx.x;
+  int t = bx;
   if (t >= p.ntiles) goto done;
   {
     uint4 v[CH];
@@ -132,8 +139,8 @@ conv1x1_stream_kernel(const S1Params p) {
     store_tile(0, v);
     __syncthreads();
     int buf = 0;
-    for (; t < p.ntiles; t += gridDim.x) {
-      const int tn = t + gridDim.x;
+    for (; t < p.ntiles; t += gx) {
+      const int tn = t + gx;
       if (tn < p.ntiles) load_tile(tn, v);   // in flight during this tile's MFMAs and stores
       f32x4 acc[CI][4];
 #pragma unroll
@@ -212,12 +219,33 @@ done:
         }
         if (r16 == 0) {
           const int c = ch0 + 16 * ci + 4 * q + e;
-          const int sh = (int)(blockIdx.x + gridDim.x * blockIdx.y) % slot_shards(p.Cout);
+          const int sh = (int)(bx + gx * by) % slot_shards(p.Cout);
           acc_add(region_acc(p.slot, p.Cout, sh, 0) + c, (double)a);
           acc_add(region_acc(p.slot, p.Cout, sh, 1) + c, (double)b);
         }
       }
   }
+}
+
+template <int CI, int KK>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+conv1x1_stream_kernel(const S1Params p) {
+  __shared__ __attribute__((aligned(16))) char smem[S1Smem<KK>::BYTES];
+  conv1x1_body<CI, KK>(p, smem, (int)blockIdx.x, (int)blockIdx.y, (int)gridDim.x, (int)gridDim.y);
+}
+
+// A residual block's projection-shortcut conv (training forward: raw output
+// + BN sums) and the BN forward apply of conv1's output in ONE launch:
+// neither reads the other's output (the shortcut reads the block input,
+// the apply conv1's raw output) and back to back each ran on half the GPU.
+// Blocks [0, gx * gy) are the conv's, the rest the apply's (bnbwd.h).
+template <int CI, int KK>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+conv1x1_apply_kernel(const S1Params p, const FwdApply a, int gx, int gy) {
+  __shared__ __attribute__((aligned(16))) char smem[S1Smem<KK>::BYTES];
+  const int nw = gx * gy, b = blockIdx.x;
+  if (b < nw) conv1x1_body<CI, KK>(p, smem, b % gx, b / gx, gx, gy);
+  else bn_apply_fin_body<4>(a, (float*)smem, b - nw, (int)gridDim.x - nw);
 }
 
 int g_cus = 0;
@@ -234,25 +262,32 @@ int cus() {
 }
 
 template <int CI, int KK>
-int launch_ci(const S1Params& p, hipStream_t st) {
+int launch_ci(const S1Params& p, hipStream_t st, const FwdApply* fa) {
   const int ny = p.Cout / (64 * CI);
   // persistent: about two resident blocks per CU over all channel tiles
   int gx = (2 * cus() + ny - 1) / ny;
   if (gx > p.ntiles) gx = p.ntiles;
   if (gx < 1) gx = 1;
+  if (fa != nullptr) {
+    if (bn_fin_lds_bytes(fa->C, fa->rreg != nullptr) > S1Smem<KK>::BYTES) return -1;
+    const int nbn = apply_blocks(fa->M * fa->C / 8, 4);
+    hipLaunchKernelGGL((conv1x1_apply_kernel<CI, KK>), dim3(gx * ny + nbn), dim3(256), 0, st, p,
+                       *fa, gx, ny);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL((conv1x1_stream_kernel<CI, KK>), dim3(gx, ny), dim3(256), 0, st, p);
   return (int)hipGetLastError();
 }
 
 template <int KK>
-int launch_kk(const S1Params& p, hipStream_t st) {
+int launch_kk(const S1Params& p, hipStream_t st, const FwdApply* fa) {
   // widest channel slice without register spills (kernel-resource-usage:
   // <4, 2> 228 VGPRs, <2, 8> 248, <4, 4> spills)
   if constexpr (KK <= 2) {
-    if (p.Cout % 256 == 0) return launch_ci<4, KK>(p, st);
+    if (p.Cout % 256 == 0) return launch_ci<4, KK>(p, st, fa);
   }
-  if (p.Cout % 128 == 0) return launch_ci<2, KK>(p, st);
-  if (p.Cout % 64 == 0) return launch_ci<1, KK>(p, st);
+  if (p.Cout % 128 == 0) return launch_ci<2, KK>(p, st, fa);
+  if (p.Cout % 64 == 0) return launch_ci<1, KK>(p, st, fa);
   return (int)hipErrorInvalidValue;
 }
 
@@ -261,11 +296,11 @@ int launch_kk(const S1Params& p, hipStream_t st) {
 // Eligibility + launch (host side of conv_igemm.hip's dispatch): 1x1, pad 0,
 // dense, K a multiple of 32 up to 256 (weight rows Kp >= K), Cout % 64 == 0, stride 1 (or 2
 // for a forward), large M.  Returns -1 when the shape is not served.
-extern "C" int mda_conv1x1_stream_try(const void* x, const void* w, const float* scale,
-                                      const float* bias, const void* res, void* y, void* preact,
-                                      void* slot, int64_t N, int64_t H, int64_t W, int64_t K,
-                                      int64_t Kp, int64_t Ho, int64_t Wo, int64_t Cout,
-                                      int64_t stride, int64_t act, hipStream_t st) {
+static int conv1x1_try(const void* x, const void* w, const float* scale, const float* bias,
+                       const void* res, void* y, void* preact, void* slot, int64_t N, int64_t H,
+                       int64_t W, int64_t K, int64_t Kp, int64_t Ho, int64_t Wo, int64_t Cout,
+                       int64_t stride, int64_t act, hipStream_t st, const FwdApply* fa,
+                       int64_t min_m_override) {
   static const bool on = [] {
     const char* e = getenv("MDA_CONV1X1_STREAM");
     return !(e && e[0] == '0');
@@ -275,7 +310,8 @@ extern "C" int mda_conv1x1_stream_try(const void* x, const void* w, const float*
     return e ? (int64_t)atoll(e) : (int64_t)16384;
   }();
   const int64_t M = N * Ho * Wo;
-  if (!on || Kp < K || K % 32 || K > 256 || Cout % 64 || M < min_m || (stride != 1 && stride != 2))
+  if (!on || Kp < K || K % 32 || K > 256 || Cout % 64 ||
+      M < (min_m_override > 0 ? min_m_override : min_m) || (stride != 1 && stride != 2))
     return -1;
   if (N * H * W * K >= ((int64_t)1 << 31) || M * Cout >= ((int64_t)1 << 31)) return -1;
   if (((uintptr_t)x | (uintptr_t)y | (uintptr_t)(res ? res : y) | (uintptr_t)(preact ? preact : y)) & 15)
@@ -287,13 +323,49 @@ extern "C" int mda_conv1x1_stream_try(const void* x, const void* w, const float*
   p.Kp = (int)Kp; p.Cout = (int)Cout; p.stride = (int)stride; p.M = (int)M; p.act = (int)act;
   p.ntiles = (int)((M + S_BM - 1) / S_BM);
   switch (K) {
-    case 32: return launch_kk<1>(p, st);   // MobileNetV1's 32 -> 64 at 112^2 (output-bound)
-    case 64: return launch_kk<2>(p, st);
-    case 96: return launch_kk<3>(p, st);
-    case 128: return launch_kk<4>(p, st);
-    case 160: return launch_kk<5>(p, st);
-    case 192: return launch_kk<6>(p, st);
-    case 224: return launch_kk<7>(p, st);
-    default: return launch_kk<8>(p, st);
+    case 32: return launch_kk<1>(p, st, fa);   // MobileNetV1's 32 -> 64 at 112^2 (output-bound)
+    case 64: return launch_kk<2>(p, st, fa);
+    case 96: return launch_kk<3>(p, st, fa);
+    case 128: return launch_kk<4>(p, st, fa);
+    case 160: return launch_kk<5>(p, st, fa);
+    case 192: return launch_kk<6>(p, st, fa);
+    case 224: return launch_kk<7>(p, st, fa);
+    default: return launch_kk<8>(p, st, fa);
   }
+}
+
+extern "C" int mda_conv1x1_stream_try(const void* x, const void* w, const float* scale,
+                                      const float* bias, const void* res, void* y, void* preact,
+                                      void* slot, int64_t N, int64_t H, int64_t W, int64_t K,
+                                      int64_t Kp, int64_t Ho, int64_t Wo, int64_t Cout,
+                                      int64_t stride, int64_t act, hipStream_t st) {
+  return conv1x1_try(x, w, scale, bias, res, y, preact, slot, N, H, W, K, Kp, Ho, Wo, Cout, stride,
+                     act, st, nullptr, 0);
+}
+
+// A projection shortcut's training conv (1 x 1, stride 1 or 2, pad 0: raw
+// bf16 output y + its BN batch sums into `slot`) and the BN forward apply of
+// ANOTHER layer (conv1 of the same block: a_y its raw output, a_reg its
+// region, the finalize operands, out / pre) in one launch
+// (conv1x1_apply_kernel).  Every M is served (the apply fills the GPU the
+// small conv leaves idle).  MDA_NOT_SERVED (nothing launched) when the conv
+// is not a streaming-kernel shape.
+MDA_API int mda_conv1x1_bnacc_apply(const void* x, const void* w, void* y, void* slot, int64_t N,
+                                    int64_t H, int64_t W, int64_t K, int64_t Kp, int64_t Ho,
+                                    int64_t Wo, int64_t Cout, int64_t stride, const void* a_y,
+                                    void* a_reg, int64_t a_M, int64_t a_C, const float* gamma,
+                                    const float* beta, float* running_mean, float* running_var,
+                                    float* stats, float momentum, float eps, int64_t* nbt,
+                                    const void* a_res, void* a_out, void* a_pre, int64_t a_act,
+                                    hipStream_t st) {
+  if (a_C % 8 || a_C > SLOT_CMAX || a_M <= 0 || a_M >= ((int64_t)1 << 31) || slot == nullptr ||
+      a_reg == nullptr)
+    return MDA_NOT_SERVED;
+  const FwdApply fa{(const bf16_t*)a_y, (BnRegion*)a_reg, a_M, (int)a_C,
+                    FinArgs{gamma, beta, running_mean, running_var, stats, momentum, eps, nbt},
+                    (const bf16_t*)a_res, (bf16_t*)a_out, (bf16_t*)a_pre, (int)a_act, nullptr,
+                    FinArgs{}};
+  const int rc = conv1x1_try(x, w, nullptr, nullptr, nullptr, y, nullptr, slot, N, H, W, K, Kp,
+                             Ho, Wo, Cout, stride, 0, st, &fa, 1);
+  return rc == -1 ? MDA_NOT_SERVED : rc;
 }

@@ -966,6 +966,43 @@ def can_defer_residual(h, conv, bn) -> bool:
             and train_supported(h, conv, bn))
 
 
+# A residual block's conv1 BN apply rides in the launch of its projection
+# shortcut's conv (csrc/conv1x1.hip mda_conv1x1_bnacc_apply): neither reads
+# the other's output, and back to back each ran on half the GPU.  The block
+# arms it (arm_apply_ride) with its input; conv1's forward then PARKS its
+# plain BN apply instead of launching it, the shortcut conv on the same input
+# launches both, and finish_apply_ride launches a parked apply that found no
+# rider (a shortcut that is not a streaming-kernel shape).  Nothing reads
+# conv1's BN output before the shortcut: conv2 runs after it.
+_RIDE = {"x": None, "apply": None}
+_RIDE_ON = [os.environ.get("MDA_APPLY_RIDE", "1") != "0"]
+_RIDE_COUNT = [0]  # fused launches issued (tests)
+
+
+def set_apply_ride(on: bool) -> None:
+    """conv1's BN apply riding in the projection shortcut's launch on / off (A/B)."""
+    _RIDE_ON[0] = bool(on)
+
+
+def arm_apply_ride(x) -> None:
+    _flush_apply_ride()
+    _RIDE["x"] = x if (_RIDE_ON[0] and _BN_FUSED[0] and x is not None and x.is_cuda
+                       and torch.is_grad_enabled()) else None
+
+
+def _flush_apply_ride() -> None:
+    pend, _RIDE["apply"] = _RIDE["apply"], None
+    if pend is not None:
+        stream, args, _ = pend
+        with torch.cuda.stream(stream):
+            _ext.call("mda_bn_apply_fin", *args)
+
+
+def finish_apply_ride() -> None:
+    _RIDE["x"] = None
+    _flush_apply_ride()
+
+
 # pw -> dw virtual input / dw dgrad BN-sum epilogue: both OFF by default -- each
 # removes a memory pass but its kernel variant needs more VGPRs (fewer waves)
 # or a capped grid, and the steps measured slower (profiles/r4_dw_fusion_ab.md)
@@ -1023,6 +1060,7 @@ class _ConvBNActTrain(torch.autograd.Function):
         gc = G > 1 and cin_w % 8 == 0 and (weight.shape[0] // G) % 8 == 0 and _GROUPED_COMPACT[0]
         link_in = getattr(x, "_mda_bnlink", None) if (need_dx and (G == 1 or gc) and _BNB_ON[0]) else None
         chpad = G == 1 and (not need_dx) and needs_channel_pad(cin_w)
+        x_in = x
         x = pad_channels8(x) if chpad else _cl_bf16(x)
         N, Cin, H, W = x.shape
         Cout, _, KH, KW = weight.shape
@@ -1100,8 +1138,20 @@ class _ConvBNActTrain(torch.autograd.Function):
             # conv whose epilogue adds the BN sums into the stream's slot, then
             # apply with the finalize in its prologue (2 launches)
             reg = _region(Cout, dev)
-            _ext.call("mda_conv_fwd_bnacc_g", x, wf, y, part, reg, N, H, W, Cin, Ho, Wo,
-                      Cout, KH, KW, stride, pad, Kp, tile, splits, G if gc else 1)
+            pend = _RIDE["apply"]
+            rc = _ext.NOT_SERVED
+            if (pend is not None and x_in is _RIDE["x"] and pend[0] == torch.cuda.current_stream()
+                    and KH == 1 and KW == 1 and pad == 0 and G == 1 and splits == 1 and not gc):
+                # a projection shortcut: conv1's parked BN apply rides in this launch
+                rc = _ext.call("mda_conv1x1_bnacc_apply", x, wf, y, reg, N, H, W, Cin, Kp, Ho, Wo,
+                               Cout, stride, *pend[1], ok=(0, _ext.NOT_SERVED))
+                if rc == 0:
+                    _RIDE["apply"] = None
+                    _RIDE_COUNT[0] += 1
+            if rc != 0:
+                _flush_apply_ride()
+                _ext.call("mda_conv_fwd_bnacc_g", x, wf, y, part, reg, N, H, W, Cin, Ho, Wo,
+                          Cout, KH, KW, stride, pad, Kp, tile, splits, G if gc else 1)
             if defer:
                 # no apply: the consumer's apply finalizes this BN (VirtualBN)
                 ctx.vbn = VirtualBN(reg, gamma.detach(), beta.detach(), bn, stats, act)
@@ -1112,9 +1162,15 @@ class _ConvBNActTrain(torch.autograd.Function):
                           rv.gamma, rv.beta, rv.bn.running_mean, rv.bn.running_var, rv.stats,
                           float(rv.bn.momentum), float(rv.bn.eps), rv.bn.num_batches_tracked)
             else:
-                _ext.call("mda_bn_apply_fin", y, reg, M, Cout, gamma.detach(), beta.detach(),
-                          bn.running_mean, bn.running_var, stats, float(bn.momentum), float(bn.eps),
-                          bn.num_batches_tracked, res, out, pre, act)
+                args = (y, reg, M, Cout, gamma.detach(), beta.detach(), bn.running_mean,
+                        bn.running_var, stats, float(bn.momentum), float(bn.eps),
+                        bn.num_batches_tracked, res, out, pre, act)
+                if (_RIDE["x"] is not None and x_in is _RIDE["x"] and _RIDE["apply"] is None
+                        and res is None and pre is None):
+                    # conv1 of an armed block: park its apply for the shortcut's launch
+                    _RIDE["apply"] = (torch.cuda.current_stream(), args, (y, out))
+                else:
+                    _ext.call("mda_bn_apply_fin", *args)
         else:
             if rv is not None:
                 raise RuntimeError("virtual residuals need the fused BN kernels (MDA_BN_FUSED=1)")

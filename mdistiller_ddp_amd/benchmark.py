@@ -68,28 +68,6 @@ def run(cfg_file: str, per_gpu_batch: int, steps: int, warmup: int, opts=(), use
     from .data.synthetic import SyntheticLoader, dataset_shape
     from .runtime import streams
 
-    prio = int(os.environ.get("MDA_STEP_PRIO", "0"))
-    if prio and torch.cuda.is_available():
-        # A/B: the whole step (and everything it forks from the current
-        # stream) on a stream of HIP priority `prio` (< 0 = higher)
-        with torch.cuda.stream(torch.cuda.Stream(priority=prio)):
-            return _run(cfg_file, per_gpu_batch, steps, warmup, opts, use_graph, backend, dtype,
-                        teacher_stream, dataset, crd_k, check_replicas)
-    return _run(cfg_file, per_gpu_batch, steps, warmup, opts, use_graph, backend, dtype,
-                teacher_stream, dataset, crd_k, check_replicas)
-
-
-def _run(cfg_file, per_gpu_batch, steps, warmup, opts, use_graph, backend, dtype, teacher_stream,
-         dataset, crd_k, check_replicas):
-    from .ops.backend import set_backend
-    from .parallel import dist as D
-    from .config import get_cfg
-    from .engine.build import build_distiller
-    from .engine.step import TrainStep
-    from .engine.trainer import BATCH_KEYS
-    from .data.synthetic import SyntheticLoader, dataset_shape
-    from .runtime import streams
-
     set_backend(backend)
     streams.set_enabled(teacher_stream)
     # release the graphs of an earlier run in this process first: a live graph

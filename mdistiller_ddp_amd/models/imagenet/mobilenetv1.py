@@ -74,9 +74,7 @@ class MobileNetV1(nn.Module, ModelBase):
         h = stem
         for a, b in self.STAGES:
             for i in range(a, b):
-                # a block's activated output feeds only the next block's depthwise
-                # conv inside a stage: that conv applies the BN on load (run_seq)
-                h = run_seq(self.model[i], h, next_seq=self.model[i + 1] if i + 1 < b else None)[0]
+                h = run_seq(self.model[i], h)[0]
             pres.append(h)
             h = F.relu(h)
             feats.append(h)

@@ -44,8 +44,6 @@ SIGNATURES = {
     "mda_event_destroy": "p",
     "mda_event_record": "pis",
     "mda_clock_probe": "pis",
-    "mda_stream_create": "iiip",
-    "mda_stream_destroy": "p",
     "mda_stream_wait_event": "pis",
     # convolution (csrc/conv_igemm.hip)
     "mda_conv_fwd": "pppppppp" + "i" * 15 + "s",
@@ -88,11 +86,9 @@ SIGNATURES = {
     "mda_dw_pack": "pppiis",
     "mda_dw_fwd": "ppppppp" + "i" * 11 + "s",
     "mda_dw_dgrad": "ppp" + "i" * 10 + "s",
-    "mda_dw_dgrad_bnsum": "ppp" + "i" * 10 + "ppp" + "i" + "pp" + "s",
     "mda_dw_wgrad_blocks": "iiiip",
-    "mda_dw_wgrad": "pppp" + "i" * 12 + "pi" + "s",
+    "mda_dw_wgrad": "pppp" + "i" * 12 + "s",
     "mda_dw_wgrad_blocks2": "i" * 8 + "p",
-    "mda_dw_fwd_bnacc_vin": "pppp" + "i" * 10 + "pppppp" + "ff" + "pi" + "s",
     # training-mode BatchNorm (csrc/bn.hip)
     "mda_bn_stats": "pii" + "pp" + "pppp" + "pppp" + "ffps",
     "mda_bn_apply": "pppppp" + "iii" + "s",

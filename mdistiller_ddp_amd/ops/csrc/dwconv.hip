@@ -104,59 +104,7 @@ struct DwParams {
   // separate statistics pass; needs a grid stride that is a multiple of C / V
   // (every thread keeps one channel group), see launch_fwd
   BnRegion* stats_slot;
-  // dgrad only (BnLink, csrc/conv_igemm.hip conv_epilogue_bnb): dx is the
-  // whole output gradient of the training BN that produced this conv's input;
-  // the kernel also adds that BN's backward sums (sum dz, sum dz*xhat of the
-  // stored dx through the activation) into bnb_slot
-  const bf16_t* bnb_y;      // that BN's input [N, H, W, C]
-  const bf16_t* bnb_res;    // its residual (activation after the add) or null
-  const float* bnb_stats;   // its [4][C] mean, rstd, scale, shift
-  const float* bnb_vres;    // virtual residual stats [4][C] or null
-  int bnb_act;
-  BnRegion* bnb_slot;
-  // forward only (virtual input, VirtualBN of ops/hip_train.py): x is the RAW
-  // output of a training conv whose BN + activation were never applied; its
-  // batch sums are in in_reg.  Every thread finalizes its channel group's
-  // scale / shift in the prologue (block 0 also writes the [4][C] stats and
-  // the running statistics) and loads act(x * scale + shift) (zero padding
-  // stays zero) -- the producer's apply pass never runs.
-  BnRegion* in_reg;
-  const float* in_gamma; const float* in_beta;
-  float* in_rmean; float* in_rvar; float* in_stats;
-  float in_mom, in_eps;
-  int64_t* in_nbt;
-  int in_act;
 };
-
-// BN finalize of channel c from a region (sums of a producer's output over
-// M rows): scale / shift; with `wr` (block 0) also the [4][C] stats and the
-// running statistics (csrc/bn.hip fin_channel, same arithmetic).
-__device__ __forceinline__ void dw_fin_channel(const DwParams& p, int c, int64_t M, bool wr,
-                                               float& sc, float& sh) {
-  const int C = p.C, SH = slot_shards(C);
-  double t0 = 0.0, t1 = 0.0;
-  for (int k = 0; k < SH; ++k) {
-    t0 += region_acc(p.in_reg, C, k, 0)[c];
-    t1 += region_acc(p.in_reg, C, k, 1)[c];
-  }
-  const double mean = t0 / (double)M;
-  double var = t1 / (double)M - mean * mean;
-  if (var < 0) var = 0;
-  const float rstd = (float)(1.0 / sqrt(var + (double)p.in_eps));
-  sc = (p.in_gamma ? p.in_gamma[c] : 1.f) * rstd;
-  sh = (p.in_beta ? p.in_beta[c] : 0.f) - (float)mean * sc;
-  if (wr) {
-    p.in_stats[c] = (float)mean;
-    p.in_stats[C + c] = rstd;
-    p.in_stats[2 * C + c] = sc;
-    p.in_stats[3 * C + c] = sh;
-    if (p.in_rmean) {
-      const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
-      p.in_rmean[c] = (1.f - p.in_mom) * p.in_rmean[c] + p.in_mom * (float)mean;
-      p.in_rvar[c] = (1.f - p.in_mom) * p.in_rvar[c] + p.in_mom * (float)unbiased;
-    }
-  }
-}
 
 // Block channel sums of the per-thread (channel group) partials st1/st2 into
 // a region shard; deterministic: thread t always held channel group
@@ -187,7 +135,7 @@ __device__ __forceinline__ void dw_block_sums(BnRegion* slot, int C, const float
   }
 }
 
-template <int V, int S, bool VIN>
+template <int V, int S>
 __global__ void __launch_bounds__(256)
 dw_fwd_kernel(const DwParams p) {
   constexpr int NCOLS = (OWT - 1) * S + KS;
@@ -197,26 +145,6 @@ dw_fwd_kernel(const DwParams p) {
   float st1[V], st2[V];
 #pragma unroll
   for (int v = 0; v < V; ++v) st1[v] = st2[v] = 0.f;
-  // virtual input: this thread's channel group never changes (grid stride a
-  // multiple of CG, region_grid), so its input scale / shift are finalized once
-  // (a separate instantiation: the plain kernel keeps its register budget)
-  constexpr bool vin = VIN;
-  float isc[V], ish[V];
-  if constexpr (VIN) {
-    // the block finalizes every channel once (LDS), each thread takes its group's
-    __shared__ float s_in[2][SLOT_CMAX];
-    const int64_t Min = (int64_t)p.N * p.H * p.W;
-    for (int c = threadIdx.x; c < p.C; c += blockDim.x)
-      dw_fin_channel(p, c, Min, blockIdx.x == 0, s_in[0][c], s_in[1][c]);
-    if (blockIdx.x == 0 && threadIdx.x == 0 && p.in_nbt) p.in_nbt[0] += 1;
-    __syncthreads();
-    const int c0 = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) % CG) * V;
-#pragma unroll
-    for (int v = 0; v < V; ++v) {
-      isc[v] = s_in[0][c0 + v];
-      ish[v] = s_in[1][c0 + v];
-    }
-  }
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int cg = (int)(i % CG);
@@ -233,7 +161,6 @@ dw_fwd_kernel(const DwParams p) {
 #pragma unroll
     for (int t = 0; t < KS * KS; ++t) ld_w<V>(p.w + t * p.C + c0, wv[t]);
     typename vec<V>::t raw[KS][NCOLS];
-    uint32_t okm = 0;  // in-bounds taps (zero padding is zero after the input's apply too)
 #pragma unroll
     for (int kh = 0; kh < KS; ++kh) {
       const int ih = ho * S - p.pad + kh;
@@ -242,9 +169,7 @@ dw_fwd_kernel(const DwParams p) {
 #pragma unroll
       for (int q = 0; q < NCOLS; ++q) {
         const int iw = iw0 + q;
-        const bool ok = okr && (unsigned)iw < (unsigned)p.W;
-        raw[kh][q] = ld_raw<V>(row + (int64_t)iw * p.C, ok);
-        okm |= (ok ? 1u : 0u) << (kh * NCOLS + q);
+        raw[kh][q] = ld_raw<V>(row + (int64_t)iw * p.C, okr && (unsigned)iw < (unsigned)p.W);
       }
     }
     float acc[OWT][V];
@@ -256,18 +181,7 @@ dw_fwd_kernel(const DwParams p) {
     for (int kh = 0; kh < KS; ++kh) {
       float xin[NCOLS][V];
 #pragma unroll
-      for (int q = 0; q < NCOLS; ++q) {
-        unpack<V>(raw[kh][q], xin[q]);
-        if (vin) {
-          const bool ok = (okm >> (kh * NCOLS + q)) & 1u;
-#pragma unroll
-          for (int v = 0; v < V; ++v) {
-            // the producer's apply rounds to bf16: same value here
-            const float z = bf2f(f2bf(act_fn(xin[q][v] * isc[v] + ish[v], p.in_act)));
-            xin[q][v] = ok ? z : 0.f;
-          }
-        }
-      }
+      for (int q = 0; q < NCOLS; ++q) unpack<V>(raw[kh][q], xin[q]);
 #pragma unroll
       for (int kw = 0; kw < KS; ++kw)
 #pragma unroll
@@ -317,23 +231,12 @@ dw_fwd_kernel(const DwParams p) {
 // over taps landing on the stride grid.  p.x = dy, p.y = dx; H/W = input dims.
 // S = 1: dx[h, w0 + j] = sum dy[h + p - kh, w0 + j + p - kw] * w[kh, kw], the
 // OWT + 2 dy columns of each of the three rows loaded once, all up front.
-__device__ __forceinline__ float dw_act_grad(float z, int act) {
-  if (act == 1) return z > 0.f ? 1.f : 0.f;
-  if (act == 2) return (z > 0.f && z < 6.f) ? 1.f : 0.f;
-  return 1.f;
-}
-
-template <int V, int S, bool BNB>
+template <int V, int S>
 __global__ void __launch_bounds__(256)
 dw_dgrad_kernel(const DwParams p) {
   const int CG = p.C / V;
   const int WT = (p.W + OWT - 1) / OWT;
   const int64_t total = (int64_t)p.N * p.H * WT * CG;
-  constexpr bool bnb = BNB;  // (a separate instantiation, see dw_fwd_kernel)
-  const bool zres = bnb && p.bnb_res != nullptr && p.bnb_act != 0;
-  float st1[V], st2[V];
-#pragma unroll
-  for (int v = 0; v < V; ++v) st1[v] = st2[v] = 0.f;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int cg = (int)(i % CG);
@@ -407,57 +310,13 @@ dw_dgrad_kernel(const DwParams p) {
       }
     }
     }
-    if constexpr (!BNB) {
-#pragma unroll
-      for (int j = 0; j < OWT; ++j) {
-        const int w = w0 + j;
-        if (w >= p.W) break;
-        st_vec<V>(p.y + (((int64_t)n * p.H + h) * p.W + w) * p.C + c0, acc[j]);
-      }
-      continue;
-    } else {
-    // BnLink epilogue: every load first, then the stores and the sums of the
-    // STORED (bf16) values
-    typename vec<V>::t yr[OWT], rr[OWT];
-    const int64_t o0 = (((int64_t)n * p.H + h) * p.W + w0) * p.C + c0;
 #pragma unroll
     for (int j = 0; j < OWT; ++j) {
-      const bool ok = w0 + j < p.W;
-      yr[j] = ld_raw<V>(p.bnb_y + o0 + (int64_t)j * p.C, ok);
-      rr[j] = ld_raw<V>(zres ? p.bnb_res + o0 + (int64_t)j * p.C : p.bnb_y, ok && zres);
-    }
-    float mu[V], rs[V], sc[V], sh[V], vsc[V], vsh[V];
-#pragma unroll
-    for (int v = 0; v < V; ++v) {
-      mu[v] = p.bnb_stats[c0 + v];
-      rs[v] = p.bnb_stats[p.C + c0 + v];
-      sc[v] = p.bnb_stats[2 * p.C + c0 + v];
-      sh[v] = p.bnb_stats[3 * p.C + c0 + v];
-      vsc[v] = p.bnb_vres ? p.bnb_vres[2 * p.C + c0 + v] : 1.f;
-      vsh[v] = p.bnb_vres ? p.bnb_vres[3 * p.C + c0 + v] : 0.f;
-    }
-#pragma unroll
-    for (int j = 0; j < OWT; ++j) {
-      if (w0 + j >= p.W) break;
-      st_vec<V>(p.y + o0 + (int64_t)j * p.C, acc[j]);
-      float yf[V], rf[V];
-      unpack<V>(yr[j], yf);
-      unpack<V>(rr[j], rf);
-#pragma unroll
-      for (int v = 0; v < V; ++v) {
-        float d = bf2f(f2bf(acc[j][v]));
-        if (p.bnb_act != 0) {
-          float z = yf[v] * sc[v] + sh[v];
-          if (zres) z += rf[v] * vsc[v] + vsh[v];
-          d *= dw_act_grad(z, p.bnb_act);
-        }
-        st1[v] += d;
-        st2[v] += d * ((yf[v] - mu[v]) * rs[v]);
-      }
-    }
+      const int w = w0 + j;
+      if (w >= p.W) break;
+      st_vec<V>(p.y + (((int64_t)n * p.H + h) * p.W + w) * p.C + c0, acc[j]);
     }
   }
-  if constexpr (BNB) dw_block_sums<V>(p.bnb_slot, p.C, st1, st2);
 }
 
 // Per-block partials of dW[tap, c] = sum_m dy[m, c] * x[src(m, tap), c].
@@ -465,11 +324,11 @@ dw_dgrad_kernel(const DwParams p) {
 // output pixels of one output row: it loads the 3 x ((OWT-1)*S + 3) input
 // columns and OWT dy vectors once (~5.5 loads per pixel instead of 10, all
 // independent), accumulating acc[9][V].  partial[blk][9][C].
-template <int V, int S, bool VIN>
+template <int V, int S>
 __global__ void __launch_bounds__(256)
 dw_wgrad_partial_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
                         float* __restrict__ partial, int N, int H, int W, int C, int Ho, int Wo,
-                        int pad, const float* __restrict__ in_stats, int in_act) {
+                        int pad) {
   constexpr int NCOLS = (OWT - 1) * S + KS;
   constexpr int KK = KS * KS;
   constexpr int TG = 3;  // taps per reduction round
@@ -483,15 +342,6 @@ dw_wgrad_partial_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__
   const int c0 = cg * V;
   const int WT = (Wo + OWT - 1) / OWT;
   const int64_t items = (int64_t)N * Ho * WT;
-  // virtual input (see DwParams::in_reg): x is the raw producer output, the
-  // input is act(x * scale + shift) from the producer's [4][C] stats
-  constexpr bool vin = VIN;  // (a separate instantiation, see dw_fwd_kernel)
-  float isc[V], ish[V];
-#pragma unroll
-  for (int v = 0; v < V; ++v) {
-    isc[v] = vin && active ? in_stats[2 * C + c0 + v] : 1.f;
-    ish[v] = vin && active ? in_stats[3 * C + c0 + v] : 0.f;
-  }
   float acc[KK][V];
 #pragma unroll
   for (int t = 0; t < KK; ++t)
@@ -506,7 +356,6 @@ dw_wgrad_partial_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__
       const int wo0 = wt * OWT;
       const int iw0 = wo0 * S - pad;
       typename vec<V>::t draw[OWT], raw[KS][NCOLS];
-      uint32_t okm = 0;
       const bf16_t* drow = dy + (((int64_t)n * Ho + ho) * Wo + wo0) * C + c0;
 #pragma unroll
       for (int j = 0; j < OWT; ++j) draw[j] = ld_raw<V>(drow + (int64_t)j * C, wo0 + j < Wo);
@@ -518,9 +367,7 @@ dw_wgrad_partial_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__
 #pragma unroll
         for (int q = 0; q < NCOLS; ++q) {
           const int iw = iw0 + q;
-          const bool ok = okr && (unsigned)iw < (unsigned)W;
-          raw[kh][q] = ld_raw<V>(row + (int64_t)iw * C, ok);
-          okm |= (ok ? 1u : 0u) << (kh * NCOLS + q);
+          raw[kh][q] = ld_raw<V>(row + (int64_t)iw * C, okr && (unsigned)iw < (unsigned)W);
         }
       }
       float d[OWT][V];
@@ -530,17 +377,7 @@ dw_wgrad_partial_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__
       for (int kh = 0; kh < KS; ++kh) {
         float xin[NCOLS][V];
 #pragma unroll
-        for (int q = 0; q < NCOLS; ++q) {
-          unpack<V>(raw[kh][q], xin[q]);
-          if (vin) {
-            const bool ok = (okm >> (kh * NCOLS + q)) & 1u;
-#pragma unroll
-            for (int v = 0; v < V; ++v) {
-              const float z = bf2f(f2bf(act_fn(xin[q][v] * isc[v] + ish[v], in_act)));
-              xin[q][v] = ok ? z : 0.f;
-            }
-          }
-        }
+        for (int q = 0; q < NCOLS; ++q) unpack<V>(raw[kh][q], xin[q]);
 #pragma unroll
         for (int kw = 0; kw < KS; ++kw)
 #pragma unroll
@@ -611,48 +448,28 @@ inline int64_t dwt_budget() {
   return b;
 }
 
-__device__ __forceinline__ uint4 dw_vin8(uint4 v, const float* sc, const float* sh, int act) {
-  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-  uint32_t o[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float a = act_fn(__uint_as_float(w[k] << 16) * sc[2 * k] + sh[2 * k], act);
-    const float b = act_fn(__uint_as_float(w[k] & 0xffff0000u) * sc[2 * k + 1] + sh[2 * k + 1], act);
-    o[k] = pack_bf16x2(a, b);
-  }
-  return make_uint4(o[0], o[1], o[2], o[3]);
-}
-
 // x rows [ih0, ih0 + rin) x cols [-1, W] of channels [c0, c0 + cc) -> xs
-// (zero outside the image); VIN: act(x * sc + sh) with sc/sh indexed by the
-// chunk-local channel.
-template <bool VIN>
+// (zero outside the image).
 __device__ __forceinline__ void dw_fill_x(const bf16_t* __restrict__ x, bf16_t* xs, int n, int H, int W,
-                                          int C, int c0, int cc, int ih0, int rin, const float* vsc,
-                                          const float* vsh, int act) {
+                                          int C, int c0, int cc, int ih0, int rin) {
   const int Wp = W + 2, cv = cc / 8;
   for (int i = threadIdx.x; i < rin * Wp * cv; i += blockDim.x) {
     const int pos = i / cv, q = i - pos * cv;
     const int r = pos / Wp, col = pos - r * Wp;
     const int ih = ih0 + r, iw = col - 1;
     uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) {
+    if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
       v = *(const uint4*)(x + (((int64_t)n * H + ih) * W + iw) * C + c0 + 8 * q);
-      if constexpr (VIN) v = dw_vin8(v, vsc + 8 * q, vsh + 8 * q, act);
-    }
     *(uint4*)(xs + (size_t)pos * cc + 8 * q) = v;
   }
 }
 
-template <int S, bool VIN>
+template <int S>
 __global__ void __launch_bounds__(256) dw_wgrad_tile_kernel(const bf16_t* __restrict__ x,
                                                             const bf16_t* __restrict__ dy,
                                                             float* __restrict__ partial, int N, int H,
-                                                            int W, int C, int Ho, int Wo, int tr, int cc,
-                                                            const float* __restrict__ in_stats,
-                                                            int in_act) {
+                                                            int W, int C, int Ho, int Wo, int tr, int cc) {
   extern __shared__ __attribute__((aligned(16))) bf16_t dwt_sm[];
-  __shared__ float s_v[2][64];
   const int tid = threadIdx.x;
   const int nrt = (Ho + tr - 1) / tr;
   const int blk = blockIdx.x, n = blk / nrt, rt = blk - n * nrt;
@@ -661,14 +478,7 @@ __global__ void __launch_bounds__(256) dw_wgrad_tile_kernel(const bf16_t* __rest
   const int rin = (tr - 1) * S + 3, Wp = W + 2, cv = cc / 8;
   bf16_t* xs = dwt_sm;
   bf16_t* ds = dwt_sm + (size_t)rin * Wp * cc;
-  if constexpr (VIN) {
-    if (tid < cc) {
-      s_v[0][tid] = in_stats[2 * C + c0 + tid];
-      s_v[1][tid] = in_stats[3 * C + c0 + tid];
-    }
-    __syncthreads();
-  }
-  dw_fill_x<VIN>(x, xs, n, H, W, C, c0, cc, ho0 * S - 1, rin, s_v[0], s_v[1], in_act);
+  dw_fill_x(x, xs, n, H, W, C, c0, cc, ho0 * S - 1, rin);
   for (int i = tid; i < tr * Wo * cv; i += 256) {
     const int pos = i / cv, q = i - pos * cv;
     const int r = pos / Wo, col = pos - r * Wo;
@@ -704,25 +514,18 @@ __global__ void __launch_bounds__(256) dw_wgrad_tile_kernel(const bf16_t* __rest
 }
 
 // Training forward: raw bf16 output + the BN batch sums of the stored values
-// into p.stats_slot (or no statistics).  VIN: p.in_reg finalized per chunk.
-template <int S, bool VIN>
+// into p.stats_slot (or no statistics).
+template <int S>
 __global__ void __launch_bounds__(256) dw_fwd_tile_kernel(const DwParams p, int tr, int cc) {
   extern __shared__ __attribute__((aligned(16))) bf16_t dwt_sm[];
-  __shared__ float s_v[2][64];
   const int tid = threadIdx.x;
   const int nrt = (p.Ho + tr - 1) / tr;
   const int blk = blockIdx.x, n = blk / nrt, rt = blk - n * nrt;
   const int c0 = blockIdx.y * cc;
   const int ho0 = rt * tr, hon = min(tr, p.Ho - ho0);
   const int rin = (tr - 1) * S + 3, Wp = p.W + 2;
-  if constexpr (VIN) {
-    const int64_t Min = (int64_t)p.N * p.H * p.W;
-    if (tid < cc) dw_fin_channel(p, c0 + tid, Min, blk == 0, s_v[0][tid], s_v[1][tid]);
-    if (blk == 0 && blockIdx.y == 0 && tid == 0 && p.in_nbt) p.in_nbt[0] += 1;
-    __syncthreads();
-  }
   bf16_t* xs = dwt_sm;
-  dw_fill_x<VIN>(p.x, xs, n, p.H, p.W, p.C, c0, cc, ho0 * S - 1, rin, s_v[0], s_v[1], p.in_act);
+  dw_fill_x(p.x, xs, n, p.H, p.W, p.C, c0, cc, ho0 * S - 1, rin);
   __syncthreads();
   const int c = tid % cc, sl = tid / cc, nsl = 256 / cc;
   float wv[9];
@@ -912,32 +715,18 @@ int launch_fwd(const DwParams& p, hipStream_t st) {
       dw_tile_plan(p.H, p.W, p.C, p.Ho, p.Wo, p.stride, p.pad, false, tr, cc)) {
     const dim3 g((unsigned)(p.N * ((p.Ho + tr - 1) / tr)), (unsigned)(p.C / cc));
     const size_t lds = dw_tile_lds(p.W, p.Wo, p.stride, tr, cc, false);
-#define DW_FT(SS, VV) hipLaunchKernelGGL((dw_fwd_tile_kernel<SS, VV>), g, dim3(256), lds, st, p, tr, cc)
-    if (p.stride == 1) { if (p.in_reg) DW_FT(1, true); else DW_FT(1, false); }
-    else { if (p.in_reg) DW_FT(2, true); else DW_FT(2, false); }
-#undef DW_FT
+    if (p.stride == 1) hipLaunchKernelGGL((dw_fwd_tile_kernel<1>), g, dim3(256), lds, st, p, tr, cc);
+    else hipLaunchKernelGGL((dw_fwd_tile_kernel<2>), g, dim3(256), lds, st, p, tr, cc);
     return (int)hipGetLastError();
   }
   const int V = vwidth(p.C);
   const int64_t work = (int64_t)p.N * p.Ho * ((p.Wo + OWT - 1) / OWT) * (p.C / V);
   int nb = grid_for(work);
-  if (p.stats_slot) {
-    // grid stride a multiple of CG (each thread keeps its channel group); at most
-    // 256 blocks per region shard, so each region address sees few atomics
-    const int CG = p.C / V;
-    int a = CG, b = 256;
-    while (b) { const int t = a % b; a = b; b = t; }
-    const int unit = CG / a;  // blocks per stride period
-    const int cap = 256 * slot_shards(p.C);
-    nb = nb < cap ? nb : cap;
-    nb = (nb + unit - 1) / unit * unit;
-  }
+  // grid stride a multiple of CG (each thread keeps its channel group); at most
+  // 256 blocks per region shard, so each region address sees few atomics
+  if (p.stats_slot) nb = region_grid(nb, p.C, V);
   const dim3 g(nb);
-#define DW_FWD(VV, SS)                                                                   \
-  do {                                                                                   \
-    if (p.in_reg) hipLaunchKernelGGL((dw_fwd_kernel<VV, SS, true>), g, dim3(256), 0, st, p); \
-    else hipLaunchKernelGGL((dw_fwd_kernel<VV, SS, false>), g, dim3(256), 0, st, p);         \
-  } while (0)
+#define DW_FWD(VV, SS) hipLaunchKernelGGL((dw_fwd_kernel<VV, SS>), g, dim3(256), 0, st, p)
   if (p.stride == 1) {
     if (V == 8) DW_FWD(8, 1); else if (V == 4) DW_FWD(4, 1); else if (V == 2) DW_FWD(2, 1); else DW_FWD(1, 1);
   } else {
@@ -973,7 +762,7 @@ int launch_dgrad(const DwParams& p, hipStream_t st) {
   const int64_t N = p.N, H = p.H, W = p.W, C = p.C;
   const int stride = p.stride;
   int tr, cc;
-  if (!p.bnb_slot && dw_tile_plan((int)H, (int)W, (int)C, (int)H, (int)W, 1, p.pad, false, tr, cc)) {
+  if (dw_tile_plan((int)H, (int)W, (int)C, (int)H, (int)W, 1, p.pad, false, tr, cc)) {
     const dim3 g((unsigned)(N * ((H + tr - 1) / tr)), (unsigned)(C / cc));
     const size_t lds = dw_tile_lds((int)W, (int)W, 1, tr, cc, false);
     if (stride == 1) hipLaunchKernelGGL((dw_dgrad_tile_kernel<1>), g, dim3(256), lds, st, p, tr, cc);
@@ -982,14 +771,8 @@ int launch_dgrad(const DwParams& p, hipStream_t st) {
   }
   const int V = vwidth((int)C);
   const int64_t work = N * H * ((W + OWT - 1) / OWT) * (C / V);
-  int nb = grid_for(work);
-  if (p.bnb_slot) nb = region_grid(nb, (int)C, V);
-  const dim3 g(nb);
-#define DW_DG(VV, SS)                                                                        \
-  do {                                                                                       \
-    if (p.bnb_slot) hipLaunchKernelGGL((dw_dgrad_kernel<VV, SS, true>), g, dim3(256), 0, st, p); \
-    else hipLaunchKernelGGL((dw_dgrad_kernel<VV, SS, false>), g, dim3(256), 0, st, p);           \
-  } while (0)
+  const dim3 g(grid_for(work));
+#define DW_DG(VV, SS) hipLaunchKernelGGL((dw_dgrad_kernel<VV, SS>), g, dim3(256), 0, st, p)
   if (stride == 1) {
     if (V == 8) DW_DG(8, 1); else if (V == 4) DW_DG(4, 1); else if (V == 2) DW_DG(2, 1); else DW_DG(1, 1);
   } else {
@@ -1007,24 +790,6 @@ MDA_API int mda_dw_dgrad(const void* dy, const float* w, void* dx, int64_t N, in
   if (KH != KS || KW != KS || stride < 1 || stride > 2) return (int)hipErrorInvalidValue;
   DwParams p{(const bf16_t*)dy, w, nullptr, nullptr, nullptr, (bf16_t*)dx, nullptr, (int)N,
              (int)H, (int)W, (int)C, (int)Ho, (int)Wo, (int)KH, (int)KW, (int)stride, (int)pad, 0};
-  return launch_dgrad(p, st);
-}
-
-// mda_dw_dgrad + the BnLink epilogue: dx is the whole output gradient of the
-// training BN (input y, residual res, stats, act, virtual-residual stats
-// vres) that produced this conv's input; its backward sums go into region.
-MDA_API int mda_dw_dgrad_bnsum(const void* dy, const float* w, void* dx, int64_t N, int64_t H,
-                               int64_t W, int64_t C, int64_t Ho, int64_t Wo, int64_t KH, int64_t KW,
-                               int64_t stride, int64_t pad, const void* y, const void* res,
-                               const float* stats, int64_t act, void* region, const float* vres,
-                               hipStream_t st) {
-  if (KH != KS || KW != KS || stride < 1 || stride > 2 || region == nullptr || y == nullptr ||
-      stats == nullptr || C > SLOT_CMAX || C % 8)
-    return (int)hipErrorInvalidValue;
-  DwParams p{(const bf16_t*)dy, w, nullptr, nullptr, nullptr, (bf16_t*)dx, nullptr, (int)N,
-             (int)H, (int)W, (int)C, (int)Ho, (int)Wo, (int)KH, (int)KW, (int)stride, (int)pad, 0,
-             nullptr, (const bf16_t*)y, (const bf16_t*)res, stats, vres, (int)act,
-             (BnRegion*)region};
   return launch_dgrad(p, st);
 }
 
@@ -1065,12 +830,10 @@ MDA_API int mda_dw_wgrad_blocks(int64_t N, int64_t Ho, int64_t Wo, int64_t C, in
 
 // x [N,H,W,C], dy [N,Ho,Wo,C] bf16; partial >= nblk*KH*KW*C floats;
 // grad fp32 [C, KH, KW] (accumulated when accumulate != 0).
-// in_stats (or null): x is a virtual input (raw producer output; the input is
-// act(x * in_stats[2] + in_stats[3]), see DwParams::in_reg).
 MDA_API int mda_dw_wgrad(const void* x, const void* dy, float* partial, float* grad, int64_t N,
                          int64_t H, int64_t W, int64_t C, int64_t Ho, int64_t Wo, int64_t KH,
                          int64_t KW, int64_t stride, int64_t pad, int64_t nblk,
-                         int64_t accumulate, const float* in_stats, int64_t in_act, hipStream_t st) {
+                         int64_t accumulate, hipStream_t st) {
   if (KH != KS || KW != KS || stride < 1 || stride > 2 || nblk < 1) return (int)hipErrorInvalidValue;
   int tr, cc;
   if (dw_tile_plan((int)H, (int)W, (int)C, (int)Ho, (int)Wo, (int)stride, (int)pad, true, tr, cc)) {
@@ -1078,27 +841,19 @@ MDA_API int mda_dw_wgrad(const void* x, const void* dy, float* partial, float* g
     if (nb != nblk) return (int)hipErrorInvalidValue;  // partial rows sized by mda_dw_wgrad_blocks2
     const dim3 g((unsigned)nb, (unsigned)(C / cc));
     const size_t lds = dw_tile_lds((int)W, (int)Wo, (int)stride, tr, cc, true);
-#define DW_WT(SS, VV)                                                                          \
-  hipLaunchKernelGGL((dw_wgrad_tile_kernel<SS, VV>), g, dim3(256), lds, st, (const bf16_t*)x,    \
+#define DW_WT(SS)                                                                              \
+  hipLaunchKernelGGL((dw_wgrad_tile_kernel<SS>), g, dim3(256), lds, st, (const bf16_t*)x,        \
                      (const bf16_t*)dy, partial, (int)N, (int)H, (int)W, (int)C, (int)Ho, (int)Wo, \
-                     tr, cc, in_stats, (int)in_act)
-    if (stride == 1) { if (in_stats) DW_WT(1, true); else DW_WT(1, false); }
-    else { if (in_stats) DW_WT(2, true); else DW_WT(2, false); }
+                     tr, cc)
+    if (stride == 1) DW_WT(1); else DW_WT(2);
 #undef DW_WT
   } else {
   const int V = vwidth((int)C);
   if (C / V > 256) return (int)hipErrorInvalidValue;
-#define DW_WG(VV, SS)                                                                         \
-  do {                                                                                        \
-    if (in_stats)                                                                             \
-      hipLaunchKernelGGL((dw_wgrad_partial_kernel<VV, SS, true>), dim3(nblk), dim3(256), 0, st, \
-                         (const bf16_t*)x, (const bf16_t*)dy, partial, (int)N, (int)H, (int)W,  \
-                         (int)C, (int)Ho, (int)Wo, (int)pad, in_stats, (int)in_act);            \
-    else                                                                                      \
-      hipLaunchKernelGGL((dw_wgrad_partial_kernel<VV, SS, false>), dim3(nblk), dim3(256), 0, st, \
-                         (const bf16_t*)x, (const bf16_t*)dy, partial, (int)N, (int)H, (int)W,  \
-                         (int)C, (int)Ho, (int)Wo, (int)pad, in_stats, (int)in_act);            \
-  } while (0)
+#define DW_WG(VV, SS)                                                                       \
+  hipLaunchKernelGGL((dw_wgrad_partial_kernel<VV, SS>), dim3(nblk), dim3(256), 0, st,          \
+                     (const bf16_t*)x, (const bf16_t*)dy, partial, (int)N, (int)H, (int)W,      \
+                     (int)C, (int)Ho, (int)Wo, (int)pad)
   if (stride == 1) {
     if (V == 8) DW_WG(8, 1); else if (V == 4) DW_WG(4, 1); else if (V == 2) DW_WG(2, 1); else DW_WG(1, 1);
   } else {
@@ -1122,28 +877,5 @@ MDA_API int mda_dw_fwd_bnacc(const void* x, const float* w, void* y, void* regio
   DwParams p{(const bf16_t*)x, w, nullptr, nullptr, nullptr, (bf16_t*)y, nullptr, (int)N, (int)H,
              (int)W, (int)C, (int)Ho, (int)Wo, (int)KH, (int)KW, (int)stride, (int)pad, 0,
              (BnRegion*)region};
-  return launch_fwd(p, st);
-}
-
-// mda_dw_fwd_bnacc with a virtual input (DwParams::in_reg): x is the raw
-// output of a training conv whose BN (region in_reg, affine in_gamma /
-// in_beta, running stats, [4][C] stats out in_stats) + activation in_act this
-// launch applies on load.
-MDA_API int mda_dw_fwd_bnacc_vin(const void* x, const float* w, void* y, void* region, int64_t N,
-                                 int64_t H, int64_t W, int64_t C, int64_t Ho, int64_t Wo,
-                                 int64_t KH, int64_t KW, int64_t stride, int64_t pad, void* in_reg,
-                                 const float* in_gamma, const float* in_beta, float* in_rmean,
-                                 float* in_rvar, float* in_stats, float in_mom, float in_eps,
-                                 int64_t* in_nbt, int64_t in_act, hipStream_t st) {
-  if (KH != KS || KW != KS || stride < 1 || stride > 2 || C > SLOT_CMAX || region == nullptr ||
-      in_reg == nullptr || in_stats == nullptr || C % 8)
-    return (int)hipErrorInvalidValue;
-  DwParams p{(const bf16_t*)x, w, nullptr, nullptr, nullptr, (bf16_t*)y, nullptr, (int)N, (int)H,
-             (int)W, (int)C, (int)Ho, (int)Wo, (int)KH, (int)KW, (int)stride, (int)pad, 0,
-             (BnRegion*)region};
-  p.in_reg = (BnRegion*)in_reg;
-  p.in_gamma = in_gamma; p.in_beta = in_beta;
-  p.in_rmean = in_rmean; p.in_rvar = in_rvar; p.in_stats = in_stats;
-  p.in_mom = in_mom; p.in_eps = in_eps; p.in_nbt = in_nbt; p.in_act = (int)in_act;
   return launch_fwd(p, st);
 }

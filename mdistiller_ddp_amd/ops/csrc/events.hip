@@ -74,37 +74,3 @@ MDA_API int mda_clock_probe(float* out, int64_t slot, hipStream_t st) {
   hipLaunchKernelGGL(clock_probe_kernel, dim3(1), dim3(64), 0, st, out, (int)slot);
   return (int)hipGetLastError();
 }
-
-// A stream restricted to `ncu` compute units (hipExtStreamCreateWithCUMask;
-// ncu <= 0: every CU) with HIP priority `prio` (0 = normal, < 0 higher; only
-// for unmasked streams).  spread != 0 sets every (total / ncu)-th bit of the
-// mask instead of the first ncu, so the CUs come from every XCD / L2.  The
-// teacher stream of the look-ahead uses it to leave the student's critical
-// path CUs of its own (runtime/streams.py).
-MDA_API int mda_stream_create(int64_t ncu, int64_t spread, int64_t prio, void** out) {
-  hipStream_t s = nullptr;
-  hipError_t e;
-  if (ncu > 0) {
-    int dev = 0, total = 0;
-    e = hipGetDevice(&dev);
-    if (e != hipSuccess) return (int)e;
-    e = hipDeviceGetAttribute(&total, hipDeviceAttributeMultiprocessorCount, dev);
-    if (e != hipSuccess) return (int)e;
-    if (ncu > total) ncu = total;
-    const int words = (total + 31) / 32;
-    uint32_t mask[64] = {0};
-    if (words > 64) return (int)hipErrorInvalidValue;
-    for (int64_t i = 0; i < ncu; ++i) {
-      const int64_t b = spread ? (i * total) / ncu : i;
-      mask[b / 32] |= 1u << (b % 32);
-    }
-    e = hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask);
-  } else {
-    e = hipStreamCreateWithPriority(&s, hipStreamNonBlocking, (int)prio);
-  }
-  if (e != hipSuccess) return (int)e;
-  *out = (void*)s;
-  return 0;
-}
-
-MDA_API int mda_stream_destroy(void* s) { return (int)hipStreamDestroy((hipStream_t)s); }

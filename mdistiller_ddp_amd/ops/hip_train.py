@@ -714,17 +714,17 @@ def set_deterministic(on: bool) -> None:
     pool + FC head) whose order varies run to run; here BN runs on per-block
     partial rows and a fixed-order finalize launch instead (the
     ``MDA_BN_FUSED=0`` kernels), and the fusions that exist only on the
-    regions (VirtualBN, BnLink sums, the depthwise fusions) are off.  Everything else is fixed-order in both modes (split-K
+    regions (VirtualBN, BnLink sums) are off.  Everything else is fixed-order in both modes (split-K
     combines, weight-gradient partial reduces, losses, optimizer, VID).
     Turning it off restores the switches as they were."""
     on = bool(on)
     if on == _DET["on"]:
         return
     if on:
-        _DET["saved"] = (_BN_FUSED[0], _BNB_ON[0], _VRES_ON[0], _DW_VIN_ON[0], _DW_BNB_ON[0])
-        _BN_FUSED[0] = _BNB_ON[0] = _VRES_ON[0] = _DW_VIN_ON[0] = _DW_BNB_ON[0] = False
+        _DET["saved"] = (_BN_FUSED[0], _BNB_ON[0], _VRES_ON[0])
+        _BN_FUSED[0] = _BNB_ON[0] = _VRES_ON[0] = False
     else:
-        (_BN_FUSED[0], _BNB_ON[0], _VRES_ON[0], _DW_VIN_ON[0], _DW_BNB_ON[0]) = _DET["saved"]
+        (_BN_FUSED[0], _BNB_ON[0], _VRES_ON[0]) = _DET["saved"]
     _DET["on"] = on
 
 
@@ -943,11 +943,10 @@ class VirtualBN:
     stats as ``vres`` and applies the same affine to the raw residual.
     """
 
-    __slots__ = ("reg", "gamma", "beta", "bn", "stats", "act")
+    __slots__ = ("reg", "gamma", "beta", "bn", "stats")
 
-    def __init__(self, reg, gamma, beta, bn, stats, act=0):
+    def __init__(self, reg, gamma, beta, bn, stats):
         self.reg, self.gamma, self.beta, self.bn, self.stats = reg, gamma, beta, bn, stats
-        self.act = act  # != 0: a virtual INPUT of a depthwise conv (can_defer_to_depthwise)
 
 
 _VRES_ON = [os.environ.get("MDA_VIRTUAL_RES", "1") != "0"]
@@ -1001,33 +1000,6 @@ def _flush_apply_ride() -> None:
 def finish_apply_ride() -> None:
     _RIDE["x"] = None
     _flush_apply_ride()
-
-
-# pw -> dw virtual input / dw dgrad BN-sum epilogue: both OFF by default -- each
-# removes a memory pass but its kernel variant needs more VGPRs (fewer waves)
-# or a capped grid, and the steps measured slower (profiles/r4_dw_fusion_ab.md)
-_DW_VIN_ON = [os.environ.get("MDA_DW_VIN", "0") == "1"]
-_DW_BNB_ON = [os.environ.get("MDA_DW_BNB", "0") == "1"]
-
-
-def set_dw_fusions(vin: bool, bnb: bool) -> None:
-    """Depthwise fusions on / off (A/B): ``vin`` -- a pointwise BN + act applied
-    on load by the consuming depthwise conv (run_seq defers to it); ``bnb`` --
-    the depthwise dgrad adds the producer BN's backward sums (BnLink)."""
-    _DW_VIN_ON[0] = bool(vin)
-    _DW_BNB_ON[0] = bool(bnb)
-
-
-def can_defer_to_depthwise(x, dwconv, dwbn) -> bool:
-    """A pointwise conv + BN + act on input ``x`` may leave its BN apply to
-    its one consumer, the depthwise conv ``dwconv`` + ``dwbn`` (MobileNet
-    pw -> dw): that consumer runs on the native training kernels and applies
-    act(y * scale + shift) on load (csrc/dwconv.hip virtual input), so the
-    activated pointwise output is never written.  The caller guarantees the
-    depthwise conv is the ONLY consumer."""
-    return (_DW_VIN_ON[0] and _VRES_ON[0] and _BN_FUSED[0] and x is not None and x.is_cuda
-            and isinstance(dwconv, nn.Conv2d) and is_depthwise(dwconv) and dwconv.bias is None
-            and dwbn is not None and dwbn.training and train_supported(x, dwconv, dwbn))
 
 
 class _ConvBNActTrain(torch.autograd.Function):
@@ -1126,10 +1098,9 @@ class _ConvBNActTrain(torch.autograd.Function):
             raise RuntimeError("a virtual residual must reach its consumer unchanged (bf16 NHWC)")
         if getattr(x, "_mda_vbn", None) is not None:
             raise RuntimeError("a virtual (un-applied) BN output reached a dense conv")
-        # defer: True -- a projection shortcut (act none) whose apply the block's
-        # residual consumer performs; "dw" -- any act, applied on load by the
-        # consuming depthwise conv (can_defer_to_depthwise)
-        defer = bool(defer) and (_BN_FUSED[0] or gc) and (act == 0 or defer == "dw") \
+        # defer: a projection shortcut (act none) whose apply the block's
+        # residual consumer performs
+        defer = bool(defer) and (_BN_FUSED[0] or gc) and act == 0 \
             and residual is None and not want_preact and G == 1 and cbias is None
         ctx.vbn = None
         out = y if defer else torch.empty_like(y)
@@ -1154,7 +1125,7 @@ class _ConvBNActTrain(torch.autograd.Function):
                           Cout, KH, KW, stride, pad, Kp, tile, splits, G if gc else 1)
             if defer:
                 # no apply: the consumer's apply finalizes this BN (VirtualBN)
-                ctx.vbn = VirtualBN(reg, gamma.detach(), beta.detach(), bn, stats, act)
+                ctx.vbn = VirtualBN(reg, gamma.detach(), beta.detach(), bn, stats)
             elif rv is not None:
                 _ext.call("mda_bn_apply_fin_vr", y, reg, M, Cout, gamma.detach(), beta.detach(),
                           bn.running_mean, bn.running_var, stats, float(bn.momentum),
@@ -1444,16 +1415,9 @@ def _bn_train_backward(ctx, dout, dpre, y, res, stats, gamma, beta, M, C, act):
 
 def _dw_forward(ctx, x, weight, gamma, beta, residual, stride, pad, act, bn, want_preact):
     ctx.kind = "dw"
-    # x is the output of a linked training BN (a pointwise conv's): this
-    # layer's dgrad can produce that BN's backward sums (mda_dw_dgrad_bnsum)
-    ctx.link_in = getattr(x, "_mda_bnlink", None) if (ctx.needs_input_grad[0] and _BNB_ON[0]
-                                                       and _DW_BNB_ON[0]) else None
-    vin = getattr(x, "_mda_vbn", None)
-    xin = x
+    if getattr(x, "_mda_vbn", None) is not None:
+        raise RuntimeError("a virtual (un-applied) BN output reached a depthwise conv")
     x = _cl_bf16(x)
-    if vin is not None and (x is not xin or vin.act == 0 or not _BN_FUSED[0]):
-        raise RuntimeError("a virtual depthwise input must arrive unchanged (bf16 NHWC, fused BN)")
-    ctx.vin = vin
     N, C, H, W = x.shape
     Ho = (H + 2 * pad - 3) // stride + 1
     Wo = (W + 2 * pad - 3) // stride + 1
@@ -1473,15 +1437,7 @@ def _dw_forward(ctx, x, weight, gamma, beta, residual, stride, pad, act, bn, wan
     if _BN_FUSED[0]:
         # the depthwise kernel adds the BN batch sums of its output (no stats pass)
         reg = _region(C, x.device)
-        if vin is not None:
-            # x is the producer's raw conv output: its BN finalize + apply + act
-            # happen inside this launch (the producer never ran an apply pass)
-            vb = vin.bn
-            _ext.call("mda_dw_fwd_bnacc_vin", x, wp, y, reg, N, H, W, C, Ho, Wo, 3, 3, stride, pad,
-                      vin.reg, vin.gamma, vin.beta, vb.running_mean, vb.running_var, vin.stats,
-                      float(vb.momentum), float(vb.eps), vb.num_batches_tracked, vin.act)
-        else:
-            _ext.call("mda_dw_fwd_bnacc", x, wp, y, reg, N, H, W, C, Ho, Wo, 3, 3, stride, pad)
+        _ext.call("mda_dw_fwd_bnacc", x, wp, y, reg, N, H, W, C, Ho, Wo, 3, 3, stride, pad)
     else:
         _ext.call("mda_dw_fwd", x, wp, None, None, None, y, None, N, H, W, C, Ho, Wo, 3, 3,
                   stride, pad, 0)
@@ -1509,20 +1465,10 @@ def _dw_backward(ctx, dout, dpre):
     if ctx.needs_input_grad[0]:
         dx = torch.empty((N, C, H, W), dtype=torch.bfloat16, device=y.device,
                          memory_format=torch.channels_last)
-        link = ctx.link_in
-        if link is not None and link.C == C and link.M == N * H * W:
-            # dx is the whole output gradient of the BN that made x (BnLink)
-            reg = _region(C, y.device)
-            _ext.call("mda_dw_dgrad_bnsum", dy, wp, dx, N, H, W, C, Ho, Wo, 3, 3, stride, pad,
-                      link.y, link.res, link.stats, link.act, reg, link.vres)
-            link.arm(dx, reg)
-        else:
-            _ext.call("mda_dw_dgrad", dy, wp, dx, N, H, W, C, Ho, Wo, 3, 3, stride, pad)
+        _ext.call("mda_dw_dgrad", dy, wp, dx, N, H, W, C, Ho, Wo, 3, 3, stride, pad)
     dw = None
     if ctx.needs_input_grad[1]:
         nblk = _dw_wgrad_blocks(N, H, W, C, Ho, Wo, stride, pad)
-        vin = getattr(ctx, "vin", None)  # virtual input: the activation recomputed on load
-        vst, vact = (vin.stats, vin.act) if vin is not None else (None, 0)
         direct_w = weight.grad is not None and weight.grad.is_contiguous()
         target = weight.grad if direct_w else torch.empty_like(weight, memory_format=torch.contiguous_format)
 
@@ -1531,13 +1477,13 @@ def _dw_backward(ctx, dout, dpre):
             if direct_w and _WG_DEFER[0] is not None:
                 # partials now, their sum in the backward's one multi-layer reduce
                 _ext.call("mda_dw_wgrad", x, dy, part, None, N, H, W, C, Ho, Wo, 3, 3, stride,
-                          pad, nblk, 1, vst, vact)
+                          pad, nblk, 1)
                 _WG_DEFER[0].append([part.data_ptr(), target.data_ptr(), nblk, C, 1, 3, 3, 0, 1,
                                      0, -1])
                 _WG_KEEP.append(part)
                 return
             _ext.call("mda_dw_wgrad", x, dy, part, target, N, H, W, C, Ho, Wo, 3, 3, stride, pad,
-                      nblk, 1 if direct_w else 0, vst, vact)
+                      nblk, 1 if direct_w else 0)
         wg()
         dw = None if direct_w else target
         if direct_w:
@@ -1828,9 +1774,7 @@ def conv_bn_act_train(x, conv, bn, act, residual, want_preact, fork=None, res_fo
     its gradient into this layer's dgrad, or vice versa); ``res_fork``: the
     fork of ``residual`` (identity shortcut).  ``defer_apply``: return the raw
     conv output as a :class:`VirtualBN` (the caller guarantees its one
-    consumer is a native conv + BN that takes it as ``residual``); "dw": the
-    activated output as a virtual input of the one consuming depthwise conv
-    (:func:`can_defer_to_depthwise`)."""
+    consumer is a native conv + BN that takes it as ``residual``)."""
     meta = (conv.stride[0], conv.padding[0], _ACT[act])
     if is_depthwise(conv):
         meta = meta + ("dw",)

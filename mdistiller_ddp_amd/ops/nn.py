@@ -57,7 +57,7 @@ def _bn(x: torch.Tensor, bn: nn.BatchNorm2d) -> torch.Tensor:
 
 def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d | None = None,
                 act: str = "relu", residual: torch.Tensor | None = None,
-                want_preact: bool = False, fork=None, res_fork=None, defer_apply: bool | str = False,
+                want_preact: bool = False, fork=None, res_fork=None, defer_apply: bool = False,
                 private: bool = False):
     """``act(bn(conv(x)) + residual)``; returns ``(out, preact_or_None)``.
 
@@ -67,9 +67,7 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d | None = No
     ``defer_apply`` (a projection shortcut, ``act="none"``): on the native
     training path the BN apply is left to the one consumer, which must be a
     native conv + BN taking the result as ``residual``
-    (:class:`ops.hip_train.VirtualBN`; see :func:`ops.hip_train.can_defer_residual`);
-    ``defer_apply="dw"``: the one consumer is a native depthwise conv that
-    applies this BN + act on load (:func:`ops.hip_train.can_defer_to_depthwise`).
+    (:class:`ops.hip_train.VirtualBN`; see :func:`ops.hip_train.can_defer_residual`).
     ``private``: the output feeds only native convs / native residual consumers
     (no feature loss, no other autograd consumer), so the consuming conv's
     dgrad may finish this BN's backward in its own launch."""
@@ -85,8 +83,7 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d | None = No
         raise RuntimeError("a VirtualBN residual reached a non-native consumer "
                            "(check ops.hip_train.can_defer_residual at the call site)")
     if getattr(x, "_mda_vbn", None) is not None:
-        raise RuntimeError("a virtual depthwise input reached a non-native consumer "
-                           "(check ops.hip_train.can_defer_to_depthwise at the call site)")
+        raise RuntimeError("a virtual (un-applied) BN output reached a non-native consumer")
     if hip_enabled_for(x):
         from . import hip_train
         if _TRAIN_KERNELS["on"] and bn is None and hip_train.conv_train_supported(x, conv):

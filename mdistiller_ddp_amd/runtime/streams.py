@@ -88,37 +88,14 @@ def _fresh_stream(idx, avoid=(), priority: int = 0) -> "torch.cuda.Stream":
     return s
 
 
-# Teacher-stream placement (A/B knobs, profiles/r6_overlap.md): restrict the
-# teacher's queue to a CU subset (MDA_TEACHER_CUS = n CUs, spread over the
-# XCDs unless MDA_TEACHER_CU_SPREAD=0) or give it a HIP stream priority.
-_TEACHER_CUS = [int(os.environ.get("MDA_TEACHER_CUS", "0"))]
-_TEACHER_SPREAD = [os.environ.get("MDA_TEACHER_CU_SPREAD", "1") != "0"]
-_TEACHER_PRIO = [int(os.environ.get("MDA_TEACHER_PRIO", "0"))]
-_RAW_STREAMS: list = []  # handles of streams created natively (kept for the process)
-
-
-def native_stream(device, ncu: int = 0, spread: bool = True, prio: int = 0):
-    """A HIP stream made by ``mda_stream_create`` (CU-masked when ``ncu`` > 0,
-    else with priority ``prio``), wrapped as a torch ExternalStream."""
-    import ctypes
-    from ..ops import _ext
-    idx = torch.device(device).index or 0
-    h = ctypes.c_void_p(0)
-    with torch.cuda.device(idx):
-        _ext.call("mda_stream_create", int(ncu), int(bool(spread)), int(prio), h)
-    _RAW_STREAMS.append(h.value)
-    return torch.cuda.ExternalStream(h.value, device=torch.device("cuda", idx))
-
-
 def side_stream(device) -> "torch.cuda.Stream":
     idx = torch.device(device).index or 0
     with _lock:
         s = _streams.get(idx)
         if s is None:
-            if _TEACHER_CUS[0] > 0 or _TEACHER_PRIO[0] != 0:
-                s = native_stream(idx, _TEACHER_CUS[0], _TEACHER_SPREAD[0], _TEACHER_PRIO[0])
-            else:
-                s = _fresh_stream(idx, (_branch_streams.get(idx),))
+            # (a CU-masked or prioritised teacher queue was measured slower or
+            # no better, profiles/r6_ab.md "Teacher placement")
+            s = _fresh_stream(idx, (_branch_streams.get(idx),))
             _streams[idx] = s
         return s
 
@@ -388,6 +365,10 @@ _branch_streams: dict = {}
 
 def set_branches(flag: bool) -> None:
     _branch["enabled"] = bool(flag)
+
+
+def branches_enabled() -> bool:
+    return _branch["enabled"]
 
 
 def branch_stream(device) -> "torch.cuda.Stream":

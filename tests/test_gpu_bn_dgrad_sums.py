@@ -204,17 +204,13 @@ def test_depthwise_to_pointwise(C, H, stride):
             assert _rel(p.grad, q.grad) < 1e-2
 
 
-@pytest.mark.parametrize("defer", [False, "dw"])
 @pytest.mark.parametrize("C,H,stride,act", [(64, 32, 1, "relu"), (128, 16, 2, "relu"),
                                              (512, 8, 1, "relu"), (96, 14, 1, "relu6")])
-def test_pointwise_to_depthwise(C, H, stride, act, defer):
+def test_pointwise_to_depthwise(C, H, stride, act):
     """MobileNet pair the other way round: pointwise conv + BN + act feeding a
-    depthwise conv; the pointwise layer's BN sums come from the depthwise
-    dgrad epilogue (csrc/dwconv.hip mda_dw_dgrad_bnsum).  defer="dw": the
-    pointwise BN + act is never applied in a pass of its own -- the depthwise
-    forward and weight gradient apply it on load (virtual input).  Against
-    the unlinked, undeferred path (bit-identical forward) and an fp32
-    PyTorch reference (running statistics included)."""
+    depthwise conv (the depthwise dgrad takes no BnLink: the pointwise BN runs
+    its own backward).  Against an fp32 PyTorch reference, running statistics
+    included."""
     torch.manual_seed(6)
     pw = nn.Conv2d(C // 2, C, 1, bias=False).cuda()
     b1 = nn.BatchNorm2d(C).cuda()
@@ -224,34 +220,14 @@ def test_pointwise_to_depthwise(C, H, stride, act, defer):
         for b in (b1, b2):
             b.weight.uniform_(0.5, 1.5)
             b.bias.uniform_(-0.5, 0.5)
-    mods = [(pw, b1), (dw, b2)]
-    mods_off = copy.deepcopy(mods)
-    mods_ref = copy.deepcopy(mods)
+    mods_ref = copy.deepcopy([(pw, b1), (dw, b2)])
     x = torch.randn(64, C // 2, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     Ho = (H + 2 - 3) // stride + 1
     g = torch.randn(64, C, Ho, Ho, device="cuda").to(torch.bfloat16).float()
-
-    def chain(layers, dfr=False):
-        (c1, bb1), (c2, bb2) = layers
-        xx = x.clone().requires_grad_(True)
-        h, _ = hip_train.conv_bn_act_train(xx, c1, bb1, act, None, False, defer_apply=dfr)
-        assert (getattr(h, "_mda_vbn", None) is not None) == bool(dfr)
-        out, _ = hip_train.conv_bn_act_train(h, c2, bb2, act, None, False)
-        (out.float() * g).sum().backward()
-        return out, xx.grad
-
-    hip_train.bn_dgrad_sums_count(reset=True)
-    hip_train.set_dw_fusions(True, True)
-    try:
-        out, dx = chain(mods, defer)
-    finally:
-        hip_train.set_dw_fusions(False, False)
-    assert hip_train.bn_dgrad_sums_count(reset=True) == (1, 0)
-    hip_train.set_bn_dgrad_sums(False)
-    try:
-        out_off, dx_off = chain(mods_off)
-    finally:
-        hip_train.set_bn_dgrad_sums(True)
+    xx = x.clone().requires_grad_(True)
+    h, _ = hip_train.conv_bn_act_train(xx, pw, b1, act, None, False)
+    out, _ = hip_train.conv_bn_act_train(h, dw, b2, act, None, False)
+    (out.float() * g).sum().backward()
     (r1, rb1), (r2, rb2) = mods_ref
     fa = F.relu if act == "relu" else F.relu6
     x2 = x.float().clone().requires_grad_(True)
@@ -259,13 +235,8 @@ def test_pointwise_to_depthwise(C, H, stride, act, defer):
     o.backward(g)
     torch.cuda.synchronize()
     assert hip_train.slot_errors() == 0
-    torch.testing.assert_close(out, out_off, atol=0, rtol=0)
-    assert _rel(dx, dx_off) < 1e-2
-    for m, mo in zip(mods, mods_off):
-        for p, q in zip(list(m[0].parameters()) + list(m[1].parameters()),
-                        list(mo[0].parameters()) + list(mo[1].parameters())):
-            assert _rel(p.grad, q.grad) < 1e-2
-    assert _rel(dx, x2.grad) < 1e-1
+    assert _rel(out.float(), o) < 2e-2
+    assert _rel(xx.grad, x2.grad) < 1e-1
     for a, b in zip([pw.weight, b1.weight, b1.bias, dw.weight, b2.weight, b2.bias],
                     [r1.weight, rb1.weight, rb1.bias, r2.weight, rb2.weight, rb2.bias]):
         assert _rel(a.grad, b.grad) < 1e-1

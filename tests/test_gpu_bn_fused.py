@@ -198,6 +198,7 @@ def test_residual_block_grad_fork(inplanes, planes, stride, branch):
 
     def run(m, forks):
         mda_nn.set_grad_forks(forks)
+        prev = streams.branches_enabled()
         streams.set_branches(branch)
         try:
             xx = x.clone().requires_grad_(True)
@@ -207,7 +208,7 @@ def test_residual_block_grad_fork(inplanes, planes, stride, branch):
             torch.cuda.current_stream().wait_stream(streams.branch_stream(x.device))
         finally:
             mda_nn.set_grad_forks(True)
-            streams.set_branches(True)
+            streams.set_branches(prev)
         return out, xx.grad
 
     out, dx = run(blk, True)

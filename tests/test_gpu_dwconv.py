@@ -122,6 +122,6 @@ def test_dw_dgrad_wgrad_exact_inputs(shape):
     nblk = hip_train._dw_wgrad_blocks(N, H, H, C, Ho, Ho, s)
     part = torch.empty(nblk * 9 * C, device="cuda")
     dw = torch.full_like(w, 1.0)
-    _ext.call("mda_dw_wgrad", x, dy, part, dw, N, H, H, C, Ho, Ho, 3, 3, s, 1, nblk, 1, None, 0)
+    _ext.call("mda_dw_wgrad", x, dy, part, dw, N, H, H, C, Ho, Ho, 3, 3, s, 1, nblk, 1)
     assert _rel(dx, xr.grad) < 1e-2
     assert _rel(dw - 1.0, wr.grad) < 1e-3

@@ -75,20 +75,3 @@ def test_vit_tiny_forward():
         logits, f = m(torch.randn(1, 3, 224, 224))
     assert logits.shape == (1, 1000)
     assert m.get_arch() == "transformer"
-
-
-def test_run_seq_depthwise_deferral_is_gpu_only():
-    """run_seq's pointwise -> depthwise deferral (next_seq / in-sequence) never
-    engages off the native GPU path: on the CPU the outputs equal the plain
-    walk of the same modules."""
-    import torch.nn as nn
-    from mdistiller_ddp_amd.models._seq import run_seq, _defer_to
-    torch.manual_seed(0)
-    a = nn.Sequential(nn.Conv2d(8, 16, 1, bias=False), nn.BatchNorm2d(16), nn.ReLU())
-    b = nn.Sequential(nn.Conv2d(16, 16, 3, 1, 1, groups=16, bias=False), nn.BatchNorm2d(16), nn.ReLU())
-    x = torch.randn(2, 8, 6, 6)
-    assert _defer_to(x, list(b), 0) is False
-    h1 = run_seq(a, x, next_seq=b)[0]
-    h2 = run_seq(a, x)[0]
-    torch.testing.assert_close(h1, h2)
-    assert getattr(h1, "_mda_vbn", None) is None

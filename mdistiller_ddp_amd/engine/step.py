@@ -255,6 +255,14 @@ class TrainStep:
         # runtime/streams.py::TeacherFeed.capture_pipe) instead of a branch of
         # the step graph
         self.teacher_split = str(cfg.RUNTIME.get("TEACHER_GRAPH", "split")).lower() == "split"
+        if getattr(distiller, "_teacher_train_bn", False):
+            # a train-mode teacher (OFD.TEACHER_TRAIN_BN) keeps its look-ahead a
+            # branch of the step graph: as a graph of its own, the SECOND replay
+            # of the step graph finds garbage BN sums in a connector BN
+            # (running_var inf / NaN losses, scripts/debug/ofd_lookahead_nan.py;
+            # only with the fused BN regions, teacher graph replayed or not);
+            # cause not found
+            self.teacher_split = False
         self.teacher_first = bool(cfg.RUNTIME.get("TEACHER_FIRST", True))
         self._tsplit = None     # (graph, T list, X list, stream, teacher-done event, copy-done event)
         self._tp_inflight = False
@@ -625,15 +633,6 @@ class TrainStep:
         both sides already fill the GPU and it costs 6 %: ``auto`` skips that case."""
         if self.lookahead != "auto":
             return bool(self.lookahead)
-        if getattr(self.distiller, "_teacher_train_bn", False):
-            # a train-mode teacher (OFD.TEACHER_TRAIN_BN) runs inline under
-            # auto.  With every step handed its next batch the look-ahead is
-            # exact for it (tests/test_gpu_e2e.py look-ahead test, OFD case;
-            # the round-5 arena race is fixed), but a caller that passes no
-            # next batch takes the priming-graph / recapture fallback, which
-            # still gives non-finite losses with a train-mode teacher
-            # (test_distiller_graph_steps[OFD]); cause not found in round 6
-            return False
         img = static.get("image")
         big = img is not None and img.dim() == 4 and min(img.shape[-2:]) >= 128
         needs = tuple(getattr(self.distiller, "teacher_needs", ("logits",)))

@@ -250,7 +250,7 @@ def test_native_bf16_tracks_fp32_over_300_steps(typ, student):
 
 
 @pytest.mark.parametrize("typ,trainer,tgraph", [("DKD", "base", "split"), ("DKD", "base", "fork"),
-                                                 ("FITNET", "base", "split"), ("OFD", "base", "split"),
+                                                 ("FITNET", "base", "split"), ("OFD", "base", "fork"),
                                                  ("REVIEWKD", "base", "split"), ("KD", "dot", "split")])
 def test_teacher_lookahead_matches_inline_teacher(typ, trainer, tgraph):
     """The captured step with the teacher look-ahead (teacher of batch t+1 beside

@@ -79,10 +79,6 @@ def run(cfg_file: str, per_gpu_batch: int, steps: int, warmup: int, opts=(), use
         torch.cuda.empty_cache()
     info = D.init_distributed() if not D.is_dist() else D.info()
     dev = info.device
-    # diagnostics: shift the position of the framework's streams in the stream
-    # pool (their hardware-queue assignment) by allocating k pool streams first
-    for _ in range(int(os.environ.get("MDA_DEBUG_SKIP_STREAMS", "0"))):
-        torch.cuda.Stream(device=dev)
     if dev.type == "cuda":
         torch.backends.cudnn.benchmark = True
     cfg = get_cfg()

@@ -526,8 +526,6 @@ class TrainStep:
         if self.world <= 1:
             return
         if replay and self.graph_comm == "events" and self.reducer.graph_events is not None:
-            if os.environ.get("MDA_EVENTS_SYNC") == "1":  # diagnostic: the replay drained first
-                torch.cuda.current_stream().synchronize()
             self.reducer.launch_from_events()
             self.reducer.wait_launched()
         elif self.is_dot:

@@ -1626,18 +1626,6 @@ bool halo_eligible(ConvParams& p) {
   return halo_geometry(p, p.Cin == BK ? HALO1_PROWS : HALO_PROWS);
 }
 
-// Halving the channel tile of an 8 x 8 halo conv that has fewer blocks than
-// CUs: off by default since round 6 -- beside the look-ahead teacher the
-// extra blocks cost more than the idle CUs they fill (flagship 0.820 ->
-// 0.810 ms/step without it, profiles/r6_ab.md).  MDA_HALO_NARROW=1: on.
-bool halo_narrow() {
-  static const bool on = [] {
-    const char* e = getenv("MDA_HALO_NARROW");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
 bool use_halo1() {
   static const bool on = [] {
     const char* e = getenv("MDA_CONV_HALO1");
@@ -1861,12 +1849,10 @@ int dispatch(ConvParams& p, int mode, int64_t tile, int64_t splits, hipStream_t 
   if (halo) {  // halo kernel: split over 64-channel chunks, hpb pixels per block
     const int nchunks = p.Cin / BK;
     p.steps_per_split = (int)((nchunks + splits - 1) / splits);
-    int bn = p.Cout <= 32 ? 32 : 64;
-    // fewer blocks than CUs (8x8 maps: 128-pixel blocks of two images): halve
-    // the channel tile rather than leave half the CUs idle
-    if (bn == 64 && (int64_t)((p.M + p.hpb - 1) / p.hpb) * ((p.Cout + 63) / 64) * splits < 256 &&
-        halo_narrow())
-      bn = 32;
+    // (halving the channel tile of 8x8 convs with fewer blocks than CUs helped
+    // the student alone but not beside the look-ahead teacher: deleted in
+    // round 6, profiles/r6_ab.md)
+    const int bn = p.Cout <= 32 ? 32 : 64;
     dim3 grid((p.M + p.hpb - 1) / p.hpb, (p.Cout + bn - 1) / bn, (int)splits);
     if (nchunks == 1 && splits == 1 && use_halo1()) {
       if (bn == 32) {

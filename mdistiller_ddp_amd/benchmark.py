@@ -130,7 +130,7 @@ def run(cfg_file: str, per_gpu_batch: int, steps: int, warmup: int, opts=(), use
     # The collection runs BEFORE the last warm-up step, not between it and the
     # timed loop: a ~50 ms gc.collect() there left the host caches cold and the
     # GPU idle, and the first timed steps paid for it -- +30 us/step on a 20-step
-    # window, 0.875 vs 0.845 ms (profiles/r6_short_run_gap.md)
+    # window, 0.875 vs 0.845 ms (profiles/r6_ab.md)
     gc_frozen = os.environ.get("MDA_GC_FREEZE", "1") != "0"
     for i in range(warmup):
         if gc_frozen and i == warmup - 1:

@@ -337,9 +337,9 @@ class TrainStep:
     # module types whose whole backward runs on the native kernels that carry
     # two stacked cotangents (ops/hip_train.py _Dual): the CIFAR ResNets
     # (Bottleneck ResNets are left out: no test covers their dual backward)
-    _DOT_SINGLE_MODULES = frozenset({"ResNet", "BasicBlock", "Conv2d", "BatchNorm2d",
+    _DOT_SINGLE_MODULES = frozenset({"ResNet", "BasicBlock", "VGG", "Conv2d", "BatchNorm2d",
                                      "Linear", "ReLU", "Sequential", "ModuleList", "Identity", "Stage",
-                                     "AdaptiveAvgPool2d", "AvgPool2d"})
+                                     "AdaptiveAvgPool2d", "AvgPool2d", "MaxPool2d"})
 
     def _dot_single_ok(self, cfg) -> bool:
         """``RUNTIME.DOT_SINGLE_PASS`` (auto | True | False): DOT's KD and task
@@ -359,12 +359,15 @@ class TrainStep:
         from ..ops import hip_train
         if not (hip_enabled_for(self.flat.data) and hip_train._BN_FUSED[0]):
             return False
+        from ..ops.nn import MaxPool2d as NativeMaxPool
         for m in student.modules():
             name = type(m).__name__
             if name not in self._DOT_SINGLE_MODULES:
                 return False
-            if name == "Conv2d" and (m.groups != 1 or m.bias is not None):
+            if name == "Conv2d" and m.groups != 1:
                 return False
+            if name == "MaxPool2d" and not isinstance(m, NativeMaxPool):
+                return False  # torch's max pool: its backward cannot carry two sets
         return True
 
     def _dot_single_backward(self, losses):

@@ -8,7 +8,7 @@ from __future__ import annotations
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ...ops.nn import conv_bn_act
+from ...ops.nn import conv_bn_act, pool_linear
 from .._base import ModelBase, PreactStage
 from .resnet import Stage
 
@@ -139,8 +139,7 @@ class ResNet(nn.Module, ModelBase):
         f3 = out
         out, f4_pre = self.layer4(out)
         f4 = out
-        avg = self.avgpool(out).reshape(out.size(0), -1)
-        logits = self.linear(avg)
+        avg, logits = pool_linear(out, self.linear)  # fused pool + classifier
         return logits, {
             "feats": [f0, f1, f2, f3, f4],
             "preact_feats": [f0_pre, f1_pre, f2_pre, f3_pre, f4_pre],

@@ -12,7 +12,7 @@ import math
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ...ops.nn import MaxPool2d
+from ...ops.nn import MaxPool2d, pool_linear
 from .._base import ModelBase
 from .._seq import run_seq
 
@@ -62,20 +62,24 @@ class VGG(nn.Module, ModelBase):
         return self.classifier
 
     def forward(self, x):
-        x, f0_pre = run_seq(self.block0, x, want_preact=True)
-        x = F.relu(x)
+        # each block's last conv applies the ReLU in its own launch and also
+        # returns the pre-activation (the stage feature), so no separate ReLU
+        # pass runs and the backward stays on the native kernels end to end
+        # (DOT's single-pass backward, engine/step.py); the head is the fused
+        # pool + classifier (reference models/cifar/vgg.py forward: the same
+        # values through F.relu, AdaptiveAvgPool2d and Linear)
+        x, f0_pre = run_seq(self.block0, x, want_preact=True, final_act="relu")
         f0 = x
         feats, pres = [f0], [f0_pre]
         for i, (pool, block) in enumerate(((self.pool0, self.block1), (self.pool1, self.block2),
                                             (self.pool2, self.block3), (self.pool3, self.block4))):
             if i < 3 or x.shape[-1] > 4:
                 x = pool(x)
-            x, _ = run_seq(block, x)
-            pres.append(x)
-            x = F.relu(x)
+            x, pre = run_seq(block, x, want_preact=True, final_act="relu")
+            pres.append(pre)
             feats.append(x)
-        avg = self.pool4(x).reshape(x.size(0), -1)
-        return self.classifier(avg), {"feats": feats, "preact_feats": pres, "pooled_feat": avg}
+        avg, logits = pool_linear(x, self.classifier)
+        return logits, {"feats": feats, "preact_feats": pres, "pooled_feat": avg}
 
     @staticmethod
     def _make_layers(cfg, batch_norm=False, in_channels=3):

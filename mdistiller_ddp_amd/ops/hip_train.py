@@ -1317,9 +1317,13 @@ def _conv_bn_backward_dual(ctx, dout, dpre):
     """:meth:`_ConvBNActTrain.backward` over two stacked cotangents (see
     :class:`_Dual`): the BN backward, dgrad (2N images, BN-sum epilogue with
     one region per set) and both weight gradients."""
-    if ctx.kind == "dw" or ctx.gc or ctx.groups != 1 or ctx.cbias:
-        raise RuntimeError("DOT single-pass backward: depthwise / grouped convs and conv biases "
-                           "are not supported; set RUNTIME.DOT_SINGLE_PASS=False")
+    if ctx.kind == "dw" or ctx.gc or ctx.groups != 1:
+        raise RuntimeError("DOT single-pass backward: depthwise / grouped convs are not "
+                           "supported; set RUNTIME.DOT_SINGLE_PASS=False")
+    if ctx.cbias and (ctx.cbias_t.grad is None or not ctx.needs_input_grad[9]):
+        # a conv bias in front of a training BN has an exactly zero gradient: both
+        # sets keep their zeroed slots of the flat buffer (_cbias_grad)
+        raise RuntimeError("DOT single-pass backward: a conv bias needs a bound flat gradient")
     if dout is None:
         raise RuntimeError("DOT single-pass backward: a layer output without a gradient")
     x, wt, weight, gamma, beta, y, res, stats = ctx.saved_tensors
@@ -1372,7 +1376,7 @@ def _conv_bn_backward_dual(ctx, dout, dpre):
         wg()
         notify_grad(weight)
     notify_grad(gamma, beta)
-    return dx, None, None, None, dres, None, None, None, None, None, None, None
+    return dx, None, None, None, dres, None, None, None, None, _cbias_grad(ctx), None, None
 
 
 def _bn_train_forward(y, M, C, gamma, beta, bn, residual, act, want_preact, reg=None):

@@ -536,12 +536,33 @@ class _MaxPoolNHWC(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         from . import _ext
+        from .hip_train import _DUAL
         idx, = ctx.saved_tensors
         N, C, H, W, Ho, Wo, k, s, p = ctx.meta
+        if _DUAL[0] is not None:
+            return _MaxPoolNHWC._backward_dual(ctx, dy)
         dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         dx = torch.empty((N, C, H, W), dtype=torch.bfloat16, device=dy.device,
                          memory_format=torch.channels_last)
         _ext.call("mda_maxpool_bwd", dy, idx, dx, N, H, W, C, Ho, Wo, k, s, p)
+        return dx, None, None, None
+
+    @staticmethod
+    def _backward_dual(ctx, dy):
+        """DOT single-pass backward (ops.hip_train._Dual): the gather once per
+        gradient set (the forward's argmax offsets serve both) into the two
+        halves of one stacked dx."""
+        from . import _ext
+        from .hip_train import dual_full, dual_alloc
+        idx, = ctx.saved_tensors
+        N, C, H, W, Ho, Wo, k, s, p = ctx.meta
+        if dy.dtype != torch.bfloat16 or not dy.is_contiguous(memory_format=torch.channels_last):
+            raise RuntimeError("DOT single-pass backward: max-pool gradient not bf16 channels_last")
+        dfull = dual_full(dy)
+        full, dx = dual_alloc((N, C, H, W), torch.bfloat16, dy.device)
+        for i in (0, 1):
+            _ext.call("mda_maxpool_bwd", dfull[i * N:(i + 1) * N], idx, full[i * N:(i + 1) * N],
+                      N, H, W, C, Ho, Wo, k, s, p)
         return dx, None, None, None
 
 

@@ -15,10 +15,11 @@ from mdistiller_ddp_amd.data.synthetic import SyntheticLoader
 pytestmark = pytest.mark.gpu
 
 
-def _cfg(student, single):
+def _cfg(student, single, teacher="resnet32x4", data="cifar100"):
     cfg = get_cfg()
+    cfg.DATASET.TYPE = data
     cfg.DISTILLER.TYPE = "KD"
-    cfg.DISTILLER.TEACHER = "resnet32x4"
+    cfg.DISTILLER.TEACHER = teacher
     cfg.DISTILLER.STUDENT = student
     cfg.DISTILLER.RANDOM_TEACHER = True
     cfg.SOLVER.TRAINER = "dot"
@@ -30,17 +31,28 @@ def _rel(a, b):
     return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
 
 
-@pytest.mark.parametrize("student", ["resnet8x4", "resnet20", "resnet32x4"])
+# vgg8: biased convs (zero gradient in front of a training BN), native max pools,
+# ReLU inside the conv launch (models/cifar/vgg.py); ResNet18: the ImageNet stem's
+# 7x7 conv and 3x3 / stride-2 max pool (configs/imagenet/r34_r18/dot.yaml)
+_STUDENTS = {"resnet8x4": ("resnet32x4", "cifar100", 100, 64),
+             "resnet20": ("resnet32x4", "cifar100", 100, 64),
+             "resnet32x4": ("resnet32x4", "cifar100", 100, 64),
+             "vgg8": ("vgg13", "cifar100", 100, 64),
+             "ResNet18": ("ResNet34", "imagenet", 1000, 16)}
+
+
+@pytest.mark.parametrize("student", list(_STUDENTS))
 def test_single_pass_gradients_match_two_passes(student):
+    teacher, data, ncls, bs = _STUDENTS[student]
     torch.manual_seed(0)
-    d1 = build_distiller(_cfg(student, True), 100, "cuda")
+    d1 = build_distiller(_cfg(student, True, teacher, data), ncls, "cuda")
     d2 = copy.deepcopy(d1)
-    ld = SyntheticLoader("cifar100", 64, "cuda", steps_per_epoch=1, channels_last=True)
+    ld = SyntheticLoader(data, bs, "cuda", steps_per_epoch=1, channels_last=True)
     batch = next(iter(ld))
     grads = []
     for d, single in ((d1, True), (d2, False)):
         d.train()
-        st = TrainStep(d, _cfg(student, single), "cuda", trainer="dot", use_graph=False,
+        st = TrainStep(d, _cfg(student, single, teacher, data), "cuda", trainer="dot", use_graph=False,
                        dtype=torch.bfloat16)
         assert st.dot_single == single
         st.set_epoch(1.0)

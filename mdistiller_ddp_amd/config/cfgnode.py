@@ -190,6 +190,9 @@ def _check_and_coerce_cfg_value_type(replacement, original, key, full_key):
             return to_type(replacement)
     if original_type is float and replacement_type is int:
         return float(replacement)
+    if original_type is str and replacement_type is bool:
+        # a mode key (``"auto"`` default) set from the command line as True / False
+        return "true" if replacement else "false"
     raise ValueError(
         f"Type mismatch ({original_type} vs. {replacement_type}) with values "
         f"({original} vs. {replacement}) for config key: {full_key}")

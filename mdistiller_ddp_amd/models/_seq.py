@@ -21,10 +21,13 @@ def _act_of(m):
     return None
 
 
-def run_seq(seq, x, residual=None, want_preact=False, final_act=None):
+def run_seq(seq, x, residual=None, want_preact=False, final_act=None, fork=None):
     """Returns ``(out, preact_of_last_group_or_None)``.
 
     ``residual`` is added after the last group's BN, before its activation.
+    ``fork`` (:func:`ops.nn.grad_fork` of ``x`` when ``residual`` is ``x``):
+    the first conv and the residual add sum their input gradients inside the
+    native backward instead of by an autograd add.
     ``final_act`` overrides the last group's activation (e.g. "relu" on a
     linear-bottleneck output whose consumer applies ReLU: one fused launch
     returns both the activated tensor and, with ``want_preact``, the linear
@@ -44,7 +47,9 @@ def run_seq(seq, x, residual=None, want_preact=False, final_act=None):
             last = j >= n
             if last and final_act is not None:
                 act = final_act
-            x, pre = conv_bn_act(x, m, bn, act, residual if last else None, want_preact and last)
+            x, pre = conv_bn_act(x, m, bn, act, residual if last else None, want_preact and last,
+                                 fork=fork if i == 0 else None,
+                                 res_fork=fork if (last and residual is not None) else None)
             i = j
         elif isinstance(m, nn.BatchNorm2d):
             act, j = "none", i + 1

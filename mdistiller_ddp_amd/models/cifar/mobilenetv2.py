@@ -25,6 +25,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ...ops.nn import grad_fork, pool_linear
 from .._base import ModelBase
 from .._seq import run_seq
 
@@ -82,9 +83,13 @@ class InvertedResidual(nn.Module):
         """``final_act``: also apply this activation to the block output and
         return ``(activated, linear)`` from the same fused launch."""
         res = x if self.use_res_connect else None
+        # x feeds the expansion conv and the residual add: their input
+        # gradients are summed in the native backward (GradFork)
+        fork = grad_fork(x) if res is not None else None
         if final_act is None:
-            return run_seq(self.conv, x, residual=res)[0]
-        return run_seq(self.conv, x, residual=res, want_preact=True, final_act=final_act)
+            return run_seq(self.conv, x, residual=res, fork=fork)[0]
+        return run_seq(self.conv, x, residual=res, want_preact=True, final_act=final_act,
+                       fork=fork)
 
 
 class _Group(nn.Module):
@@ -240,10 +245,16 @@ class MobileNetV2(nn.Module, ModelBase):
         out = self.blocks[5](a3)
         a4, f4 = self._stage(self.blocks[6], out)
         out = run_seq(self.conv2, a4)[0]
-        if not self.remove_avg:
-            out = self.avgpool(out)
-        avg = out.reshape(out.size(0), -1)
-        logits = self.classifier(avg)
+        if not self.remove_avg and out.shape[-1] == out.shape[-2] == self._pool_k:
+            # a global pool: the fused pool + classifier (same values as
+            # AvgPool2d + Linear, native backward)
+            avg, logits = pool_linear(out, self.classifier[0], self._pool_k)
+        else:
+            if not self.remove_avg:
+                out = self.avgpool(out)
+            avg = out.reshape(out.size(0), -1)
+            logits = self.classifier(avg)
+
         def real(ts):
             return [t if t.shape[1] == c else t[:, :c] for t, c in zip(ts, self._feat_c)]
         return logits, {

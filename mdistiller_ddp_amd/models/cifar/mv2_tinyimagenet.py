@@ -10,6 +10,7 @@ from __future__ import annotations
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ...ops.nn import grad_fork, pool_linear
 from .._base import ModelBase
 from .._seq import run_seq
 
@@ -27,9 +28,27 @@ class LinearBottleNeck(nn.Module):
         )
         self.stride, self.in_channels, self.out_channels = stride, in_channels, out_channels
 
-    def forward(self, x):
+    def forward(self, x, final_act=None):
+        """``final_act``: also apply this activation to the block output and
+        return ``(activated, linear)`` from the same fused launch."""
         res = x if (self.stride == 1 and self.in_channels == self.out_channels) else None
-        return run_seq(self.residual, x, residual=res)[0]
+        # x feeds the expansion conv and the residual add: their input
+        # gradients are summed in the native backward (GradFork)
+        fork = grad_fork(x) if res is not None else None
+        if final_act is None:
+            return run_seq(self.residual, x, residual=res, fork=fork)[0]
+        return run_seq(self.residual, x, residual=res, want_preact=True, final_act=final_act,
+                       fork=fork)
+
+
+def _stage_act(stage, x):
+    """A stage whose output feeds a ReLU6: its last block returns
+    (relu6(out), out) from one fused launch."""
+    if isinstance(stage, LinearBottleNeck):
+        return stage(x, final_act="relu6")
+    for blk in list(stage)[:-1]:
+        x = blk(x)
+    return stage[-1](x, final_act="relu6")
 
 
 class _Chain(nn.Module):
@@ -80,21 +99,24 @@ class MobileNetV2(nn.Module, ModelBase):
                 self.stage4[-1].residual[-1], self.conv1[1]]
 
     def forward(self, x):
-        f0 = run_seq(self.pre, x)[0]
-        x = self.stage1(F.relu6(f0))
-        f1 = self.stage2(x)
-        f2 = self.stage3(F.relu6(f1))
-        f3 = self.stage4(F.relu6(f2))
-        x = self.stage5(F.relu6(f3))
+        # the reference applies F.relu6 to f0..f3 before their consumers; here
+        # each producer emits both tensors from one fused launch, f4 is already
+        # ReLU6'd (conv1), and the head is the fused pool + 1x1 classifier --
+        # no PyTorch op touches an activation gradient (DOT's single pass)
+        a0, f0 = run_seq(self.pre, x, want_preact=True, final_act="relu6")
+        x = self.stage1(a0)
+        a1, f1 = _stage_act(self.stage2, x)
+        a2, f2 = _stage_act(self.stage3, a1)
+        a3, f3 = _stage_act(self.stage4, a2)
+        x = self.stage5(a3)
         x = self.stage6(x)
         x = self.stage7(x)
         f4 = run_seq(self.conv1, x)[0]
-        avg = F.adaptive_avg_pool2d(f4, 1)
-        logits = self.conv2(avg).flatten(1)
+        avg, logits = pool_linear(f4, self.conv2)
         return logits, {
-            "feats": [F.relu6(f0), F.relu6(f1), F.relu6(f2), F.relu6(f3), F.relu6(f4)],
+            "feats": [a0, a1, a2, a3, f4],
             "preact_feats": [f0, f1, f2, f3, f4],
-            "pooled_feat": avg.flatten(1),
+            "pooled_feat": avg,
         }
 
     def _make_stage(self, repeat, in_channels, out_channels, stride, t):

@@ -1317,9 +1317,11 @@ def _conv_bn_backward_dual(ctx, dout, dpre):
     """:meth:`_ConvBNActTrain.backward` over two stacked cotangents (see
     :class:`_Dual`): the BN backward, dgrad (2N images, BN-sum epilogue with
     one region per set) and both weight gradients."""
-    if ctx.kind == "dw" or ctx.gc or ctx.groups != 1:
-        raise RuntimeError("DOT single-pass backward: depthwise / grouped convs are not "
-                           "supported; set RUNTIME.DOT_SINGLE_PASS=False")
+    if ctx.kind == "dw":
+        return _dw_backward_dual(ctx, dout, dpre)
+    if ctx.gc or ctx.groups != 1:
+        raise RuntimeError("DOT single-pass backward: grouped convs are not supported; set "
+                           "RUNTIME.DOT_SINGLE_PASS=False")
     if ctx.cbias and (ctx.cbias_t.grad is None or not ctx.needs_input_grad[9]):
         # a conv bias in front of a training BN has an exactly zero gradient: both
         # sets keep their zeroed slots of the flat buffer (_cbias_grad)
@@ -1493,6 +1495,50 @@ def _dw_backward(ctx, dout, dpre):
         if direct_w:
             notify_grad(weight)
     return dx, dw, dgamma, dbeta, dres, None, None, None, None, _cbias_grad(ctx), None, None
+
+
+def _dw_backward_dual(ctx, dout, dpre):
+    """:func:`_dw_backward` over two stacked cotangents (see :class:`_Dual`):
+    both sets' BN backward in one launch, the depthwise dgrad over 2N images,
+    and one weight-gradient partial launch per set (x read by both) into the
+    two sets of the flat gradient."""
+    if ctx.cbias and (ctx.cbias_t.grad is None or not ctx.needs_input_grad[9]):
+        raise RuntimeError("DOT single-pass backward: a conv bias needs a bound flat gradient")
+    if dout is None:
+        raise RuntimeError("DOT single-pass backward: a layer output without a gradient")
+    x, wp, weight, gamma, beta, y, res, stats = ctx.saved_tensors
+    N, C, H, W, Ho, Wo, stride, pad, act = ctx.meta
+    M = N * Ho * Wo
+    dev = y.device
+    if dout.dtype != torch.bfloat16 or not dout.is_contiguous(memory_format=torch.channels_last):
+        raise RuntimeError("DOT single-pass backward: gradient not bf16 channels_last")
+    need_res = ctx.has_res and ctx.needs_input_grad[4]
+    dy, dres = _bn_bwd_dual(dout, dpre, y, res, stats, gamma, beta, M, C, act, need_res,
+                            getattr(ctx, "bnlink", None), None, None)
+    dyf = dual_full(dy)
+    dx = None
+    if ctx.needs_input_grad[0]:
+        full, dx = dual_alloc((N, C, H, W), torch.bfloat16, dev)
+        _ext.call("mda_dw_dgrad", dyf, wp, full, 2 * N, H, W, C, Ho, Wo, 3, 3, stride, pad)
+    if ctx.needs_input_grad[1]:
+        if weight.grad is None or not weight.grad.is_contiguous():
+            raise RuntimeError("DOT single-pass backward: conv weights need bound flat gradients")
+        nblk = _dw_wgrad_blocks(N, H, W, C, Ho, Wo, stride, pad)
+        for k in (0, 1):
+            part = torch.empty(nblk * 9 * C, dtype=torch.float32, device=dev)
+            dyk = dyf[k * N:(k + 1) * N]
+            tgt = dual_ptr(weight.grad, k)
+            if _WG_DEFER[0] is not None:
+                _ext.call("mda_dw_wgrad", x, dyk, part, None, N, H, W, C, Ho, Wo, 3, 3, stride,
+                          pad, nblk, 1)
+                _WG_DEFER[0].append([part.data_ptr(), tgt, nblk, C, 1, 3, 3, 0, 1, 0, -1])
+                _WG_KEEP.append(part)
+            else:
+                _ext.call("mda_dw_wgrad", x, dyk, part, tgt, N, H, W, C, Ho, Wo, 3, 3, stride,
+                          pad, nblk, 1)
+        notify_grad(weight)
+    notify_grad(gamma, beta)
+    return dx, None, None, None, dres, None, None, None, None, _cbias_grad(ctx), None, None
 
 
 def _cbias_grad(ctx):

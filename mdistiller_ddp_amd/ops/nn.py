@@ -450,13 +450,26 @@ class _PoolFC(torch.autograd.Function):
         return dx, None, None
 
 
-def _pool_fc_native(x: torch.Tensor, fc: nn.Linear, kernel) -> bool:
+def _fc_dims(fc):
+    """(in, out) of a classifier: an ``nn.Linear`` or a 1 x 1 ``nn.Conv2d`` on
+    the pooled map (Tiny-ImageNet MobileNetV2's head); None otherwise."""
+    if isinstance(fc, nn.Linear):
+        return fc.in_features, fc.out_features
+    if (isinstance(fc, nn.Conv2d) and fc.kernel_size == (1, 1) and fc.groups == 1
+            and fc.stride == (1, 1) and fc.padding in ((0, 0), 0)):
+        return fc.in_channels, fc.out_channels
+    return None
+
+
+def _pool_fc_native(x: torch.Tensor, fc, kernel) -> bool:
     if not (x.dim() == 4 and hip_enabled_for(x)):
         return False
     N, C, H, W = x.shape
-    if kernel not in (None, H) or H != W or fc.in_features != C or fc.weight.dtype != torch.float32:
+    dims = _fc_dims(fc)
+    if dims is None or kernel not in (None, H) or H != W or dims[0] != C \
+            or fc.weight.dtype != torch.float32:
         return False
-    if C > 8192 or fc.out_features * C > (1 << 24) or N > 16384:
+    if C > 8192 or dims[1] * C > (1 << 24) or N > 16384:
         return False
     if x.dtype == torch.bfloat16:
         return True
@@ -497,14 +510,17 @@ def pool_linear(x: torch.Tensor, fc: nn.Linear, kernel: int | None = None):
                 avg = xf.mean(dim=(2, 3))
             else:
                 avg = F.avg_pool2d(xf, kernel).reshape(x.size(0), -1)
-            return avg, F.linear(avg, fc.weight.float(),
+            return avg, F.linear(avg, fc.weight.float().reshape(fc.weight.shape[0], -1),
                                  fc.bias.float() if fc.bias is not None else None)
     if _pool_fc_native(x, fc, kernel):
+        # (a 1 x 1 conv's [J, C, 1, 1] weight is the same memory as [J, C])
         return _PoolFC.apply(x, fc.weight, fc.bias)
     if kernel is None:
         avg = F.adaptive_avg_pool2d(x, 1).reshape(x.size(0), -1)
     else:
         avg = F.avg_pool2d(x, kernel).reshape(x.size(0), -1)
+    if isinstance(fc, nn.Conv2d):
+        return avg, fc(avg.reshape(avg.size(0), -1, 1, 1)).flatten(1)
     return avg, fc(avg)
 
 

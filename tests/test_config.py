@@ -76,3 +76,13 @@ def test_method_nodes_declared():
     cfg = get_cfg()
     for n in METHOD_NODES:
         assert n in cfg
+
+
+def test_mode_key_accepts_bool_from_command_line():
+    """``RUNTIME.DOT_SINGLE_PASS False`` on the command line: a string mode key
+    (default "auto") takes the boolean as "false" / "true"."""
+    from mdistiller_ddp_amd.config import get_cfg
+    cfg = get_cfg()
+    cfg.merge_from_list(["RUNTIME.DOT_SINGLE_PASS", "False", "RUNTIME.TEACHER_LOOKAHEAD", "True"])
+    assert cfg.RUNTIME.DOT_SINGLE_PASS == "false"
+    assert cfg.RUNTIME.TEACHER_LOOKAHEAD == "true"

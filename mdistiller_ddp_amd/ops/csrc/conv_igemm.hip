@@ -1626,6 +1626,15 @@ bool halo_eligible(ConvParams& p) {
   return halo_geometry(p, p.Cin == BK ? HALO1_PROWS : HALO_PROWS);
 }
 
+// grouped convs: re-pick the N tile width for the group size (MDA_GROUPED_BN=0: off, A/B)
+bool grouped_bn_fit() {
+  static const bool on = [] {
+    const char* e = getenv("MDA_GROUPED_BN");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 bool use_halo1() {
   static const bool on = [] {
     const char* e = getenv("MDA_CONV_HALO1");
@@ -1835,6 +1844,19 @@ int dispatch(ConvParams& p, int mode, int64_t tile, int64_t splits, hipStream_t 
   p.w_bytes = (int)wb;
   if (tile == 0 || splits == 0) mda_conv_plan(p.M, p.Cout, p.Kp, &tile, &splits);
   if (splits > 1 && p.partial == nullptr) return (int)hipErrorInvalidValue;
+  if (p.cout_g < p.Cout && grouped_bn_fit()) {
+    // group-aligned N tiles: the tile width that pads a group least (the
+    // plan's width is chosen for the whole Cout).  ShuffleNetV1's groups of
+    // 24 / 72 / 80 / 160 channels waste 25-62 % of a 64 / 128-wide tile.
+    const int cg = p.cout_g;
+    int best = (int)(tile % 1000), best_pad = (cg + best - 1) / best * best;
+    for (int bn : {128, 64, 32}) {
+      const int pad = (cg + bn - 1) / bn * bn;
+      if (pad * 8 <= cg * 9) { best = bn; best_pad = pad; break; }  // <= 12.5 % padding
+      if (pad < best_pad) { best = bn; best_pad = pad; }
+    }
+    tile = tile / 1000 * 1000 + best;
+  }
   int rc;
   if (p.x2 != nullptr && (halo || p.par <= 1 || splits != 1 || p.cin2 % BK || p.cls2 < 0 ||
                           p.cls2 >= p.par * p.par))

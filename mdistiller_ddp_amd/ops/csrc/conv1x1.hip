@@ -75,6 +75,9 @@ __device__ __forceinline__ void conv1x1_body(const S1Params& p, char* smem, int 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int q = lane >> 4, r16 = lane & 15;
   const int ch0 = by * (64 * CI) + wid * (16 * CI);   // this wave's first channel
+  // Cout % 64 == 32 (CI == 1): the last channel slice's upper two waves have no
+  // channels -- they still stage X tiles, but multiply and store nothing
+  const bool live = ch0 < p.Cout;
 
   // resident A fragments: W[ch0 + 16 ci + r16][32 kk + 8 q .. + 8]
   bf16x8 af[CI][KK];
@@ -82,7 +85,8 @@ __device__ __forceinline__ void conv1x1_body(const S1Params& p, char* smem, int 
   for (int ci = 0; ci < CI; ++ci)
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk)
-      af[ci][kk] = *(const bf16x8*)(p.w + (int64_t)(ch0 + 16 * ci + r16) * p.Kp + 32 * kk + 8 * q);
+      af[ci][kk] = live ? *(const bf16x8*)(p.w + (int64_t)(ch0 + 16 * ci + r16) * p.Kp + 32 * kk + 8 * q)
+                        : (bf16x8){};
   // this lane's output channels: ch0 + 16 ci + 4 q + e
   float sc[CI][4], bi[CI][4];
 #pragma unroll
@@ -90,8 +94,8 @@ __device__ __forceinline__ void conv1x1_body(const S1Params& p, char* smem, int 
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int c = ch0 + 16 * ci + 4 * q + e;
-      sc[ci][e] = p.scale ? p.scale[c] : 1.f;
-      bi[ci][e] = p.bias ? p.bias[c] : 0.f;
+      sc[ci][e] = (p.scale && live) ? p.scale[c] : 1.f;
+      bi[ci][e] = (p.bias && live) ? p.bias[c] : 0.f;
     }
   float s1[CI][4], s2[CI][4];
 #pragma unroll
@@ -165,7 +169,7 @@ __device__ __forceinline__ void conv1x1_body(const S1Params& p, char* smem, int 
 #pragma unroll
       for (int pj = 0; pj < 4; ++pj) {
         const int m = t * S_BM + 16 * pj + r16;
-        if (m >= p.M) continue;
+        if (m >= p.M || !live) continue;
 #pragma unroll
         for (int ci = 0; ci < CI; ++ci) {
           const int c = ch0 + 16 * ci + 4 * q;
@@ -204,7 +208,7 @@ __device__ __forceinline__ void conv1x1_body(const S1Params& p, char* smem, int 
     }
   }
 done:
-  if (p.slot != nullptr) {
+  if (p.slot != nullptr && live) {
     // the 16 lanes of a quad group hold the same channels: reduce over r16,
     // then one fp64 atomic per channel and block into shard blockIdx % SH
 #pragma unroll
@@ -263,7 +267,7 @@ int cus() {
 
 template <int CI, int KK>
 int launch_ci(const S1Params& p, hipStream_t st, const FwdApply* fa) {
-  const int ny = p.Cout / (64 * CI);
+  const int ny = (p.Cout + 64 * CI - 1) / (64 * CI);
   // persistent: about two resident blocks per CU over all channel tiles
   int gx = (2 * cus() + ny - 1) / ny;
   if (gx > p.ntiles) gx = p.ntiles;
@@ -287,14 +291,14 @@ int launch_kk(const S1Params& p, hipStream_t st, const FwdApply* fa) {
     if (p.Cout % 256 == 0) return launch_ci<4, KK>(p, st, fa);
   }
   if (p.Cout % 128 == 0) return launch_ci<2, KK>(p, st, fa);
-  if (p.Cout % 64 == 0) return launch_ci<1, KK>(p, st, fa);
+  if (p.Cout % 32 == 0) return launch_ci<1, KK>(p, st, fa);  // (Cout % 64 == 32: half-live slice)
   return (int)hipErrorInvalidValue;
 }
 
 }  // namespace
 
 // Eligibility + launch (host side of conv_igemm.hip's dispatch): 1x1, pad 0,
-// dense, K a multiple of 32 up to 256 (weight rows Kp >= K), Cout % 64 == 0, stride 1 (or 2
+// dense, K a multiple of 32 up to 256 (weight rows Kp >= K), Cout % 32 == 0, stride 1 (or 2
 // for a forward), large M.  Returns -1 when the shape is not served.
 static int conv1x1_try(const void* x, const void* w, const float* scale, const float* bias,
                        const void* res, void* y, void* preact, void* slot, int64_t N, int64_t H,
@@ -310,7 +314,11 @@ static int conv1x1_try(const void* x, const void* w, const float* scale, const f
     return e ? (int64_t)atoll(e) : (int64_t)16384;
   }();
   const int64_t M = N * Ho * Wo;
-  if (!on || Kp < K || K % 32 || K > 256 || Cout % 64 ||
+  static const int cmod = [] {
+    const char* e = getenv("MDA_CONV1X1_C32");  // 0: Cout % 64 only (A/B)
+    return (e && e[0] == '0') ? 64 : 32;
+  }();
+  if (!on || Kp < K || K % 32 || K > 256 || Cout % cmod ||
       M < (min_m_override > 0 ? min_m_override : min_m) || (stride != 1 && stride != 2))
     return -1;
   if (N * H * W * K >= ((int64_t)1 << 31) || M * Cout >= ((int64_t)1 << 31)) return -1;

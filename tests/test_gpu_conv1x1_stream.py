@@ -2,7 +2,7 @@
 stores straight from the accumulators) vs PyTorch fp32: inference epilogue
 (folded BN, residual, activation, pre-activation), the training forward with
 BN batch statistics, and the stride-1 dgrad.  Shapes cover K = 32 / 64 / 96 / 128 / 192 /
-256, 64 / 128 / 256-channel slices, stride 2 and an M tail."""
+256, 64 / 128 / 256-channel slices (and half-live 32-channel ones), stride 2 and an M tail."""
 import pytest
 import torch
 import torch.nn as nn
@@ -22,6 +22,9 @@ SHAPES = [  # N, Cin, H, Cout, stride
     (8, 32, 112, 64, 1),    # K = 32 on 64-padded weight rows (MobileNetV1's first pointwise)
     (8, 96, 40, 128, 1),    # K = 96 (Kp = 128)
     (8, 64, 40, 96, 1),     # dgrad K = 96 (LOAD_DGRAD_VEC8 mode reaches the stream kernel)
+    (8, 64, 48, 32, 1),     # Cout = 32: one half-live 64-channel slice
+    (8, 192, 32, 96, 1),    # Cout = 96: a full and a half-live slice
+    (16, 64, 32, 160, 2),   # Cout = 160, stride 2
 ]
 
 
@@ -82,7 +85,8 @@ def test_stream_train_forward_stats_and_dgrad(shape):
 
 
 @pytest.mark.parametrize("shape", [(16, 256, 56, 64), (8, 128, 28, 256), (3, 64, 99, 128),
-                                   (8, 64, 40, 96), (8, 64, 112, 32)])
+                                   (8, 64, 40, 96), (8, 64, 112, 32), (64, 32, 32, 64),
+                                   (16, 96, 32, 64)])
 def test_stream_dgrad(shape):
     """dx = dgrad(dy) of a stride-1 1x1 conv (the stream kernel with W^T)."""
     N, Cin, H, Cout = shape

@@ -75,3 +75,53 @@ def test_vit_tiny_forward():
         logits, f = m(torch.randn(1, 3, 224, 224))
     assert logits.shape == (1, 1000)
     assert m.get_arch() == "transformer"
+
+
+def test_vgg_and_mv2_fused_forms_match_the_reference_composition():
+    """Round 6 moved VGG's / Tiny-ImageNet MobileNetV2's ReLU(6)s into the
+    producing conv launch (returning the pre-activation too) and their heads
+    onto ``pool_linear``: on the CPU the logits, features, pre-activations and
+    pooled features equal the reference's F.relu / AdaptiveAvgPool2d / Linear
+    composition exactly (reference models/cifar/vgg.py, mv2_tinyimagenet.py)."""
+    import copy
+    import torch.nn.functional as F
+    from mdistiller_ddp_amd.models._seq import run_seq
+    from mdistiller_ddp_amd.models.cifar import vgg
+    from mdistiller_ddp_amd.models.cifar.mv2_tinyimagenet import mobilenetv2_tinyimagenet
+    torch.manual_seed(0)
+    m = vgg.vgg8_bn(num_classes=100).train()
+    ref = copy.deepcopy(m)
+    x = torch.randn(2, 3, 32, 32)
+    logits, d = m(x)
+    h, p0 = run_seq(ref.block0, x, want_preact=True)
+    h = F.relu(h)
+    feats, pres = [h], [p0]
+    for i, (pool, block) in enumerate(((ref.pool0, ref.block1), (ref.pool1, ref.block2),
+                                        (ref.pool2, ref.block3), (ref.pool3, ref.block4))):
+        if i < 3 or h.shape[-1] > 4:
+            h = pool(h)
+        h, _ = run_seq(block, h)
+        pres.append(h)
+        h = F.relu(h)
+        feats.append(h)
+    avg = ref.pool4(h).reshape(2, -1)
+    assert torch.equal(logits, ref.classifier(avg)) and torch.equal(d["pooled_feat"], avg)
+    assert all(torch.equal(a, b) for a, b in zip(d["feats"], feats))
+    assert all(torch.equal(a, b) for a, b in zip(d["preact_feats"], pres))
+
+    m = mobilenetv2_tinyimagenet(num_classes=200).train()
+    ref = copy.deepcopy(m)
+    x = torch.randn(2, 3, 64, 64)
+    logits, d = m(x)
+    f0 = run_seq(ref.pre, x)[0]
+    h = ref.stage1(F.relu6(f0))
+    f1 = ref.stage2(h)
+    f2 = ref.stage3(F.relu6(f1))
+    f3 = ref.stage4(F.relu6(f2))
+    h = ref.stage7(ref.stage6(ref.stage5(F.relu6(f3))))
+    f4 = run_seq(ref.conv1, h)[0]
+    avg = F.adaptive_avg_pool2d(f4, 1)
+    assert torch.equal(logits, ref.conv2(avg).flatten(1))
+    assert torch.equal(d["pooled_feat"], avg.flatten(1))
+    assert all(torch.equal(a, F.relu6(b)) for a, b in zip(d["feats"], (f0, f1, f2, f3, f4)))
+    assert all(torch.equal(a, b) for a, b in zip(d["preact_feats"], (f0, f1, f2, f3, f4)))
